@@ -1,0 +1,283 @@
+"""Benchmark: Lightweight3DUNet training throughput on MI355X (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[1]): 16->32->64->128 U-Net, 48^3 patches,
+batch 4 per GPU, fp32, dropout 0.1, FocalTversky(0.7, 0.3, 0.75), AdamW(lr 1e-4, wd 1e-5).
+A step = forward + loss + backward + optimizer (trainer.py:222-232) over one synthetic batch,
+replayed from a hipGraph; inputs are generated on the host before timing and are resident in HBM
+(a pool of 8 distinct batches, copied device-to-device into the graph's input buffers inside the
+timed step).  N > 1: one process per GPU (torch.distributed.run), exact global-batch FocalTversky
+(3-float all-reduce) + one flat-gradient RCCL all-reduce per step; per-GPU batch fixed (weak
+scaling); time = max over ranks.
+
+Also reported: eval forward ms/patch (bs 1 and 4), the roofline of the dominant kernel measured
+live with HIP events around its launches, and the CPU baseline (the torch-CPU oracle restatement
+of the same network on this host's cores, rank 0 only, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "light-3d-unet-front_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "train patches/sec (48³, bs=4/GPU) at 1/2/4/8 MI355X + fwd ms/patch"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--size", type=int, default=48)
+    ap.add_argument("--enc", type=str, default="16,32,64,128")
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--ftl-mode", default="exact", choices=["exact", "local"])
+    return ap.parse_args()
+
+
+def synthetic_pool(n_pool, bs, size, rank, device):
+    xs, ts = [], []
+    for i in range(n_pool):
+        rng = np.random.default_rng(42 + 1000 * rank + i)
+        x = rng.random((bs, 1, size, size, size), dtype=np.float32)
+        t = (rng.random((bs, 1, size, size, size)) > 0.97).astype(np.float32)
+        xs.append(torch.from_numpy(x).to(device))
+        ts.append(torch.from_numpy(t).to(device))
+    return xs, ts
+
+
+def dw_bytes(N, C, S):
+    """Algorithmic HBM bytes of one fused depthwise backward launch:
+    read dZ + read X + write dX (fp32) + 27 weights."""
+    return 4 * (3 * N * C * S) + 4 * 27 * C
+
+
+class KernelTimer:
+    """Records HIP events around every launch of one C-ABI entry point (on the launch stream)."""
+
+    def __init__(self, name, match):
+        self.name, self.match, self.events = name, match, []
+
+    def wrap(self, nat):
+        orig = nat.call
+
+        def call(name, *args):
+            if name == self.name and self.match(args):
+                s = torch.cuda.current_stream()
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                orig(name, *args)
+                e1.record(s)
+                self.events.append((e0, e1))
+            else:
+                orig(name, *args)
+        nat.call = call
+        return orig
+
+    def mean_ms(self):
+        return float(np.mean([a.elapsed_time(b) for a, b in self.events])) if self.events else None
+
+
+def cpu_baseline(args, enc):
+    """The oracle (torch-CPU restatement of the same network, fp32) on the host cores."""
+    from oracle import unet_oracle as U
+    from light_unet.engine import param_layout
+    torch.set_num_threads(max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))))
+    g = torch.Generator().manual_seed(0)
+    sd = {}
+    for name, shape in param_layout(enc):
+        sd[name] = (torch.randn(shape, generator=g) * 0.1).requires_grad_(True)
+    opt = torch.optim.AdamW(list(sd.values()), lr=1e-4, weight_decay=1e-5)
+    rng = np.random.default_rng(42)
+    bs, size = args.batch, args.size
+    x = torch.from_numpy(rng.random((bs, 1, size, size, size), dtype=np.float32))
+    t = torch.from_numpy((rng.random((bs, 1, size, size, size)) > 0.97).astype(np.float32))
+
+    def step():
+        out = U.unet_forward(sd, x)
+        loss = U.focal_tversky(out, t)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    step()
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(args.cpu_steps * bs / dt, 3), "unit": "patches/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{args.cpu_steps} train steps (fwd+FocalTversky+bwd+AdamW, dropout 0) of "
+                      f"bs={bs} {size}^3 fp32 after 1 warm-up, oracle/unet_oracle.py (aten CPU)",
+            "ms_per_step": round(1000 * dt / args.cpu_steps, 1)}
+
+
+def fwd_ms_per_patch(model, bs, size, device, iters=20):
+    x = torch.rand(bs, 1, size, size, size, device=device)
+    model.eval()
+    with torch.no_grad():
+        for _ in range(3):
+            model(x)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            model(x)
+        torch.cuda.current_stream().wait_stream(s)
+        with torch.cuda.graph(g):
+            model(x)
+        g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            g.replay()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    model.train()
+    return 1000 * dt / iters / bs
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} needs torchrun with {args.gpus} processes "
+                         f"(WORLD_SIZE={world})")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    enc = tuple(int(c) for c in args.enc.split(","))
+
+    from light_unet import _native as nat
+    from light_unet.models.unet3d import Lightweight3DUNet
+    from light_unet.train_step import TrainStep
+
+    torch.manual_seed(42)
+    model = Lightweight3DUNet(encoder_channels=list(enc), dropout_p=args.dropout).to(device).train()
+    if world > 1:   # identical initial weights on every rank (DDP semantics)
+        dist.broadcast(model.flat_parameters(), 0)
+    step = TrainStep(model, {"alpha": 0.7, "beta": 0.3, "gamma": 0.75}, lr=1e-4, weight_decay=1e-5,
+                     ftl_mode=args.ftl_mode)
+    xs, ts = synthetic_pool(8, args.batch, args.size, rank, device)
+    x_static, t_static = xs[0].clone(), ts[0].clone()
+
+    # roofline leg (eager, instrumented): HIP events around the dominant kernel's launches
+    N, S = args.batch, args.size ** 3
+    cdom = 2 * enc[0]      # up3.res_block conv1.depthwise: [N, 2*c0, D^3] fused backward
+    timer = KernelTimer("l3u_dw3_bwd", lambda a: a[-5] == cdom and a[-4] == args.size)
+    orig = timer.wrap(nat)
+    for i in range(3):
+        step(xs[i % 8], ts[i % 8])
+    torch.cuda.synchronize()
+    timer.events.clear()
+    for i in range(max(5, min(args.steps, 20))):
+        step(xs[i % 8], ts[i % 8])
+    torch.cuda.synchronize()
+    dom_ms = timer.mean_ms()
+    nat.call = orig
+
+    if args.no_graph:
+        def run(i):
+            return step(xs[i % 8], ts[i % 8])
+    else:
+        step.capture(x_static, t_static, warmup=2)
+
+        def run(i):
+            x_static.copy_(xs[i % 8], non_blocking=True)
+            t_static.copy_(ts[i % 8], non_blocking=True)
+            return step.replay()
+
+    for i in range(args.warmup):
+        run(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = run(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    final_loss = float(loss.item())
+    if not np.isfinite(final_loss):
+        raise SystemExit(f"non-finite loss {final_loss}")
+
+    fwd1 = fwd_ms_per_patch(model, 1, args.size, device) if rank == 0 else None
+    fwd4 = fwd_ms_per_patch(model, args.batch, args.size, device) if rank == 0 else None
+    out = None
+    if rank == 0:
+        patches = world * args.batch * args.steps
+        value = patches / elapsed
+        dbytes = dw_bytes(N, cdom, S)
+        achieved = dbytes / (dom_ms * 1e-3) / 1e9 if dom_ms else None
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "patches/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (x~U[0,1), target Bernoulli(0.03); random-init weights, seed 42)",
+            "config": {"workload": f"Lightweight3DUNet {'->'.join(map(str, enc))} train step "
+                                   f"(fwd+FocalTversky+bwd+AdamW), {args.size}^3 patches",
+                       "batch_per_gpu": args.batch, "global_batch": args.batch * world,
+                       "patch": [args.size] * 3, "dropout_p": args.dropout,
+                       "ftl_mode": args.ftl_mode,
+                       "parallelism": f"dp{world}" if world > 1 else "single",
+                       "graph": not args.no_graph},
+            "fwd_ms_per_patch": {"bs1": round(fwd1, 4), f"bs{args.batch}": round(fwd4, 4)},
+            "final_loss": round(final_loss, 6),
+            "roofline": {
+                "kernel": f"l3u_dw3_bwd [{N},{cdom},{args.size}^3] (up3.res_block.conv1.depthwise "
+                          "fused data+weight backward)",
+                "bound": "hbm",
+                "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": None,
+                "algorithmic_bytes": dbytes,
+                "avg_launch_ms": round(dom_ms, 5) if dom_ms else None,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, enc)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,169 @@
+/*
+ * l3u.h — C ABI of the MI355X (gfx950) hot path of the Light-3D-U-Net
+ *         (Lightweight3DUNet training / inference step + FocalTverskyLoss).
+ *
+ * Library: light-3d-unet-front_amd/lib/libl3u_hip.so  (built by `make` in that directory).
+ *
+ * Conventions (every entry point):
+ *   - plain device pointers + sizes, no framework types; the caller owns all memory, nothing is
+ *     allocated inside, so every call is hipGraph-capturable;
+ *   - the last argument is the hipStream_t to enqueue on; calls are asynchronous;
+ *   - the return value is a hipError_t as int (0 = hipSuccess; hipErrorInvalidValue for a shape
+ *     the kernels do not support, e.g. an H*W plane above 4096 voxels for the stencil);
+ *   - activations are fp32 NCDHW with the spatial volume S = D*H*W contiguous per (n, c); a tensor
+ *     is (pointer, batch stride in elements) — channel stride is always S.  A batch stride larger
+ *     than C*S addresses one channel range of a concatenation buffer (zero-copy torch.cat);
+ *   - "rec" is the per-(n,c) InstanceNorm record of 8 floats:
+ *       {mean, rstd, scale = k*gamma*rstd, shift = k*beta, k, gamma, beta, 0}
+ *     and the normalised, activated value is lrelu(scale*(y - mean) + shift)
+ *     with k the Dropout3d keep scale (0 or 1/(1-p); 1 without dropout);
+ *   - partial-sum buffers are reduced in a fixed order (l3u_reduce_segments), so results are
+ *     bitwise run-to-run reproducible.
+ *
+ * The reference (xxxxxxyp/Light-3D-Unet-Front) is pure Python/PyTorch: it has no native FFI.  Each
+ * entry point below names the reference module call it replaces (file:line in the reference);
+ * the Python host mirror (light_unet/) binds them through ctypes.
+ */
+#ifndef L3U_H
+#define L3U_H
+
+#include <hip/hip_runtime.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int l3u_abi_version(void);
+
+/* ---- depthwise 3x3x3 conv, stride 1, padding 1, no bias ------------------------------------
+ * replaces nn.Conv3d(C, C, 3, 1, 1, groups=C, bias=False)
+ *          (DepthwiseSeparableConv3d.depthwise, light_unet/models/unet3d.py:16-17, forward :21)
+ * w: [C][27].  rec != NULL fuses a = lrelu(scale*(x-mean) + shift) into the input load (the
+ * InstanceNorm1 + LeakyReLU + Dropout3d that precede conv2.depthwise, unet3d.py:84-89).      */
+int l3u_dw3_nchunk(int D);
+int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float* rec, float* y,
+                long long y_nstride, int N, int C, int D, int H, int W, hipStream_t stream);
+/* fused backward (autograd of the same module): dx = conv^T(dz) (accumulate != 0: dx += ...),
+ * dw_part[C][N*nchunk][27] partial weight gradients.  rec != NULL: dx receives
+ * dpre = dA * k * lrelu'(pre) and in_part[C][N][nchunk][2] (fp64) = {sum dpre, sum dpre*xhat}.*/
+int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
+                const float* w, const float* rec, float* dx, long long dx_nstride, int accumulate,
+                float* dw_part, double* in_part, int N, int C, int D, int H, int W,
+                hipStream_t stream);
+
+/* ---- channel-contraction GEMM on MFMA (v_mfma_f32_16x16x4_f32) ------------------------------
+ * Y[n][j][s] = sum_k Wm[j][k] X[n][k][s] (+ bias[j]) (+ Y if accumulate)
+ * w_layout 0: Wm[j][k] = w[j*K + k]   (torch Conv3d 1x1 weight [Co][Ci]: forward)
+ * w_layout 1: Wm[j][k] = w[k*Nout + j] (transposed: backward-data of a 1x1 conv, and
+ *                                       ConvTranspose3d weight [Ci][Co*8])
+ * replaces nn.Conv3d(Ci, Co, 1, bias=False)  (DepthwiseSeparableConv3d.pointwise, unet3d.py:18;
+ *          shortcut conv unet3d.py:70-73; out_conv unet3d.py:201) and the GEMM of
+ *          nn.ConvTranspose3d(Ci, Ci//2, 2, 2) (unet3d.py:119).
+ * stat_part != NULL: emits InstanceNorm partials [N][Nout][l3u_pw_stat_nsb][3] = (count, mean, M2)
+ * of the output for the nn.InstanceNorm3d that follows (unet3d.py:51,62,72).                  */
+int l3u_pw_stat_nsb(int Nout, int S);
+int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout,
+               const float* bias, float* y, long long y_nstride, int accumulate,
+               float* stat_part, int N, int K, int Nout, int S, hipStream_t stream);
+/* weight gradient partials: part[N*nsc][J][K] = sum_s dY[n][j][s] X[n][k][s] per voxel chunk   */
+int l3u_pw_bwd_weight_nparts(int N, int S);
+int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
+                      float* part, int N, int J, int K, int S, hipStream_t stream);
+
+/* ---- InstanceNorm3d(affine=True, eps=1e-5) + LeakyReLU(0.01) + Dropout3d + residual --------
+ * replaces nn.InstanceNorm3d / nn.LeakyReLU / nn.Dropout3d / "out + residual"
+ *          (ResidualBlock.forward, unet3d.py:77-93)
+ * in_finalize: merge (count, mean, M2) partials -> rec; drop_p > 0 draws the Dropout3d channel
+ * mask from a counter hash of (seed, *step, layer, n, c) (graph-replay safe).               */
+int l3u_in_finalize(const float* stat_part, int nsb, const float* gamma, const float* beta,
+                    float drop_p, unsigned long long seed, const int* step, int layer, float* rec,
+                    int N, int C, hipStream_t stream);
+/* block output: out = lrelu(scale2*(y2-mean2) + shift2 + R), R = r (rec_r == NULL, nn.Identity
+ * shortcut) or scale_r*(r-mean_r) + shift_r (Conv1x1 + InstanceNorm shortcut)                        */
+int l3u_norm_act_nblocks(int S);
+int l3u_norm_act_fwd(const float* y2, long long y2_nstride, const float* rec2, const float* r,
+                     long long r_nstride, const float* rec_r, float* out, long long out_nstride,
+                     int N, int C, int S, hipStream_t stream);
+/* backward of the block tail: part[C][N][nblocks][3] (fp64) = {sum g, sum g*xhat2, sum g*xhat_r},
+ * g = dout * lrelu'(out); then dy2 / dr (dr = g for the identity shortcut)                   */
+int l3u_norm_act_bwd_reduce(const float* dout, long long dout_nstride, const float* out,
+                            long long out_nstride, const float* y2, long long y2_nstride,
+                            const float* rec2, const float* r, long long r_nstride,
+                            const float* rec_r, double* part, int N, int C, int S,
+                            hipStream_t stream);
+int l3u_norm_act_bwd_apply(const float* dout, long long dout_nstride, const float* out,
+                           long long out_nstride, const float* y2, long long y2_nstride,
+                           const float* rec2, const float* r, long long r_nstride,
+                           const float* rec_r, const double* part, float* dy2,
+                           long long dy2_nstride, float* dr, long long dr_nstride, int N, int C,
+                           int S, hipStream_t stream);
+/* inner InstanceNorm backward: dy = rstd*gamma*(dpre - mean(dpre) - xhat*mean(dpre*xhat))     */
+int l3u_in_bwd_apply(const float* dpre, long long dpre_nstride, const float* y, long long y_nstride,
+                     const float* rec, const double* in_part, int npart, float* dy,
+                     long long dy_nstride, int N, int C, int S, hipStream_t stream);
+
+/* ---- MaxPool3d(2, 2) (DownBlock.pool, unet3d.py:101, forward :109) ------------------------
+ * idx: uint8 [N][C][So] argmax slot (first max in (dz,dy,dx) order, as torch CPU)
+ * bwd: dx = route(dy) + add (add may be NULL) — writes every input voxel                      */
+int l3u_maxpool2_fwd(const float* x, long long x_nstride, float* y, long long y_nstride,
+                     unsigned char* idx, int N, int C, int D, int H, int W, hipStream_t stream);
+int l3u_maxpool2_bwd(const float* dy, long long dy_nstride, const unsigned char* idx,
+                     const float* add, long long add_nstride, float* dx, long long dx_nstride,
+                     int N, int C, int D, int H, int W, hipStream_t stream);
+
+/* ---- ConvTranspose3d(Ci, Co, 2, 2) scatter halves (UpBlock.up, unet3d.py:119, forward :127) -
+ * GEMM half = l3u_pw_fwd(w_layout=1, Nout=Co*8) into yp[N][Co*8][S_in];
+ * d2s: out[n][co][2z+a][2y+b][2x+c] = yp[n][co*8+4a+2b+c][z][y][x] + bias[co]  (D,H,W = input dims)
+ * s2d: the inverse permutation (backward)                                                     */
+int l3u_convt_d2s(const float* yp, const float* bias, float* out, long long out_nstride, int N,
+                  int Co, int D, int H, int W, hipStream_t stream);
+int l3u_convt_s2d(const float* dy, long long dy_nstride, float* dyp, int N, int Co, int D, int H,
+                  int W, hipStream_t stream);
+/* per-channel sums part[C][N][nblocks] (fp64; bias gradients)                                */
+int l3u_chan_sum_nblocks(long long S);
+int l3u_chan_sum(const float* x, long long x_nstride, double* part, int N, int C, long long S,
+                 hipStream_t stream);
+
+/* ---- out_conv (1x1x1, C->1, bias) + Sigmoid (unet3d.py:201-202, forward :220-221) ----------
+ * bwd: dz = dp*p*(1-p); dh[c] = w[c]*dz; part[N*nblocks][C+1] (fp64) = {sum dz*h[c].., sum dz}*/
+int l3u_outconv_nblocks(int S);
+int l3u_outconv_fwd(const float* h, long long h_nstride, const float* w, const float* b, float* p,
+                    int N, int C, int S, hipStream_t stream);
+int l3u_outconv_bwd(const float* dp, const float* p, const float* h, long long h_nstride,
+                    const float* w, float* dh, long long dh_nstride, double* part, int N, int C,
+                    int S, hipStream_t stream);
+
+/* ---- FocalTverskyLoss (light_unet/models/losses.py:11-54) ----------------------------------
+ * sums = {sum p*t, sum p, sum t} over ALL voxels of the batch (pred.view(-1), losses.py:40-46),
+ * reduced in double; loss = (1 - TI)^gamma; bwd writes dL/dp (* gscale[0] if given) or, with
+ * through_sigmoid, dL/dz = dL/dp * p(1-p).  Under data parallelism the 3 sums are all-reduced
+ * between l3u_ftl_sums and l3u_ftl_loss/bwd (exact global-batch semantics).                  */
+int l3u_ftl_nblocks(long long numel);
+int l3u_ftl_sums(const float* p, const float* t, long long numel, float* part, double* sums,
+                 hipStream_t stream);
+int l3u_ftl_loss(const double* sums, double alpha, double beta, double gamma, double smooth,
+                 float* loss, hipStream_t stream);
+int l3u_ftl_bwd(const float* p, const float* t, long long numel, const double* sums, double alpha,
+                double beta, double gamma, double smooth, const float* gscale,
+                int through_sigmoid, float* g, hipStream_t stream);
+
+/* ---- AdamW on the flat parameter buffer (torch.optim.AdamW, trainer.py:75-79) -------------
+ * lr and step live on the device (graph-replay safe); the call increments *step.             */
+int l3u_adamw(float* p, const float* g, float* m, float* v, long long numel, const float* lr,
+              float beta1, float beta2, float eps, float weight_decay, int* step, float grad_scale,
+              hipStream_t stream);
+
+/* ---- deterministic second-stage reduction --------------------------------------------------
+ * items[nitems][8] int64 = {src_off, count, istride, tstride, len<=256, dst_off, accumulate, f64}:
+ * dst[dst_off+t] (+)= sum_{i<count} src[src_off + i*istride + t*tstride], summed in fp64;
+ * f64 != 0: the source is fp64 and offsets/strides count doubles from the same base.         */
+int l3u_reduce_segments(const float* src, const long long* items, int nitems, float* dst,
+                        hipStream_t stream);
+
+/* device counter += value (Dropout3d RNG stream position, advanced once per training forward) */
+int l3u_counter_add(int* counter, int value, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* L3U_H */

@@ -1,0 +1,90 @@
+// Shared device helpers for the Light-3D-U-Net gfx950 kernels.
+// Layout convention: every activation is NCDHW fp32 with the spatial volume
+// S = D*H*W contiguous per (n, c); a tensor view is (base pointer, batch stride in elements).
+// Channel stride is always S.  A batch stride larger than C*S lets a kernel read/write one
+// channel range of a concatenation buffer in place (zero-copy torch.cat, unet3d.py:141).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "l3u.h"
+
+#define L3U_DEV __device__ __forceinline__
+
+namespace l3u {
+
+constexpr float kSlope = 0.01f;   // LeakyReLU(0.01)   unet3d.py:52,63
+constexpr float kEps = 1e-5f;     // InstanceNorm3d eps (torch default)  unet3d.py:51
+
+// Per-(n,c) InstanceNorm record written by in_finalize and read by every consumer.
+//  [0] mean  [1] rstd  [2] scale = k*gamma*rstd  [3] shift = k*beta
+//  [4] k (Dropout3d keep scale: 0 or 1/(1-p); 1 when no dropout)  [5] gamma  [6] beta  [7] 0
+// With the dropout scale folded in, the forward transform is  a = lrelu(scale*(y - mean) + shift),
+// valid because lrelu(k*v) = k*lrelu(v) for k >= 0.  (y - mean) is formed first: folding the mean
+// into the shift cancels catastrophically when |mean| >> std and costs ~1e-5 relative accuracy.
+constexpr int kRec = 8;
+
+L3U_DEV float lrelu(float v) { return v > 0.f ? v : v * kSlope; }
+L3U_DEV float lrelu_d(float pre) { return pre > 0.f ? 1.f : kSlope; }   // torch: x > 0 ? 1 : slope
+
+L3U_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum for 256-thread blocks; every thread gets the result.  `red` >= 4 floats of LDS.
+L3U_DEV float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+L3U_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide fp64 sum for 256-thread blocks (cross-block gradient sums of InstanceNorm backward
+// are cancellation-heavy: they are accumulated and stored in fp64).  `red` >= 4 doubles of LDS.
+L3U_DEV double block_sum256d(double v, double* red) {
+  v = wave_sum_d(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// Chan et al. parallel merge of (count, mean, M2) — deterministic when merged in fixed order.
+L3U_DEV void chan_merge(float& n_a, float& mean_a, float& m2_a, float n_b, float mean_b, float m2_b) {
+  const float n = n_a + n_b;
+  if (n <= 0.f) return;
+  const float d = mean_b - mean_a;
+  const float fb = n_b / n;
+  mean_a = mean_a + d * fb;
+  m2_a = m2_a + m2_b + d * d * n_a * fb;
+  n_a = n;
+}
+
+// XCD-aware block remap (guide §5.5 T1, bijective form): blocks that share halo planes / weight
+// tiles are consecutive in the logical order, and consecutive logical ids land on one XCD.
+L3U_DEV int xcd_remap(int bid, int nblocks) {
+  if (nblocks < 16) return bid;
+  const int xcd = bid & 7, q = nblocks >> 3, r = nblocks & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+}  // namespace l3u
+
+// Error plumbing for the C-ABI: every entry point returns a hipError_t as int.
+#define L3U_CHECK_LAUNCH() return (int)hipGetLastError()
+#define L3U_REQUIRE(cond) \
+  do {                    \
+    if (!(cond)) return (int)hipErrorInvalidValue; \
+  } while (0)

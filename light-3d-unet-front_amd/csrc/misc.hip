@@ -1,0 +1,436 @@
+// Remaining hot-path ops:
+//   maxpool2_fwd/bwd     nn.MaxPool3d(2, 2)                                   unet3d.py:101
+//   convt_d2s / s2d      the scatter half of nn.ConvTranspose3d(k=2, s=2)     unet3d.py:119,127
+//                        (the GEMM half is l3u_pw_fwd with Nout = Co*8)
+//   chan_sum             per-channel sums (bias gradients)
+//   outconv fwd/bwd      out_conv 1x1x1 (+bias) + Sigmoid                      unet3d.py:201-202,220-221
+//   ftl_*                FocalTverskyLoss forward sums / loss / closed-form backward  losses.py:30-54
+//   adamw                torch.optim.AdamW step on the flat parameter buffer     trainer.py:75-79
+//   reduce_segments      deterministic second stage of every split-K / partial reduction
+#include "common.h"
+using namespace l3u;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+// ---------------------------------------------------------------- maxpool 2x2x2 (floor mode)
+__global__ __launch_bounds__(256) void maxpool2_fwd_kernel(
+    const float* __restrict__ x, long long xns, float* __restrict__ y, long long yns,
+    unsigned char* __restrict__ idx, int C, int D, int H, int W) {
+  const int Do = D / 2, Ho = H / 2, Wo = W / 2;
+  const long long So = (long long)Do * Ho * Wo, Si = (long long)D * H * W;
+  const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const float* xp = x + (long long)n * xns + (long long)c * Si;
+  float* yp = y + (long long)n * yns + (long long)c * So;
+  unsigned char* ip = idx + (long long)nc * So;
+  for (long long o = blockIdx.x * 256ll + threadIdx.x; o < So; o += (long long)gridDim.x * 256) {
+    const int ox = (int)(o % Wo), t = (int)(o / Wo), oy = t % Ho, oz = t / Ho;
+    const float* b = xp + ((long long)(2 * oz) * H + 2 * oy) * W + 2 * ox;
+    float best = b[0];
+    int bi = 0;
+    // scan order (dz, dy, dx) and strict '>' (first maximum wins; NaN propagates) as torch CPU
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+      const int dz = j >> 2, dy = (j >> 1) & 1, dx = j & 1;
+      const float v = b[((long long)dz * H + dy) * W + dx];
+      if (v > best || v != v) { best = v; bi = j; }
+    }
+    yp[o] = best;
+    ip[o] = (unsigned char)bi;
+  }
+}
+
+// dx = route(dy) (+ add): every input voxel is written exactly once (covers odd-size tails)
+__global__ __launch_bounds__(256) void maxpool2_bwd_kernel(
+    const float* __restrict__ dy, long long dyns, const unsigned char* __restrict__ idx,
+    const float* __restrict__ add, long long addns, float* __restrict__ dx, long long dxns,
+    int C, int D, int H, int W) {
+  const int Do = D / 2, Ho = H / 2, Wo = W / 2;
+  const long long So = (long long)Do * Ho * Wo, Si = (long long)D * H * W;
+  const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const float* dyp = dy + (long long)n * dyns + (long long)c * So;
+  const unsigned char* ip = idx + (long long)nc * So;
+  const float* ap = add ? add + (long long)n * addns + (long long)c * Si : nullptr;
+  float* dxp = dx + (long long)n * dxns + (long long)c * Si;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < Si; i += (long long)gridDim.x * 256) {
+    const int xx = (int)(i % W), t = (int)(i / W), yy = t % H, zz = t / H;
+    float v = 0.f;
+    const int oz = zz >> 1, oy = yy >> 1, ox = xx >> 1;
+    if (oz < Do && oy < Ho && ox < Wo) {
+      const long long o = ((long long)oz * Ho + oy) * Wo + ox;
+      const int j = ((zz & 1) << 2) | ((yy & 1) << 1) | (xx & 1);
+      if (ip[o] == j) v = dyp[o];
+    }
+    if (ap) v += ap[i];
+    dxp[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------- ConvTranspose3d(k2,s2) scatter
+// Yp[n][co*8 + a*4 + b*2 + c][z][y][x] (+bias[co]) -> out[n][co][2z+a][2y+b][2x+c]
+__global__ __launch_bounds__(256) void convt_d2s_kernel(
+    const float* __restrict__ yp, const float* __restrict__ bias, float* __restrict__ out,
+    long long ons, int Co, int D, int H, int W) {
+  const int D2 = 2 * D, H2 = 2 * H, W2 = 2 * W;
+  const long long So = (long long)D2 * H2 * W2, Si = (long long)D * H * W;
+  const int nc = blockIdx.y, co = nc % Co, n = nc / Co;
+  const float bv = bias ? bias[co] : 0.f;
+  const float* src = yp + ((long long)n * Co * 8 + (long long)co * 8) * Si;
+  float* dst = out + (long long)n * ons + (long long)co * So;
+  for (long long o = blockIdx.x * 256ll + threadIdx.x; o < So; o += (long long)gridDim.x * 256) {
+    const int X = (int)(o % W2), t = (int)(o / W2), Y = t % H2, Z = t / H2;
+    const int par = ((Z & 1) << 2) | ((Y & 1) << 1) | (X & 1);
+    dst[o] = src[par * Si + ((long long)(Z >> 1) * H + (Y >> 1)) * W + (X >> 1)] + bv;
+  }
+}
+
+// dYp[n][co*8+par][s_in] = dy[n][co][...]
+__global__ __launch_bounds__(256) void convt_s2d_kernel(
+    const float* __restrict__ dy, long long dyns, float* __restrict__ dyp, int Co, int D, int H,
+    int W) {
+  const int D2 = 2 * D, H2 = 2 * H, W2 = 2 * W;
+  const long long So = (long long)D2 * H2 * W2, Si = (long long)D * H * W;
+  const int nc = blockIdx.y, co = nc % Co, n = nc / Co;
+  const float* src = dy + (long long)n * dyns + (long long)co * So;
+  float* dst = dyp + ((long long)n * Co * 8 + (long long)co * 8) * Si;
+  for (long long o = blockIdx.x * 256ll + threadIdx.x; o < So; o += (long long)gridDim.x * 256) {
+    const int X = (int)(o % W2), t = (int)(o / W2), Y = t % H2, Z = t / H2;
+    const int par = ((Z & 1) << 2) | ((Y & 1) << 1) | (X & 1);
+    dst[par * Si + ((long long)(Z >> 1) * H + (Y >> 1)) * W + (X >> 1)] = src[o];
+  }
+}
+
+// ---------------------------------------------------------------- per-channel sums
+// part[c][n][blk] = sum over the block's voxel range of x[n][c][:]
+__global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__ x, long long xns,
+                                                       double* __restrict__ part, int N, int C,
+                                                       long long S) {
+  __shared__ double red[4];
+  const int nc = blockIdx.y, c = nc % C, n = nc / C, nb = gridDim.x;
+  const float* xp = x + (long long)n * xns + (long long)c * S;
+  double s = 0.0;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < S; i += (long long)nb * 256) s += xp[i];
+  s = block_sum256d(s, red);
+  if (threadIdx.x == 0) part[((long long)c * N + n) * nb + blockIdx.x] = s;
+}
+
+// ---------------------------------------------------------------- out_conv + sigmoid
+__global__ __launch_bounds__(256) void outconv_fwd_kernel(
+    const float* __restrict__ h, long long hns, const float* __restrict__ w,
+    const float* __restrict__ b, float* __restrict__ p, int C, int S) {
+  const int n = blockIdx.y;
+  const float* hp = h + (long long)n * hns;
+  float* pp = p + (long long)n * S;
+  const float bv = b[0];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256) {
+    float z = bv;
+    for (int c = 0; c < C; ++c) z = fmaf(w[c], hp[(long long)c * S + i], z);
+    pp[i] = 1.f / (1.f + expf(-z));
+  }
+}
+
+// dz = dp * p * (1 - p); dh[c] = w[c] * dz; part[blk][0..C-1] = sum dz*h[c], part[blk][C] = sum dz
+__global__ __launch_bounds__(256) void outconv_bwd_kernel(
+    const float* __restrict__ dp, const float* __restrict__ p, const float* __restrict__ h,
+    long long hns, const float* __restrict__ w, float* __restrict__ dh, long long dhns,
+    double* __restrict__ part, int C, int S) {
+  extern __shared__ double redd[];   // [4][C+1]
+  const int n = blockIdx.y, nb = gridDim.x;
+  const float* hp = h + (long long)n * hns;
+  float* dhp = dh + (long long)n * dhns;
+  float acc[33];
+#pragma unroll
+  for (int c = 0; c < 33; ++c) acc[c] = 0.f;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += nb * 256) {
+    const float pv = p[(long long)n * S + i];
+    const float dz = dp[(long long)n * S + i] * pv * (1.f - pv);
+    acc[32] += dz;
+#pragma unroll
+    for (int c = 0; c < 32; ++c) {
+      if (c < C) {
+        const float hv = hp[(long long)c * S + i];
+        acc[c] = fmaf(dz, hv, acc[c]);
+        dhp[(long long)c * S + i] = w[c] * dz;
+      }
+    }
+  }
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < 33; ++c) {
+    if (c < C || c == 32) {
+      const double r = wave_sum_d((double)acc[c]);
+      if (l == 0) redd[wv * (C + 1) + (c == 32 ? C : c)] = r;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x <= C) {
+    const int t = threadIdx.x;
+    const double r = (redd[t] + redd[(C + 1) + t]) + (redd[2 * (C + 1) + t] + redd[3 * (C + 1) + t]);
+    part[((long long)n * nb + blockIdx.x) * (C + 1) + t] = r;
+  }
+}
+
+// ---------------------------------------------------------------- Focal-Tversky
+// part[blk] = {sum p*t, sum p, sum t}
+__global__ __launch_bounds__(256) void ftl_partials_kernel(const float* __restrict__ p,
+                                                           const float* __restrict__ t,
+                                                           long long numel,
+                                                           float* __restrict__ part) {
+  __shared__ float red[4];
+  float spt = 0.f, sp = 0.f, st = 0.f;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < numel; i += (long long)gridDim.x * 256) {
+    const float pv = p[i], tv = t[i];
+    spt = fmaf(pv, tv, spt);
+    sp += pv;
+    st += tv;
+  }
+  spt = block_sum256(spt, red);
+  sp = block_sum256(sp, red);
+  st = block_sum256(st, red);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x * 3 + 0] = spt;
+    part[blockIdx.x * 3 + 1] = sp;
+    part[blockIdx.x * 3 + 2] = st;
+  }
+}
+
+// sums[0..2] (double) = fixed-order sum of the partials
+__global__ void ftl_sums_kernel(const float* __restrict__ part, int nb, double* __restrict__ sums) {
+  __shared__ double red[3][64];
+  const int l = threadIdx.x;   // 64 threads
+  double a = 0, b = 0, c = 0;
+  for (int i = l; i < nb; i += 64) { a += part[i * 3]; b += part[i * 3 + 1]; c += part[i * 3 + 2]; }
+  red[0][l] = a; red[1][l] = b; red[2][l] = c;
+  __syncthreads();
+  if (l < 3) {
+    double s = 0;
+    for (int i = 0; i < 64; ++i) s += red[l][i];
+    sums[l] = s;
+  }
+}
+
+struct FtlCoef { double loss, A, B; };
+
+L3U_DEV FtlCoef ftl_coef(const double* sums, double alpha, double beta, double gamma, double smooth) {
+  const double tp = sums[0], fp = sums[1] - sums[0], fn = sums[2] - sums[0];
+  const double dn = tp + alpha * fn + beta * fp + smooth;
+  const double ti = (tp + smooth) / dn;
+  const double one_m = 1.0 - ti;
+  FtlCoef r;
+  r.loss = pow(one_m, gamma);
+  const double pre = -gamma * pow(one_m, gamma - 1.0) / (dn * dn);
+  r.A = pre * (dn - (tp + smooth) * (1.0 - alpha));   // t = 1
+  r.B = pre * (-(tp + smooth) * beta);                 // t = 0
+  return r;
+}
+
+__global__ void ftl_loss_kernel(const double* __restrict__ sums, double alpha, double beta,
+                                double gamma, double smooth, float* __restrict__ loss) {
+  const FtlCoef r = ftl_coef(sums, alpha, beta, gamma, smooth);
+  loss[0] = (float)r.loss;
+}
+
+// g_i = gscale * (A t_i + B (1 - t_i)); optionally fused sigmoid backward: g_i *= p_i (1 - p_i)
+__global__ __launch_bounds__(256) void ftl_bwd_kernel(
+    const float* __restrict__ p, const float* __restrict__ t, long long numel,
+    const double* __restrict__ sums, double alpha, double beta, double gamma, double smooth,
+    const float* __restrict__ gscale, int through_sigmoid, float* __restrict__ g) {
+  __shared__ float coef[2];
+  if (threadIdx.x == 0) {
+    const FtlCoef r = ftl_coef(sums, alpha, beta, gamma, smooth);
+    const double s = gscale ? (double)gscale[0] : 1.0;
+    coef[0] = (float)(r.A * s);
+    coef[1] = (float)(r.B * s);
+  }
+  __syncthreads();
+  const float A = coef[0], B = coef[1];
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < numel; i += (long long)gridDim.x * 256) {
+    const float tv = t[i];
+    float v = fmaf(A - B, tv, B);
+    if (through_sigmoid) { const float pv = p[i]; v *= pv * (1.f - pv); }
+    g[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------- AdamW (torch.optim.AdamW)
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    long long numel, const float* __restrict__ lr,
+                                                    float beta1, float beta2, float eps, float wd,
+                                                    const int* __restrict__ step, float gscale) {
+  const float lrv = lr[0];
+  const int t = step[0] + 1;
+  const float bc1 = 1.f - powf(beta1, (float)t);
+  const float bc2s = sqrtf(1.f - powf(beta2, (float)t));
+  const float step_size = lrv / bc1;
+  const float decay = 1.f - lrv * wd;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < numel; i += (long long)gridDim.x * 256) {
+    const float gv = g[i] * gscale;
+    float pv = p[i] * decay;
+    float mv = m[i];
+    mv = mv + (1.f - beta1) * (gv - mv);                 // exp_avg.lerp_(grad, 1 - beta1)
+    const float vv = v[i] * beta2 + (1.f - beta2) * gv * gv;
+    const float denom = sqrtf(vv) / bc2s + eps;
+    pv = pv - step_size * (mv / denom);
+    p[i] = pv;
+    m[i] = mv;
+    v[i] = vv;
+  }
+}
+
+__global__ void step_inc_kernel(int* step) { step[0] += 1; }
+__global__ void counter_add_kernel(int* c, int v) { c[0] += v; }
+
+// ---------------------------------------------------------------- segmented partial reduction
+// item (8 x int64): src_off, count, istride, tstride, len, dst_off, accumulate, unused
+// dst[dst_off + t] (+)= sum_{i<count} src[src_off + i*istride + t*tstride], t < len (<= 256)
+__global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __restrict__ src,
+                                                              const long long* __restrict__ items,
+                                                              float* __restrict__ dst) {
+  const long long* it = items + (long long)blockIdx.x * 8;
+  const int t = threadIdx.x;
+  const int len = (int)it[4];
+  if (t >= len) return;
+  const long long base = it[0] + t * it[3];
+  const long long cnt = it[1], is = it[2];
+  double s = 0.0;
+  if (it[7]) {
+    const double* sd = reinterpret_cast<const double*>(src);
+    for (long long i = 0; i < cnt; ++i) s += sd[base + i * is];
+  } else {
+    for (long long i = 0; i < cnt; ++i) s += src[base + i * is];
+  }
+  float* d = dst + it[5] + t;
+  *d = it[6] ? (float)((double)*d + s) : (float)s;
+}
+
+int grid_for(long long n, int per_block, int cap) {
+  long long b = (n + per_block - 1) / per_block;
+  if (b > cap) b = cap;
+  return b < 1 ? 1 : (int)b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int l3u_maxpool2_fwd(const float* x, long long x_nstride, float* y, long long y_nstride,
+                     unsigned char* idx, int N, int C, int D, int H, int W, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && D >= 2 && H >= 2 && W >= 2);
+  const long long So = (long long)(D / 2) * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(So, 256, 64), N * C), dim3(256), 0, stream,
+                     x, x_nstride, y, y_nstride, idx, C, D, H, W);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_maxpool2_bwd(const float* dy, long long dy_nstride, const unsigned char* idx,
+                     const float* add, long long add_nstride, float* dx, long long dx_nstride,
+                     int N, int C, int D, int H, int W, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && D >= 2 && H >= 2 && W >= 2);
+  const long long Si = (long long)D * H * W;
+  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(Si, 256, 128), N * C), dim3(256), 0, stream,
+                     dy, dy_nstride, idx, add, add_nstride, dx, dx_nstride, C, D, H, W);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_convt_d2s(const float* yp, const float* bias, float* out, long long out_nstride, int N,
+                  int Co, int D, int H, int W, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && Co > 0 && D > 0 && H > 0 && W > 0);
+  const long long So = 8ll * D * H * W;
+  hipLaunchKernelGGL(convt_d2s_kernel, dim3(grid_for(So, 256, 128), N * Co), dim3(256), 0, stream,
+                     yp, bias, out, out_nstride, Co, D, H, W);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_convt_s2d(const float* dy, long long dy_nstride, float* dyp, int N, int Co, int D, int H,
+                  int W, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && Co > 0 && D > 0 && H > 0 && W > 0);
+  const long long So = 8ll * D * H * W;
+  hipLaunchKernelGGL(convt_s2d_kernel, dim3(grid_for(So, 256, 128), N * Co), dim3(256), 0, stream,
+                     dy, dy_nstride, dyp, Co, D, H, W);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_chan_sum_nblocks(long long S) { return grid_for(S, 1024, 64); }
+
+int l3u_chan_sum(const float* x, long long x_nstride, double* part, int N, int C, long long S,
+                 hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && S > 0);
+  hipLaunchKernelGGL(chan_sum_kernel, dim3(grid_for(S, 1024, 64), N * C), dim3(256), 0, stream, x,
+                     x_nstride, part, N, C, S);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_outconv_nblocks(int S) { return grid_for(S, 1024, 128); }
+
+int l3u_outconv_fwd(const float* h, long long h_nstride, const float* w, const float* b, float* p,
+                    int N, int C, int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && C <= 32 && S > 0);
+  hipLaunchKernelGGL(outconv_fwd_kernel, dim3(grid_for(S, 1024, 128), N), dim3(256), 0, stream,
+                     h, h_nstride, w, b, p, C, S);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_outconv_bwd(const float* dp, const float* p, const float* h, long long h_nstride,
+                    const float* w, float* dh, long long dh_nstride, double* part, int N, int C,
+                    int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && C <= 32 && S > 0);
+  hipLaunchKernelGGL(outconv_bwd_kernel, dim3(grid_for(S, 1024, 128), N), dim3(256),
+                     4 * (C + 1) * sizeof(double), stream, dp, p, h, h_nstride, w, dh, dh_nstride,
+                     part, C, S);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_ftl_nblocks(long long numel) { return grid_for(numel, 2048, 512); }
+
+int l3u_ftl_sums(const float* p, const float* t, long long numel, float* part, double* sums,
+                 hipStream_t stream) {
+  L3U_REQUIRE(numel > 0);
+  const int nb = grid_for(numel, 2048, 512);
+  hipLaunchKernelGGL(ftl_partials_kernel, dim3(nb), dim3(256), 0, stream, p, t, numel, part);
+  hipLaunchKernelGGL(ftl_sums_kernel, dim3(1), dim3(64), 0, stream, part, nb, sums);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_ftl_loss(const double* sums, double alpha, double beta, double gamma, double smooth,
+                 float* loss, hipStream_t stream) {
+  hipLaunchKernelGGL(ftl_loss_kernel, dim3(1), dim3(1), 0, stream, sums, alpha, beta, gamma, smooth,
+                     loss);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_ftl_bwd(const float* p, const float* t, long long numel, const double* sums, double alpha,
+                double beta, double gamma, double smooth, const float* gscale,
+                int through_sigmoid, float* g, hipStream_t stream) {
+  L3U_REQUIRE(numel > 0);
+  hipLaunchKernelGGL(ftl_bwd_kernel, dim3(grid_for(numel, 1024, 1024)), dim3(256), 0, stream, p, t,
+                     numel, sums, alpha, beta, gamma, smooth, gscale, through_sigmoid, g);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_adamw(float* p, const float* g, float* m, float* v, long long numel, const float* lr,
+              float beta1, float beta2, float eps, float weight_decay, int* step, float grad_scale,
+              hipStream_t stream) {
+  L3U_REQUIRE(numel > 0);
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(numel, 1024, 1024)), dim3(256), 0, stream, p, g, m,
+                     v, numel, lr, beta1, beta2, eps, weight_decay, step, grad_scale);
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, stream, step);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_reduce_segments(const float* src, const long long* items, int nitems, float* dst,
+                        hipStream_t stream) {
+  L3U_REQUIRE(nitems > 0);
+  hipLaunchKernelGGL(reduce_segments_kernel, dim3(nitems), dim3(256), 0, stream, src, items, dst);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_counter_add(int* counter, int value, hipStream_t stream) {
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, stream, counter, value);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_abi_version(void) { return 1; }
+
+}  // extern "C"

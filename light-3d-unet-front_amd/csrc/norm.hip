@@ -1,0 +1,307 @@
+// InstanceNorm3d(affine) + LeakyReLU + Dropout3d + residual — statistics finalize, fused apply,
+// and the two-phase backward.  Replaces nn.InstanceNorm3d / nn.LeakyReLU / nn.Dropout3d and the
+// residual add of ResidualBlock.forward (unet3d.py:51-52, 62-66, 72, 77-93).
+//
+// Forward statistics come from the producing GEMM's epilogue as (count, mean, M2) partials per
+// (n, c, voxel-block); in_finalize merges them (Chan, fixed tree order -> deterministic) into the
+// per-(n,c) record of common.h.  All elementwise kernels are one workgroup per (n, c, voxel range)
+// so the record is a workgroup-uniform scalar load, and loads/stores are float4 when aligned.
+#include "common.h"
+using namespace l3u;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+L3U_DEV unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// one wave per (n, c)
+__global__ __launch_bounds__(256) void in_finalize_kernel(
+    const float* __restrict__ part, int nsb, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float drop_p, unsigned long long seed,
+    const int* __restrict__ step, int layer, float* __restrict__ rec, int NC, int C) {
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (wid >= NC) return;
+  const float* p = part + (long long)wid * nsb * 3;
+  float cn = 0.f, mu = 0.f, m2 = 0.f;
+  for (int i = l; i < nsb; i += 64) chan_merge(cn, mu, m2, p[i * 3], p[i * 3 + 1], p[i * 3 + 2]);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float cb = __shfl_xor(cn, o, 64), mb = __shfl_xor(mu, o, 64), vb = __shfl_xor(m2, o, 64);
+    // merge in lane order so both partners compute the same value
+    if (l & o) {
+      float c2 = cb, mu2 = mb, v2 = vb;
+      chan_merge(c2, mu2, v2, cn, mu, m2);
+      cn = c2; mu = mu2; m2 = v2;
+    } else {
+      chan_merge(cn, mu, m2, cb, mb, vb);
+    }
+  }
+  if (l != 0) return;
+  const int c = wid % C, n = wid / C;
+  const float var = cn > 0.f ? m2 / cn : 0.f;
+  const float rstd = 1.0f / sqrtf(var + kEps);
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  float k = 1.f;
+  if (drop_p > 0.f) {
+    const int st = step ? *step : 0;
+    const unsigned long long h = splitmix64(seed ^ splitmix64(((unsigned long long)st << 32) ^
+                                                              ((unsigned long long)layer << 24) ^
+                                                              (unsigned long long)(n * C + c)));
+    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+    k = u < drop_p ? 0.f : 1.f / (1.f - drop_p);
+  }
+  float* r = rec + (long long)wid * kRec;
+  r[0] = mu;
+  r[1] = rstd;
+  r[2] = k * g * rstd;
+  r[3] = k * b;
+  r[4] = k;
+  r[5] = g;
+  r[6] = b;
+  r[7] = 0.f;
+}
+
+// out = lrelu(scale2*y2 + shift2 + R),  R = r (identity shortcut) or scale_r*r + shift_r
+template <bool VEC>
+__global__ __launch_bounds__(256) void norm_act_fwd_kernel(
+    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
+    const float* __restrict__ r, long long rns, const float* __restrict__ recr,
+    float* __restrict__ out, long long ons, int C, int S) {
+  const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const float m2 = rec2[(long long)nc * kRec + 0];
+  const float a2 = rec2[(long long)nc * kRec + 2], b2 = rec2[(long long)nc * kRec + 3];
+  float ar = 1.f, br = 0.f, mr = 0.f;
+  if (recr) {
+    mr = recr[(long long)nc * kRec + 0];
+    ar = recr[(long long)nc * kRec + 2];
+    br = recr[(long long)nc * kRec + 3];
+  }
+  const float* yp = y2 + (long long)n * y2ns + (long long)c * S;
+  const float* rp = r + (long long)n * rns + (long long)c * S;
+  float* op = out + (long long)n * ons + (long long)c * S;
+  if (VEC) {
+    for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += gridDim.x * 1024) {
+      const f4 yv = *reinterpret_cast<const f4*>(yp + i), rv = *reinterpret_cast<const f4*>(rp + i);
+      f4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = lrelu(fmaf(a2, yv[q] - m2, b2) + fmaf(ar, rv[q] - mr, br));
+      *reinterpret_cast<f4*>(op + i) = o;
+    }
+  } else {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256)
+      op[i] = lrelu(fmaf(a2, yp[i] - m2, b2) + fmaf(ar, rp[i] - mr, br));
+  }
+}
+
+// partials per (c, n, block): [sum g, sum g*xhat2, sum g*xhat_r],  g = dout * lrelu'(out)
+template <bool VEC>
+__global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
+    const float* __restrict__ dout, long long dns, const float* __restrict__ out, long long ons,
+    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
+    const float* __restrict__ r, long long rns, const float* __restrict__ recr,
+    double* __restrict__ part, int N, int C, int S) {
+  __shared__ double red[4];
+  const int nc = blockIdx.y, c = nc % C, n = nc / C, nb = gridDim.x;
+  const float m2 = rec2[(long long)nc * kRec + 0], rs2 = rec2[(long long)nc * kRec + 1];
+  float mr = 0.f, rsr = 1.f;
+  if (recr) { mr = recr[(long long)nc * kRec + 0]; rsr = recr[(long long)nc * kRec + 1]; }
+  const long long co = (long long)c * S;
+  const float* dp = dout + (long long)n * dns + co;
+  const float* op = out + (long long)n * ons + co;
+  const float* yp = y2 + (long long)n * y2ns + co;
+  const float* rp = r + (long long)n * rns + co;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  if (VEC) {
+    for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += nb * 1024) {
+      const f4 dv = *reinterpret_cast<const f4*>(dp + i), ov = *reinterpret_cast<const f4*>(op + i);
+      const f4 yv = *reinterpret_cast<const f4*>(yp + i);
+      f4 rv = f4{0.f, 0.f, 0.f, 0.f};
+      if (recr) rv = *reinterpret_cast<const f4*>(rp + i);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float g = dv[q] * lrelu_d(ov[q]);
+        s0 += g;
+        s1 += (double)g * ((yv[q] - m2) * rs2);
+        if (recr) s2 += (double)g * ((rv[q] - mr) * rsr);
+      }
+    }
+  } else {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += nb * 256) {
+      const float g = dp[i] * lrelu_d(op[i]);
+      s0 += g;
+      s1 += (double)g * ((yp[i] - m2) * rs2);
+      if (recr) s2 += (double)g * ((rp[i] - mr) * rsr);
+    }
+  }
+  s0 = block_sum256d(s0, red);
+  s1 = block_sum256d(s1, red);
+  s2 = block_sum256d(s2, red);
+  if (threadIdx.x == 0) {
+    double* o = part + (((long long)c * N + n) * nb + blockIdx.x) * 3;
+    o[0] = s0; o[1] = s1; o[2] = s2;
+  }
+}
+
+// dy2 = rstd2*g2*(g - M0 - xhat2*M1);  dr = shortcut ? rstd_r*g_r*(g - M0 - xhat_r*M2) : g
+template <bool VEC>
+__global__ __launch_bounds__(256) void norm_act_bwd_apply_kernel(
+    const float* __restrict__ dout, long long dns, const float* __restrict__ out, long long ons,
+    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
+    const float* __restrict__ r, long long rns, const float* __restrict__ recr,
+    const double* __restrict__ part, int npart, float* __restrict__ dy2, long long dy2ns,
+    float* __restrict__ dr, long long drns, int N, int C, int S) {
+  const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const double* pp = part + ((long long)c * N + n) * npart * 3;
+  double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+  for (int i = 0; i < npart; ++i) { t0 += pp[i * 3]; t1 += pp[i * 3 + 1]; t2 += pp[i * 3 + 2]; }
+  const float M0 = (float)(t0 / S), M1 = (float)(t1 / S), M2 = (float)(t2 / S);
+  const float* q2 = rec2 + (long long)nc * kRec;
+  const float mu2 = q2[0], rs2 = q2[1], f2 = q2[1] * q2[5];
+  float mur = 0.f, rsr = 1.f, fr = 1.f;
+  if (recr) { const float* qr = recr + (long long)nc * kRec; mur = qr[0]; rsr = qr[1]; fr = qr[1] * qr[5]; }
+  const long long co = (long long)c * S;
+  const float* dp = dout + (long long)n * dns + co;
+  const float* op = out + (long long)n * ons + co;
+  const float* yp = y2 + (long long)n * y2ns + co;
+  const float* rp = r + (long long)n * rns + co;
+  float* d2 = dy2 + (long long)n * dy2ns + co;
+  float* drp = dr + (long long)n * drns + co;
+  if (VEC) {
+    for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += gridDim.x * 1024) {
+      const f4 dv = *reinterpret_cast<const f4*>(dp + i), ov = *reinterpret_cast<const f4*>(op + i);
+      const f4 yv = *reinterpret_cast<const f4*>(yp + i);
+      f4 rv = f4{0.f, 0.f, 0.f, 0.f};
+      if (recr) rv = *reinterpret_cast<const f4*>(rp + i);
+      f4 o2, orr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float g = dv[q] * lrelu_d(ov[q]);
+        o2[q] = f2 * (g - M0 - (yv[q] - mu2) * rs2 * M1);
+        orr[q] = recr ? fr * (g - M0 - (rv[q] - mur) * rsr * M2) : g;
+      }
+      *reinterpret_cast<f4*>(d2 + i) = o2;
+      *reinterpret_cast<f4*>(drp + i) = orr;
+    }
+  } else {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256) {
+      const float g = dp[i] * lrelu_d(op[i]);
+      d2[i] = f2 * (g - M0 - (yp[i] - mu2) * rs2 * M1);
+      drp[i] = recr ? fr * (g - M0 - (rp[i] - mur) * rsr * M2) : g;
+    }
+  }
+}
+
+// InstanceNorm backward apply for the inner norm (after dw3_bwd MODE 1 produced dpre + sums):
+// dy = rstd*gamma*(dpre - M1 - xhat*M2); in-place allowed (dy == dpre)
+template <bool VEC>
+__global__ __launch_bounds__(256) void in_bwd_apply_kernel(
+    const float* dpre, long long dns, const float* __restrict__ y, long long yns,
+    const float* __restrict__ rec, const double* __restrict__ part, int npart, float* dy,
+    long long dyns, int N, int C, int S) {
+  const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const double* pp = part + ((long long)c * N + n) * npart * 2;
+  double t0 = 0.0, t1 = 0.0;
+  for (int i = 0; i < npart; ++i) { t0 += pp[i * 2]; t1 += pp[i * 2 + 1]; }
+  const float M1 = (float)(t0 / S), M2 = (float)(t1 / S);
+  const float* q = rec + (long long)nc * kRec;
+  const float mu = q[0], rs = q[1], f = q[1] * q[5];
+  const long long co = (long long)c * S;
+  const float* dp = dpre + (long long)n * dns + co;
+  const float* yp = y + (long long)n * yns + co;
+  float* op = dy + (long long)n * dyns + co;
+  if (VEC) {
+    for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += gridDim.x * 1024) {
+      const f4 dv = *reinterpret_cast<const f4*>(dp + i), yv = *reinterpret_cast<const f4*>(yp + i);
+      f4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = f * (dv[k] - M1 - (yv[k] - mu) * rs * M2);
+      *reinterpret_cast<f4*>(op + i) = o;
+    }
+  } else {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256)
+      op[i] = f * (dp[i] - M1 - (yp[i] - mu) * rs * M2);
+  }
+}
+
+int elem_blocks(int S) {
+  const int per = 1024;   // elements per workgroup pass
+  int b = (S + per - 1) / per;
+  return b > 64 ? 64 : (b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+extern "C" {
+
+int l3u_in_finalize(const float* stat_part, int nsb, const float* gamma, const float* beta,
+                    float drop_p, unsigned long long seed, const int* step, int layer, float* rec,
+                    int N, int C, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && nsb > 0 && drop_p >= 0.f && drop_p < 1.f);
+  const int NC = N * C;
+  hipLaunchKernelGGL(in_finalize_kernel, dim3((NC + 3) / 4), dim3(256), 0, stream, stat_part, nsb,
+                     gamma, beta, drop_p, seed, step, layer, rec, NC, C);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_norm_act_nblocks(int S) { return elem_blocks(S); }
+
+int l3u_norm_act_fwd(const float* y2, long long y2_nstride, const float* rec2, const float* r,
+                     long long r_nstride, const float* rec_r, float* out, long long out_nstride,
+                     int N, int C, int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && S > 0);
+  const bool vec = S % 4 == 0 && y2_nstride % 4 == 0 && r_nstride % 4 == 0 && out_nstride % 4 == 0;
+  dim3 grid(elem_blocks(S), N * C);
+  if (vec) hipLaunchKernelGGL(norm_act_fwd_kernel<true>, grid, dim3(256), 0, stream, y2, y2_nstride, rec2, r, r_nstride, rec_r, out, out_nstride, C, S);
+  else hipLaunchKernelGGL(norm_act_fwd_kernel<false>, grid, dim3(256), 0, stream, y2, y2_nstride, rec2, r, r_nstride, rec_r, out, out_nstride, C, S);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_norm_act_bwd_reduce(const float* dout, long long dout_nstride, const float* out,
+                            long long out_nstride, const float* y2, long long y2_nstride,
+                            const float* rec2, const float* r, long long r_nstride,
+                            const float* rec_r, double* part, int N, int C, int S,
+                            hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && S > 0);
+  const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
+                   y2_nstride % 4 == 0 && r_nstride % 4 == 0;
+  dim3 grid(elem_blocks(S), N * C);
+  if (vec) hipLaunchKernelGGL(norm_act_bwd_reduce_kernel<true>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S);
+  else hipLaunchKernelGGL(norm_act_bwd_reduce_kernel<false>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_norm_act_bwd_apply(const float* dout, long long dout_nstride, const float* out,
+                           long long out_nstride, const float* y2, long long y2_nstride,
+                           const float* rec2, const float* r, long long r_nstride,
+                           const float* rec_r, const double* part, float* dy2,
+                           long long dy2_nstride, float* dr, long long dr_nstride, int N, int C,
+                           int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && S > 0);
+  const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
+                   y2_nstride % 4 == 0 && r_nstride % 4 == 0 && dy2_nstride % 4 == 0 &&
+                   dr_nstride % 4 == 0;
+  const int npart = elem_blocks(S);
+  dim3 grid(npart, N * C);
+  if (vec) hipLaunchKernelGGL(norm_act_bwd_apply_kernel<true>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, npart, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
+  else hipLaunchKernelGGL(norm_act_bwd_apply_kernel<false>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, npart, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_in_bwd_apply(const float* dpre, long long dpre_nstride, const float* y, long long y_nstride,
+                     const float* rec, const double* in_part, int npart, float* dy,
+                     long long dy_nstride, int N, int C, int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && S > 0 && npart > 0);
+  const bool vec = S % 4 == 0 && dpre_nstride % 4 == 0 && y_nstride % 4 == 0 && dy_nstride % 4 == 0;
+  dim3 grid(elem_blocks(S), N * C);
+  if (vec) hipLaunchKernelGGL(in_bwd_apply_kernel<true>, grid, dim3(256), 0, stream, dpre, dpre_nstride, y, y_nstride, rec, in_part, npart, dy, dy_nstride, N, C, S);
+  else hipLaunchKernelGGL(in_bwd_apply_kernel<false>, grid, dim3(256), 0, stream, dpre, dpre_nstride, y, y_nstride, rec, in_part, npart, dy, dy_nstride, N, C, S);
+  L3U_CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -1,0 +1,356 @@
+// Channel-contraction GEMMs on the fp32 MFMA (v_mfma_f32_16x16x4_f32, exact f32 fmac chain).
+//   pw_fwd        Y[n][j][s] = sum_k Wm[j][k] X[n][k][s] (+bias[j]) (+Y)     (1x1x1 conv fwd / bwd-data,
+//                 ConvTranspose3d(k2,s2) as a [Co*8 x Ci] GEMM)
+//   pw_bwd_weight dW[j][k] = sum_{n,s} dY[n][j][s] X[n][k][s]                 (split-K partials)
+// Replaces nn.Conv3d(Ci, Co, 1) of DepthwiseSeparableConv3d.pointwise (unet3d.py:18), the shortcut
+// conv (unet3d.py:70-73), and the GEMM part of nn.ConvTranspose3d(Ci, Ci/2, 2, 2) (unet3d.py:119).
+//
+// Register-direct operand mapping (no LDS round trip for the streamed operand): a lane loads one
+// float4 X[k0 + (l>>4)][s + 4(l&15) .. +3] (each k-row of the wave is 256 contiguous bytes) and
+// feeds component q to MFMA q, so MFMA q owns voxels {s + 4i + q}.  The accumulator row
+// i = 4(l>>4) + r of the four MFMAs then holds 4 CONSECUTIVE voxels per lane -> float4 stores.
+// The small weight operand is staged once per workgroup in LDS as Wt[k][j] (row stride padded to
+// 16 mod 32 floats: conflict-free ds_read_b32 for the 2x16-lane groups).
+// The pw_fwd epilogue can also emit per-(n, j) InstanceNorm partials (count, mean, M2) of its
+// output tile (Chan merge later), so InstanceNorm statistics never re-read the activation.
+#include "common.h"
+using namespace l3u;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+L3U_DEV f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+template <int NC, int NSW, bool VEC>
+__global__ __launch_bounds__(256) void pw_fwd_kernel(
+    const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
+    const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
+    float* __restrict__ stat_part, int K, int Nout, int S, int nsb) {
+  constexpr int CO_BLK = 16 * NC;
+  constexpr int TSB = 256 * NSW;
+  constexpr int WS = (CO_BLK % 32 == 16) ? CO_BLK : CO_BLK + 16;
+  constexpr int KCH = 128;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x;
+  const int sb = blockIdx.x, co0 = blockIdx.y * CO_BLK, n = blockIdx.z;
+  const int Kp = (K + 3) & ~3;
+  const int wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
+  const float* xn = x + (long long)n * xns;
+  const int sbase = sb * TSB + wave * 64 * NSW;
+
+  f4 acc[NSW][NC][4];
+#pragma unroll
+  for (int j = 0; j < NSW; ++j)
+#pragma unroll
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[j][m][q] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // the weight operand is staged through LDS in chunks of KCH reduction rows
+  for (int kc0 = 0; kc0 < Kp; kc0 += KCH) {
+  const int kc1 = min(Kp, kc0 + KCH);
+  if (kc0 > 0) __syncthreads();
+  for (int i = tid; i < (kc1 - kc0) * CO_BLK; i += 256) {
+    const int kr = i / CO_BLK, j = i - kr * CO_BLK, k = kc0 + kr, co = co0 + j;
+    float v = 0.f;
+    if (k < K && co < Nout) v = wl == 0 ? w[(long long)co * K + k] : w[(long long)k * Nout + co];
+    lds[kr * WS + j] = v;
+  }
+  __syncthreads();
+#pragma unroll 2
+  for (int k0 = kc0; k0 < kc1; k0 += 4) {
+    const int kk = k0 + lk;
+    f4 a[NSW];
+#pragma unroll
+    for (int j = 0; j < NSW; ++j) {
+      const int s = sbase + j * 64 + 4 * lr;
+      a[j] = f4{0.f, 0.f, 0.f, 0.f};
+      if (kk < K) {
+        const float* src = xn + (long long)kk * S + s;
+        if (VEC) {
+          if (s < S) a[j] = *reinterpret_cast<const f4*>(src);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (s + q < S) a[j][q] = src[q];
+        }
+      }
+    }
+    float b[NC];
+#pragma unroll
+    for (int m = 0; m < NC; ++m) b[m] = lds[(kk - kc0) * WS + 16 * m + lr];
+#pragma unroll
+    for (int j = 0; j < NSW; ++j)
+#pragma unroll
+      for (int m = 0; m < NC; ++m)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[j][m][q] = mfma4(a[j][q], b[m], acc[j][m][q]);
+  }
+  }
+
+  // epilogue: bias, accumulate, store, InstanceNorm partials
+  float* yn = y + (long long)n * yns;
+  float lsum[NC];
+#pragma unroll
+  for (int m = 0; m < NC; ++m) lsum[m] = 0.f;
+#pragma unroll
+  for (int m = 0; m < NC; ++m) {
+    const int co = co0 + 16 * m + lr;
+    const bool cok = co < Nout;
+    const float bv = (bias && cok) ? bias[co] : 0.f;
+#pragma unroll
+    for (int j = 0; j < NSW; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int s = sbase + j * 64 + 16 * lk + 4 * r;
+        f4 v = f4{acc[j][m][0][r], acc[j][m][1][r], acc[j][m][2][r], acc[j][m][3][r]} + bv;
+        float* dst = yn + (long long)co * S + s;
+        if (cok) {
+          if (VEC) {
+            if (s < S) {
+              if (accumulate) v += *reinterpret_cast<const f4*>(dst);
+              *reinterpret_cast<f4*>(dst) = v;
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (s + q < S) {
+                if (accumulate) v[q] += dst[q];
+                dst[q] = v[q];
+              }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[j][m][q][r] = v[q];                       // keep the stored value for the stats
+          if (s + q < S) lsum[m] += v[q];
+        }
+      }
+  }
+  if (stat_part == nullptr) return;
+  // per-channel block statistics (two-pass within the tile: mean, then M2 about that mean)
+  float* red = lds;                                     // [4][CO_BLK] (weights no longer needed)
+  const int s_lo = sb * TSB;
+  const int cnt = min(TSB, S - s_lo);
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < NC; ++m) {
+    float v = lsum[m];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lk == 0) red[wave * CO_BLK + 16 * m + lr] = v;
+  }
+  __syncthreads();
+  float mean[NC];
+#pragma unroll
+  for (int m = 0; m < NC; ++m) {
+    const int jj = 16 * m + lr;
+    mean[m] = ((red[jj] + red[CO_BLK + jj]) + (red[2 * CO_BLK + jj] + red[3 * CO_BLK + jj])) / (float)cnt;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < NC; ++m) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < NSW; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int s = sbase + j * 64 + 16 * lk + 4 * r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (s + q < S) {
+            const float d = acc[j][m][q][r] - mean[m];
+            v = fmaf(d, d, v);
+          }
+      }
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lk == 0) red[wave * CO_BLK + 16 * m + lr] = v;
+  }
+  __syncthreads();
+  if (wave == 0 && lk == 0) {
+#pragma unroll
+    for (int m = 0; m < NC; ++m) {
+      const int jj = 16 * m + lr, co = co0 + jj;
+      if (co < Nout) {
+        const float m2 = (red[jj] + red[CO_BLK + jj]) + (red[2 * CO_BLK + jj] + red[3 * CO_BLK + jj]);
+        float* o = stat_part + (((long long)n * Nout + co) * nsb + sb) * 3;
+        o[0] = (float)cnt;
+        o[1] = mean[m];
+        o[2] = m2;
+      }
+    }
+  }
+}
+
+// dW[j][k] partial over one voxel chunk of one sample.  A = dY (rows j), B = X^T (cols k),
+// the MFMA k-dimension is the voxel: lane l loads float4 dY[j0+16mo+(l&15)][s+4(l>>4)..+3] and
+// X[k0+16mi+(l&15)][s+4(l>>4)..+3]; component q feeds MFMA q.
+template <int NJ, int NK, bool VEC>
+__global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
+    const float* __restrict__ dy, long long dyns, const float* __restrict__ x, long long xns,
+    float* __restrict__ part, int J, int K, int S, int SCH, int nsc) {
+  constexpr int TJ = 16 * NJ, TK = 16 * NK, T = NJ * NK * 4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];   // [64][T]
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
+  const int sc = blockIdx.x % nsc, n = blockIdx.x / nsc;
+  const int ntk = (K + TK - 1) / TK;
+  const int j0 = (blockIdx.y / ntk) * TJ, k0 = (blockIdx.y % ntk) * TK;
+  const float* dyn = dy + (long long)n * dyns;
+  const float* xn = x + (long long)n * xns;
+  const int s_lo = sc * SCH, s_hi = min(S, s_lo + SCH);
+
+  f4 acc[NJ][NK];
+#pragma unroll
+  for (int a = 0; a < NJ; ++a)
+#pragma unroll
+    for (int b = 0; b < NK; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int s = s_lo + wave * 16; s < s_hi; s += 64) {
+    const int sl = s + 4 * lk;
+    f4 av[NJ], bv[NK];
+#pragma unroll
+    for (int a = 0; a < NJ; ++a) {
+      const int jj = j0 + 16 * a + lr;
+      av[a] = f4{0.f, 0.f, 0.f, 0.f};
+      if (jj < J) {
+        const float* src = dyn + (long long)jj * S + sl;
+        if (VEC) {
+          if (sl < s_hi) av[a] = *reinterpret_cast<const f4*>(src);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (sl + q < s_hi) av[a][q] = src[q];
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NK; ++b) {
+      const int kk = k0 + 16 * b + lr;
+      bv[b] = f4{0.f, 0.f, 0.f, 0.f};
+      if (kk < K) {
+        const float* src = xn + (long long)kk * S + sl;
+        if (VEC) {
+          if (sl < s_hi) bv[b] = *reinterpret_cast<const f4*>(src);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (sl + q < s_hi) bv[b][q] = src[q];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int a = 0; a < NJ; ++a)
+#pragma unroll
+        for (int b = 0; b < NK; ++b) acc[a][b] = mfma4(av[a][q], bv[b][q], acc[a][b]);
+  }
+  // fixed-order cross-wave reduction through LDS
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv) {
+#pragma unroll
+      for (int a = 0; a < NJ; ++a)
+#pragma unroll
+        for (int b = 0; b < NK; ++b)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int idx = l * T + (a * NK + b) * 4 + r;
+            lds[idx] = wv == 0 ? acc[a][b][r] : lds[idx] + acc[a][b][r];
+          }
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+    float* o = part + (long long)blockIdx.x * J * K;
+#pragma unroll
+    for (int a = 0; a < NJ; ++a)
+#pragma unroll
+      for (int b = 0; b < NK; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int jj = j0 + 16 * a + 4 * lk + r, kk = k0 + 16 * b + lr;
+          if (jj < J && kk < K) o[(long long)jj * K + kk] = lds[l * T + (a * NK + b) * 4 + r];
+        }
+  }
+}
+
+int pw_sch(int S) { return S >= 4096 ? 1024 : (S >= 1024 ? 512 : 256); }
+
+}  // namespace
+
+extern "C" {
+
+int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout,
+               const float* bias, float* y, long long y_nstride, int accumulate,
+               float* stat_part, int N, int K, int Nout, int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && K > 0 && Nout > 0 && S > 0);
+  const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (y_nstride % 4 == 0);
+  const int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
+  const int NC = CO_BLK / 16, NSW = 4 / NC, TSB = 256 * NSW;
+  const int nsb = (S + TSB - 1) / TSB;
+  const int WS = (CO_BLK % 32 == 16) ? CO_BLK : CO_BLK + 16;
+  const int Kp = (K + 3) & ~3;
+  size_t lds = (size_t)(Kp < 128 ? Kp : 128) * WS * sizeof(float);
+  if (lds < 4 * CO_BLK * sizeof(float)) lds = 4 * CO_BLK * sizeof(float);
+  L3U_REQUIRE(lds <= 160 * 1024);
+  dim3 grid(nsb, (Nout + CO_BLK - 1) / CO_BLK, N), block(256);
+#define PWF(NC_, NSW_)                                                                          \
+  do {                                                                                          \
+    if (vec) hipLaunchKernelGGL((pw_fwd_kernel<NC_, NSW_, true>), grid, block, lds, stream, x,  \
+                                x_nstride, w, w_layout, bias, y, y_nstride, accumulate,          \
+                                stat_part, K, Nout, S, nsb);                                     \
+    else hipLaunchKernelGGL((pw_fwd_kernel<NC_, NSW_, false>), grid, block, lds, stream, x,     \
+                            x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part,   \
+                            K, Nout, S, nsb);                                                    \
+  } while (0)
+  if (NC == 1) PWF(1, 4);
+  else if (NC == 2) PWF(2, 2);
+  else PWF(4, 1);
+#undef PWF
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_pw_stat_nsb(int Nout, int S) {
+  const int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
+  const int TSB = 256 * (4 / (CO_BLK / 16));
+  return (S + TSB - 1) / TSB;
+}
+
+int l3u_pw_bwd_weight_nparts(int N, int S) {
+  const int SCH = pw_sch(S);
+  return N * ((S + SCH - 1) / SCH);
+}
+
+int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
+                      float* part, int N, int J, int K, int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && J > 0 && K > 0 && S > 0);
+  const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (dy_nstride % 4 == 0);
+  const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
+  const int NJ = J <= 16 ? 1 : (J <= 32 ? 2 : 4);
+  const int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
+  const int ntj = (J + 16 * NJ - 1) / (16 * NJ), ntk = (K + 16 * NK - 1) / (16 * NK);
+  const size_t lds = 64 * (size_t)NJ * NK * 4 * sizeof(float);
+  dim3 grid(N * nsc, ntj * ntk), block(256);
+#define PWB(A_, B_)                                                                               \
+  do {                                                                                            \
+    if (vec) hipLaunchKernelGGL((pw_bwd_weight_kernel<A_, B_, true>), grid, block, lds, stream,  \
+                                dy, dy_nstride, x, x_nstride, part, J, K, S, SCH, nsc);          \
+    else hipLaunchKernelGGL((pw_bwd_weight_kernel<A_, B_, false>), grid, block, lds, stream, dy, \
+                            dy_nstride, x, x_nstride, part, J, K, S, SCH, nsc);                  \
+  } while (0)
+  if (NJ == 1 && NK == 1) PWB(1, 1);
+  else if (NJ == 1 && NK == 2) PWB(1, 2);
+  else if (NJ == 1 && NK == 4) PWB(1, 4);
+  else if (NJ == 2 && NK == 1) PWB(2, 1);
+  else if (NJ == 2 && NK == 2) PWB(2, 2);
+  else if (NJ == 2 && NK == 4) PWB(2, 4);
+  else if (NJ == 4 && NK == 1) PWB(4, 1);
+  else if (NJ == 4 && NK == 2) PWB(4, 2);
+  else PWB(4, 4);
+#undef PWB
+  L3U_CHECK_LAUNCH();
+}
+
+}  // extern "C"

@@ -1,0 +1,116 @@
+"""ctypes binding of the gfx950 C-ABI library (include/l3u.h -> lib/libl3u_hip.so).
+
+This is the only place the host mirror touches native code.  There is no fallback: if the
+library is missing or the tensors are not on a ROCm device, calls raise immediately.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime the library binds to: one runtime per process)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "L3U_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libl3u_hip.so"))
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_longlong
+F = ctypes.c_float
+D = ctypes.c_double
+U64 = ctypes.c_ulonglong
+
+# name -> argtypes (stream is always the trailing void*; every function returns int hipError_t)
+_SIGS = {
+    "l3u_abi_version": [],
+    "l3u_dw3_nchunk": [I],
+    "l3u_dw3_fwd": [P, L, P, P, P, L, I, I, I, I, I, P],
+    "l3u_dw3_bwd": [P, L, P, L, P, P, P, L, I, P, P, I, I, I, I, I, P],
+    "l3u_pw_stat_nsb": [I, I],
+    "l3u_pw_fwd": [P, L, P, I, P, P, L, I, P, I, I, I, I, P],
+    "l3u_pw_bwd_weight_nparts": [I, I],
+    "l3u_pw_bwd_weight": [P, L, P, L, P, I, I, I, I, P],
+    "l3u_in_finalize": [P, I, P, P, F, U64, P, I, P, I, I, P],
+    "l3u_norm_act_nblocks": [I],
+    "l3u_norm_act_fwd": [P, L, P, P, L, P, P, L, I, I, I, P],
+    "l3u_norm_act_bwd_reduce": [P, L, P, L, P, L, P, P, L, P, P, I, I, I, P],
+    "l3u_norm_act_bwd_apply": [P, L, P, L, P, L, P, P, L, P, P, P, L, P, L, I, I, I, P],
+    "l3u_in_bwd_apply": [P, L, P, L, P, P, I, P, L, I, I, I, P],
+    "l3u_maxpool2_fwd": [P, L, P, L, P, I, I, I, I, I, P],
+    "l3u_maxpool2_bwd": [P, L, P, P, L, P, L, I, I, I, I, I, P],
+    "l3u_convt_d2s": [P, P, P, L, I, I, I, I, I, P],
+    "l3u_convt_s2d": [P, L, P, I, I, I, I, I, P],
+    "l3u_chan_sum_nblocks": [L],
+    "l3u_chan_sum": [P, L, P, I, I, L, P],
+    "l3u_outconv_nblocks": [I],
+    "l3u_outconv_fwd": [P, L, P, P, P, I, I, I, P],
+    "l3u_outconv_bwd": [P, P, P, L, P, P, L, P, I, I, I, P],
+    "l3u_ftl_nblocks": [L],
+    "l3u_ftl_sums": [P, P, L, P, P, P],
+    "l3u_ftl_loss": [P, D, D, D, D, P, P],
+    "l3u_ftl_bwd": [P, P, L, P, D, D, D, D, P, I, P, P],
+    "l3u_adamw": [P, P, P, P, L, P, F, F, F, F, P, F, P],
+    "l3u_reduce_segments": [P, P, I, P, P],
+    "l3u_counter_add": [P, I, P],
+}
+# query helpers that return a value instead of an error code
+_QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_weight_nparts",
+            "l3u_norm_act_nblocks", "l3u_chan_sum_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks"}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the library (once).  Raises NativeError if it is missing: there is no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"HIP library not found at {LIB_PATH}; build it with `make -C light-3d-unet-front_amd` "
+            "(or __graft_entry__.build()).  The Light-3D-U-Net MI355X path has no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = I
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise NativeError(f"{name} failed with hipError {rc}")
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t, offset=0):
+    """Device pointer of tensor `t` (+ element offset).  None -> NULL."""
+    if t is None:
+        return None
+    return t.data_ptr() + offset * t.element_size()
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and (not t.is_cuda or t.dtype not in (torch.float32, torch.float64,
+                                                               torch.int32, torch.int64,
+                                                               torch.uint8)):
+            raise NativeError(
+                f"light_unet MI355X path needs ROCm device tensors (got {t.device}, {t.dtype}); "
+                "there is no CPU fallback")

@@ -1,0 +1,490 @@
+"""Forward / backward schedule of Lightweight3DUNet on the gfx950 C-ABI kernels.
+
+Reference semantics: light_unet/models/unet3d.py:146-223 (network), :77-93 (ResidualBlock),
+:96-111 (DownBlock), :114-143 (UpBlock).  Every arithmetic op runs in a HIP kernel of
+lib/libl3u_hip.so (include/l3u.h); this module only allocates buffers and orders launches on the
+current HIP stream, so a whole training step can be captured into one hipGraph.
+
+Memory layout: fp32 NCDHW.  The three decoder concatenations are single buffers
+cat_k = [up_k | skip_k]; the encoder block that produces skip_k writes straight into the upper
+channel half and the ConvTranspose3d writes the lower half, so torch.cat never copies
+(unet3d.py:141).  Their gradients share the same layout.
+
+Partial sums (IN statistics, weight-gradient split-K partials) live in a per-shape arena whose
+layout is fixed by a dry run on first use; one l3u_reduce_segments launch at the end of backward
+turns all weight-gradient partials into the flat gradient buffer in a fixed order.
+"""
+import math
+
+import torch
+
+from . import _native as nat
+
+F32 = 4
+
+
+class V:
+    """A strided activation view: channel c of sample n at t[off + n*ns + c*S]."""
+    __slots__ = ("t", "off", "ns", "C")
+
+    def __init__(self, t, off, ns, C):
+        self.t, self.off, self.ns, self.C = t, off, ns, C
+
+    @property
+    def p(self):
+        return self.t.data_ptr() + F32 * self.off
+
+
+def param_layout(enc, in_channels=1, out_channels=1):
+    """(name, shape) in reference registration order (unet3d.py:146-202)."""
+    out = []
+
+    def rb(pre, cin, cout):
+        out.extend([
+            (pre + "conv1.depthwise.weight", (cin, 1, 3, 3, 3)),
+            (pre + "conv1.pointwise.weight", (cout, cin, 1, 1, 1)),
+            (pre + "norm1.weight", (cout,)), (pre + "norm1.bias", (cout,)),
+            (pre + "conv2.depthwise.weight", (cout, 1, 3, 3, 3)),
+            (pre + "conv2.pointwise.weight", (cout, cout, 1, 1, 1)),
+            (pre + "norm2.weight", (cout,)), (pre + "norm2.bias", (cout,)),
+        ])
+        if cin != cout:
+            out.extend([(pre + "shortcut.0.weight", (cout, cin, 1, 1, 1)),
+                        (pre + "shortcut.1.weight", (cout,)), (pre + "shortcut.1.bias", (cout,))])
+
+    c0, c1, c2, c3 = enc
+    rb("init_conv.", in_channels, c0)
+    rb("down1.res_block.", c0, c1)
+    rb("down2.res_block.", c1, c2)
+    rb("down3.res_block.", c2, c3)
+    rb("bottleneck.", c3, c3)
+    for name, ci, co in (("up1.", c3, c2), ("up2.", c2, c1), ("up3.", c1, c0)):
+        out.append((name + "up.weight", (ci, ci // 2, 2, 2, 2)))
+        out.append((name + "up.bias", (ci // 2,)))
+        rb(name + "res_block.", ci, co)
+    out.append(("out_conv.weight", (out_channels, c0, 1, 1, 1)))
+    out.append(("out_conv.bias", (out_channels,)))
+    return out
+
+
+class _Arena:
+    """Bump allocator over one float32 tensor; sized by a dry run on first use of a shape."""
+
+    def __init__(self):
+        self.t = None
+        self.top = 0
+
+    def reset(self, t):
+        self.t, self.top = t, 0
+
+    def alloc(self, n):
+        off = self.top
+        self.top += (int(n) + 63) & ~63
+        return off
+
+    def ptr(self, off):
+        return 0 if self.t is None else self.t.data_ptr() + F32 * off
+
+
+class UNetEngine:
+    """Runs Lightweight3DUNet forward/backward on the C-ABI kernels for one architecture."""
+
+    BLOCKS = ("init_conv.", "down1.res_block.", "down2.res_block.", "down3.res_block.",
+              "bottleneck.", "up1.res_block.", "up2.res_block.", "up3.res_block.")
+
+    def __init__(self, encoder_channels=(16, 32, 64, 128), in_channels=1, out_channels=1,
+                 seed=0x5EED):
+        if in_channels != 1 or out_channels != 1:
+            raise NotImplementedError("the MI355X path implements in_channels = out_channels = 1 "
+                                      "(the reference's only configuration, trainer.py:57-66)")
+        enc = tuple(int(c) for c in encoder_channels)
+        if len(enc) != 4 or any(c % 2 for c in enc[1:]):
+            raise ValueError(f"encoder_channels must be 4 even ints, got {encoder_channels}")
+        if enc[0] > 32:
+            raise NotImplementedError("out_conv kernel supports encoder_channels[0] <= 32")
+        self.enc = enc
+        self.layout = param_layout(enc)
+        self.offsets = {}
+        off = 0
+        for name, shape in self.layout:
+            n = math.prod(shape)
+            self.offsets[name] = (off, n, shape)
+            off += n
+        self.numel = off
+        self.seed = seed
+        self._arenas = {}
+        self._items = {}
+        self._dry = False
+        self._items_rec = None
+        self.debug = None      # dict -> backward stashes each block's output-gradient view
+        self.fwd_arena = _Arena()
+        self.bwd_arena = _Arena()
+
+    # ------------------------------------------------------------------ helpers
+    def _call(self, name, *args):
+        if not self._dry:
+            nat.call(name, *args)
+
+    def _w(self, flat, name):
+        return flat.data_ptr() + F32 * self.offsets[name][0]
+
+    def _has(self, name):
+        return name in self.offsets
+
+    def _empty(self, *shape, dtype=torch.float32, device=None):
+        return torch.empty(shape, dtype=dtype, device=device)
+
+    def _seg(self, src_off, count, istride, tstride, length, dst_name, dst_elem=0, accumulate=0,
+             f64=0):
+        """Record reduction items: grad[dst_name][dst_elem + t] = sum_i part[src_off+i*is+t*ts].
+        f64=1: the partials are fp64 and src_off/strides count doubles from the arena base."""
+        base = self.offsets[dst_name][0] + dst_elem
+        t0 = 0
+        while t0 < length:
+            ln = min(256, length - t0)
+            self._items_rec.append((src_off + t0 * tstride, count, istride, tstride, ln,
+                                    base + t0, accumulate, f64))
+            t0 += ln
+
+    @staticmethod
+    def check_shape(x):
+        if x.dim() != 5 or x.shape[1] != 1:
+            raise ValueError(f"expected input [N, 1, D, H, W], got {tuple(x.shape)}")
+        _, _, D, H, W = x.shape
+        if D % 8 or H % 8 or W % 8:
+            raise NotImplementedError(
+                "D, H, W must be divisible by 8 on the MI355X path (the reference's pad branch, "
+                f"unet3d.py:130-138, only fires otherwise); got {(D, H, W)}")
+        if H * W > 4096:
+            raise NotImplementedError(f"H*W <= 4096 required by the stencil kernel, got {H * W}")
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, flat, x, training=False, dropout_p=0.0, counter=None, save=True):
+        """x: [N,1,D,H,W] fp32 on device -> probabilities [N,1,D,H,W] (+ saved state)."""
+        self.check_shape(x)
+        x = x.contiguous()
+        N, _, D, H, W = x.shape
+        dev = x.device
+        key = ("f", N, D, H, W)
+        if key not in self._arenas:
+            self._dry = True
+            self.fwd_arena.reset(None)
+            try:
+                self._forward_impl(flat, x, training, dropout_p, counter, save, dev)
+            finally:
+                self._dry = False
+            self._arenas[key] = torch.empty(max(self.fwd_arena.top, 64), dtype=torch.float32,
+                                            device=dev)
+        self.fwd_arena.reset(self._arenas[key])
+        return self._forward_impl(flat, x, training, dropout_p, counter, save, dev)
+
+    def _forward_impl(self, flat, x, training, dropout_p, counter, save, dev):
+        N, _, D, H, W = x.shape
+        c0, c1, c2, c3 = self.enc
+        dims = [(D >> k, H >> k, W >> k) for k in range(4)]
+        S = [d * h * w for d, h, w in dims]
+        e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
+        drop = dropout_p if training else 0.0
+        st = nat.stream()
+        sv = {"N": N, "dims": dims, "S": S, "x": x, "drop": drop}
+        if drop > 0.0 and counter is not None:
+            self._call("l3u_counter_add", counter.data_ptr(), 1, st)
+        cptr = counter.data_ptr() if counter is not None else None
+        # concatenation buffers [up | skip]
+        cat3, cat2, cat1 = e(N, 2 * c0, S[0]), e(N, 2 * c1, S[1]), e(N, 2 * c2, S[2])
+        x4 = e(N, c3, S[3])
+        sv.update(cat3=cat3, cat2=cat2, cat1=cat1, x4=x4)
+        x_in = V(x, 0, S[0], 1)
+        x1 = V(cat3, c0 * S[0], 2 * c0 * S[0], c0)
+        x2 = V(cat2, c1 * S[1], 2 * c1 * S[1], c1)
+        x3 = V(cat1, c2 * S[2], 2 * c2 * S[2], c2)
+        x4v = V(x4, 0, c3 * S[3], c3)
+        blk = {}
+        blk["init_conv."] = self._block_fwd(flat, "init_conv.", 0, x_in, x1, dims[0], drop, cptr, st, dev)
+        pools = []
+        for k, (name, src, dst) in enumerate((("down1.res_block.", x1, x2), ("down2.res_block.", x2, x3),
+                                              ("down3.res_block.", x3, x4v))):
+            d, h, w = dims[k]
+            pooled = e(N, src.C, S[k + 1])
+            idx = self._empty(N, src.C, S[k + 1], dtype=torch.uint8, device=dev)
+            self._call("l3u_maxpool2_fwd", src.p, src.ns, pooled.data_ptr(), src.C * S[k + 1],
+                       idx.data_ptr(), N, src.C, d, h, w, st)
+            pools.append((pooled, idx))
+            pv = V(pooled, 0, src.C * S[k + 1], src.C)
+            blk[name] = self._block_fwd(flat, name, k + 1, pv, dst, dims[k + 1], drop, cptr, st, dev)
+        sv["pools"] = pools
+        bott = e(N, c3, S[3])
+        blk["bottleneck."] = self._block_fwd(flat, "bottleneck.", 4, x4v, V(bott, 0, c3 * S[3], c3),
+                                             dims[3], drop, cptr, st, dev)
+        prev = V(bott, 0, c3 * S[3], c3)
+        ups = []
+        for k, (up, cat, co, lvl) in enumerate((("up1.", cat1, c2, 2), ("up2.", cat2, c1, 1),
+                                                ("up3.", cat3, c0, 0))):
+            d, h, w = dims[lvl + 1]
+            ci = prev.C
+            yp = e(N, co * 8, S[lvl + 1])
+            self._call("l3u_pw_fwd", prev.p, prev.ns, self._w(flat, up + "up.weight"), 1, None,
+                       yp.data_ptr(), co * 8 * S[lvl + 1], 0, None, N, ci, co * 8, S[lvl + 1], st)
+            self._call("l3u_convt_d2s", yp.data_ptr(), self._w(flat, up + "up.bias"), cat.data_ptr(),
+                       2 * co * S[lvl], N, co, d, h, w, st)
+            out = e(N, co, S[lvl])
+            cat_v = V(cat, 0, 2 * co * S[lvl], 2 * co)
+            blk[up + "res_block."] = self._block_fwd(flat, up + "res_block.", 5 + k, cat_v,
+                                                     V(out, 0, co * S[lvl], co), dims[lvl], drop,
+                                                     cptr, st, dev)
+            ups.append((prev, out))
+            prev = V(out, 0, co * S[lvl], co)
+        sv["ups"] = ups
+        p = e(N, 1, D, H, W)
+        self._call("l3u_outconv_fwd", prev.p, prev.ns, self._w(flat, "out_conv.weight"),
+                   self._w(flat, "out_conv.bias"), p.data_ptr(), N, c0, S[0], st)
+        sv["h"] = prev
+        sv["p"] = p
+        sv["blk"] = blk
+        return p, (sv if save else None)
+
+    def _stats_and_finalize(self, flat, name_g, name_b, stat_off, nsb, rec, N, C, drop, cptr, layer, st):
+        g = self._w(flat, name_g)
+        b = self._w(flat, name_b)
+        self._call("l3u_in_finalize", self.fwd_arena.ptr(stat_off), nsb, g, b, float(drop),
+                   self.seed, cptr, layer, rec, N, C, st)
+
+    def _block_fwd(self, flat, pre, layer, x, out, dims, drop, cptr, st, dev):
+        """ResidualBlock.forward (unet3d.py:77-93) into the view `out`."""
+        N = x.t.shape[0]
+        d, h, w = dims
+        S = d * h * w
+        cin = x.C
+        cout = out.C
+        e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
+        nsb = nat.query("l3u_pw_stat_nsb", cout, S)
+        recs = e(3, N * cout, 8)
+        rec_r, rec1, rec2 = (recs[0].data_ptr(), recs[1].data_ptr(), recs[2].data_ptr())
+        sv = {"x": x, "out": out, "recs": recs}
+        shortcut = self._has(pre + "shortcut.0.weight")
+        if shortcut:
+            r = e(N, cout, S)
+            so = self.fwd_arena.alloc(N * cout * nsb * 3)
+            self._call("l3u_pw_fwd", x.p, x.ns, self._w(flat, pre + "shortcut.0.weight"), 0, None,
+                       r.data_ptr(), cout * S, 0, self.fwd_arena.ptr(so), N, cin, cout, S, st)
+            self._stats_and_finalize(flat, pre + "shortcut.1.weight", pre + "shortcut.1.bias", so,
+                                     nsb, rec_r, N, cout, 0.0, cptr, 0, st)
+            rv = V(r, 0, cout * S, cout)
+            sv["r"] = rv
+        else:
+            rv = x
+            sv["r"] = None
+        z1 = e(N, cin, S)
+        self._call("l3u_dw3_fwd", x.p, x.ns, self._w(flat, pre + "conv1.depthwise.weight"), None,
+                   z1.data_ptr(), cin * S, N, cin, d, h, w, st)
+        y1 = e(N, cout, S)
+        s1 = self.fwd_arena.alloc(N * cout * nsb * 3)
+        self._call("l3u_pw_fwd", z1.data_ptr(), cin * S, self._w(flat, pre + "conv1.pointwise.weight"),
+                   0, None, y1.data_ptr(), cout * S, 0, self.fwd_arena.ptr(s1), N, cin, cout, S, st)
+        self._stats_and_finalize(flat, pre + "norm1.weight", pre + "norm1.bias", s1, nsb, rec1, N,
+                                 cout, drop, cptr, 1 + layer, st)
+        z2 = e(N, cout, S)
+        self._call("l3u_dw3_fwd", y1.data_ptr(), cout * S, self._w(flat, pre + "conv2.depthwise.weight"),
+                   rec1, z2.data_ptr(), cout * S, N, cout, d, h, w, st)
+        y2 = e(N, cout, S)
+        s2 = self.fwd_arena.alloc(N * cout * nsb * 3)
+        self._call("l3u_pw_fwd", z2.data_ptr(), cout * S, self._w(flat, pre + "conv2.pointwise.weight"),
+                   0, None, y2.data_ptr(), cout * S, 0, self.fwd_arena.ptr(s2), N, cout, cout, S, st)
+        self._stats_and_finalize(flat, pre + "norm2.weight", pre + "norm2.bias", s2, nsb, rec2, N,
+                                 cout, 0.0, cptr, 0, st)
+        self._call("l3u_norm_act_fwd", y2.data_ptr(), cout * S, rec2, rv.p, rv.ns,
+                   rec_r if shortcut else None, out.p, out.ns, N, cout, S, st)
+        sv.update(z1=z1, y1=y1, z2=z2, y2=y2, dims=dims, shortcut=shortcut)
+        return sv
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, flat, gflat, sv, dp, need_dx=False):
+        """Given dL/dp write all parameter gradients into gflat
+        (overwrite) and return dL/dx if need_dx."""
+        N = sv["N"]
+        D, H, W = sv["dims"][0]
+        key = ("b", N, D, H, W, bool(need_dx))
+        if key not in self._arenas:
+            self._dry = True
+            self.bwd_arena.reset(None)
+            self._items_rec = []
+            try:
+                self._backward_impl(flat, gflat, sv, dp, need_dx)
+            finally:
+                self._dry = False
+            dev = dp.device
+            self._arenas[key] = torch.empty(max(self.bwd_arena.top, 64), dtype=torch.float32,
+                                            device=dev)
+            self._items[key] = torch.tensor(self._items_rec, dtype=torch.int64, device=dev)
+        self.bwd_arena.reset(self._arenas[key])
+        self._items_rec = []
+        dx = self._backward_impl(flat, gflat, sv, dp, need_dx)
+        items = self._items[key]
+        nat.call("l3u_reduce_segments", self.bwd_arena.ptr(0), items.data_ptr(), items.shape[0],
+                 gflat.data_ptr(), nat.stream())
+        return dx
+
+    def _backward_impl(self, flat, gflat, sv, dp, need_dx):
+        N = sv["N"]
+        dims, S = sv["dims"], sv["S"]
+        c0, c1, c2, c3 = self.enc
+        dev = sv["p"].device
+        e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
+        st = nat.stream()
+        A = self.bwd_arena
+        # ---- out_conv + sigmoid (unet3d.py:220-221)
+        h = sv["h"]
+        dh = e(N, c0, S[0])
+        nb = nat.query("l3u_outconv_nblocks", S[0])
+        po = A.alloc(2 * N * nb * (c0 + 1))          # fp64 partials
+        self._call("l3u_outconv_bwd", dp.data_ptr(), sv["p"].data_ptr(), h.p, h.ns,
+                   self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po), N, c0,
+                   S[0], st)
+        self._seg(po // 2, N * nb, c0 + 1, 1, c0, "out_conv.weight", f64=1)
+        self._seg(po // 2 + c0, N * nb, c0 + 1, 1, 1, "out_conv.bias", f64=1)
+        dcat3, dcat2, dcat1 = e(N, 2 * c0, S[0]), e(N, 2 * c1, S[1]), e(N, 2 * c2, S[2])
+        dcats = {0: dcat3, 1: dcat2, 2: dcat1}
+        dout = V(dh, 0, c0 * S[0], c0)
+        # ---- decoder (reverse order); up_specs = (prefix, Co, level, index into sv["ups"])
+        up_specs = [("up3.", c0, 0, 2), ("up2.", c1, 1, 1), ("up1.", c2, 2, 0)]
+        for up, co, lvl, uidx in up_specs:
+            dcat = dcats[lvl]
+            self._block_bwd(flat, up + "res_block.", sv["blk"][up + "res_block."], dout,
+                            V(dcat, 0, 2 * co * S[lvl], 2 * co), st, dev)
+            # ConvTranspose3d backward: input = prev (the lower-level output), dOut = dcat[:, :co]
+            prev, _ = sv["ups"][uidx]
+            ci = prev.C
+            d, hh, w = dims[lvl + 1]
+            dyp = e(N, co * 8, S[lvl + 1])
+            self._call("l3u_convt_s2d", dcat.data_ptr(), 2 * co * S[lvl], dyp.data_ptr(), N, co, d,
+                       hh, w, st)
+            dprev = e(N, ci, S[lvl + 1])
+            self._call("l3u_pw_fwd", dyp.data_ptr(), co * 8 * S[lvl + 1],
+                       self._w(flat, up + "up.weight"), 0, None, dprev.data_ptr(), ci * S[lvl + 1],
+                       0, None, N, co * 8, ci, S[lvl + 1], st)
+            npw = nat.query("l3u_pw_bwd_weight_nparts", N, S[lvl + 1])
+            pw = A.alloc(npw * ci * co * 8)
+            self._call("l3u_pw_bwd_weight", prev.p, prev.ns, dyp.data_ptr(), co * 8 * S[lvl + 1],
+                       A.ptr(pw), N, ci, co * 8, S[lvl + 1], st)
+            self._seg(pw, npw, ci * co * 8, 1, ci * co * 8, up + "up.weight")
+            ncs = nat.query("l3u_chan_sum_nblocks", 8 * S[lvl + 1])
+            pb = A.alloc(2 * co * N * ncs)            # fp64 partials
+            self._call("l3u_chan_sum", dyp.data_ptr(), co * 8 * S[lvl + 1], A.ptr(pb), N, co,
+                       8 * S[lvl + 1], st)
+            self._seg(pb // 2, N * ncs, 1, N * ncs, co, up + "up.bias", f64=1)
+            dout = V(dprev, 0, ci * S[lvl + 1], ci)
+        # ---- bottleneck
+        dx4 = e(N, c3, S[3])
+        self._block_bwd(flat, "bottleneck.", sv["blk"]["bottleneck."], dout,
+                        V(dx4, 0, c3 * S[3], c3), st, dev)
+        dout = V(dx4, 0, c3 * S[3], c3)
+        # ---- encoder
+        enc_specs = [("down3.res_block.", c2, 2), ("down2.res_block.", c1, 1),
+                     ("down1.res_block.", c0, 0)]
+        for name, cprev, lvl in enc_specs:
+            pooled, idx = sv["pools"][lvl]
+            dpool = e(N, cprev, S[lvl + 1])
+            self._block_bwd(flat, name, sv["blk"][name], dout, V(dpool, 0, cprev * S[lvl + 1], cprev),
+                            st, dev)
+            # d(level output) = maxpool_bwd(dpool) + d(skip) (upper half of dcat at this level)
+            dcat = dcats[lvl]
+            dlev = e(N, cprev, S[lvl])
+            d, hh, w = dims[lvl]
+            self._call("l3u_maxpool2_bwd", dpool.data_ptr(), cprev * S[lvl + 1], idx.data_ptr(),
+                       dcat.data_ptr() + F32 * cprev * S[lvl], 2 * cprev * S[lvl], dlev.data_ptr(),
+                       cprev * S[lvl], N, cprev, d, hh, w, st)
+            dout = V(dlev, 0, cprev * S[lvl], cprev)
+        # ---- init block
+        dx = e(N, 1, *dims[0])
+        self._block_bwd(flat, "init_conv.", sv["blk"]["init_conv."], dout, V(dx, 0, S[0], 1),
+                        st, dev)
+        return dx if need_dx else None
+
+    def _block_bwd(self, flat, pre, sv, dout, dxv, st, dev):
+        """Backward of ResidualBlock.forward (unet3d.py:77-93).  Writes d(block input) into dxv
+        (overwrite) and records the block's weight-gradient reductions."""
+        A = self.bwd_arena
+        x, out, recs = sv["x"], sv["out"], sv["recs"]
+        if self.debug is not None and not self._dry:
+            self.debug[pre] = dout
+        d, h, w = sv["dims"]
+        S = d * h * w
+        N = x.t.shape[0]
+        cin, cout = x.C, out.C
+        e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
+        rec_r, rec1, rec2 = recs[0].data_ptr(), recs[1].data_ptr(), recs[2].data_ptr()
+        shortcut = sv["shortcut"]
+        rv = sv["r"] if shortcut else x
+        y2, z2, y1, z1 = sv["y2"], sv["z2"], sv["y1"], sv["z1"]
+        # (1) block tail: out = lrelu(IN2(y2) + residual)
+        nb = nat.query("l3u_norm_act_nblocks", S)
+        pn = A.alloc(2 * cout * N * nb * 3)            # fp64 partials
+        pnd = pn // 2
+        self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(), cout * S,
+                   rec2, rv.p, rv.ns, rec_r if shortcut else None, A.ptr(pn), N, cout, S, st)
+        self._seg(pnd + 1, N * nb, 3, N * nb * 3, cout, pre + "norm2.weight", f64=1)
+        self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "norm2.bias", f64=1)
+        dy2 = e(N, cout, S)
+        if shortcut:
+            dr = e(N, cout, S)
+            drv = V(dr, 0, cout * S, cout)
+            self._seg(pnd + 2, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.weight", f64=1)
+            self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.bias", f64=1)
+        else:
+            drv = dxv   # identity shortcut: d(input) starts as g
+        self._call("l3u_norm_act_bwd_apply", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(), cout * S,
+                   rec2, rv.p, rv.ns, rec_r if shortcut else None, A.ptr(pn), dy2.data_ptr(),
+                   cout * S, drv.p, drv.ns, N, cout, S, st)
+        # (2) conv2.pointwise backward
+        dz2 = e(N, cout, S)
+        self._call("l3u_pw_fwd", dy2.data_ptr(), cout * S, self._w(flat, pre + "conv2.pointwise.weight"),
+                   1, None, dz2.data_ptr(), cout * S, 0, None, N, cout, cout, S, st)
+        npw = nat.query("l3u_pw_bwd_weight_nparts", N, S)
+        pp2 = A.alloc(npw * cout * cout)
+        self._call("l3u_pw_bwd_weight", dy2.data_ptr(), cout * S, z2.data_ptr(), cout * S, A.ptr(pp2),
+                   N, cout, cout, S, st)
+        self._seg(pp2, npw, cout * cout, 1, cout * cout, pre + "conv2.pointwise.weight")
+        # (3) conv2.depthwise backward fused with LeakyReLU/Dropout/IN1 backward partials
+        nch = nat.query("l3u_dw3_nchunk", d)
+        pd2 = A.alloc(cout * N * nch * 27)
+        pi1 = A.alloc(2 * cout * N * nch * 2)          # fp64 partials
+        pid = pi1 // 2
+        dpre = e(N, cout, S)
+        self._call("l3u_dw3_bwd", dz2.data_ptr(), cout * S, y1.data_ptr(), cout * S,
+                   self._w(flat, pre + "conv2.depthwise.weight"), rec1, dpre.data_ptr(), cout * S, 0,
+                   A.ptr(pd2), A.ptr(pi1), N, cout, d, h, w, st)
+        self._seg_dw(pd2, N * nch, cout, pre + "conv2.depthwise.weight")
+        self._seg(pid + 1, N * nch, 2, N * nch * 2, cout, pre + "norm1.weight", f64=1)
+        self._seg(pid + 0, N * nch, 2, N * nch * 2, cout, pre + "norm1.bias", f64=1)
+        self._call("l3u_in_bwd_apply", dpre.data_ptr(), cout * S, y1.data_ptr(), cout * S, rec1,
+                   A.ptr(pi1), nch, dpre.data_ptr(), cout * S, N, cout, S, st)
+        dy1 = dpre
+        # (4) conv1.pointwise backward
+        dz1 = e(N, cin, S)
+        self._call("l3u_pw_fwd", dy1.data_ptr(), cout * S, self._w(flat, pre + "conv1.pointwise.weight"),
+                   1, None, dz1.data_ptr(), cin * S, 0, None, N, cout, cin, S, st)
+        pp1 = A.alloc(npw * cout * cin)
+        self._call("l3u_pw_bwd_weight", dy1.data_ptr(), cout * S, z1.data_ptr(), cin * S, A.ptr(pp1),
+                   N, cout, cin, S, st)
+        self._seg(pp1, npw, cout * cin, 1, cout * cin, pre + "conv1.pointwise.weight")
+        # (5) shortcut conv backward writes d(input) first
+        if shortcut:
+            self._call("l3u_pw_fwd", drv.p, drv.ns, self._w(flat, pre + "shortcut.0.weight"), 1, None,
+                       dxv.p, dxv.ns, 0, None, N, cout, cin, S, st)
+            ppr = A.alloc(npw * cout * cin)
+            self._call("l3u_pw_bwd_weight", drv.p, drv.ns, x.p, x.ns, A.ptr(ppr), N, cout, cin, S, st)
+            self._seg(ppr, npw, cout * cin, 1, cout * cin, pre + "shortcut.0.weight")
+        # (6) conv1.depthwise backward accumulates into d(input)
+        pd1 = A.alloc(cin * N * nch * 27)
+        self._call("l3u_dw3_bwd", dz1.data_ptr(), cin * S, x.p, x.ns,
+                   self._w(flat, pre + "conv1.depthwise.weight"), None, dxv.p, dxv.ns, 1, A.ptr(pd1),
+                   None, N, cin, d, h, w, st)
+        self._seg_dw(pd1, N * nch, cin, pre + "conv1.depthwise.weight")
+        if self.debug is not None and not self._dry:
+            self.debug[pre + "#"] = {"dy2": dy2, "dr": drv, "dz2": dz2, "dy1": dy1, "dz1": dz1,
+                                     "dx": dxv}
+
+    def _seg_dw(self, off, count, C, name):
+        # dw_part layout [C][count][27] -> grad [C][27]
+        for c in range(C):
+            self._seg(off + c * count * 27, count, 27, 1, 27, name, dst_elem=c * 27)

@@ -1,0 +1,220 @@
+"""Lightweight3DUNet — MI355X (gfx950) drop-in for light_unet/models/unet3d.py of the reference.
+
+Same class names, constructor arguments, submodule tree and therefore identical state_dict keys,
+shapes and default initialisation as the reference (unet3d.py:12-229), so reference checkpoints
+load unchanged (inferencer.py:49) and `Trainer` (trainer.py:57-79) constructs it as before.
+
+What differs is execution: `Lightweight3DUNet.forward` runs the whole network as one autograd
+node whose forward and backward are the hand-written HIP kernels of lib/libl3u_hip.so, scheduled
+by `light_unet.engine.UNetEngine`.  The nn.Conv3d / nn.InstanceNorm3d / ... submodules below are
+parameter containers only (their own forward is never called on this path).  All parameters are
+views into ONE flat fp32 buffer (`flat_parameters()`), which is what the kernels, the fused
+AdamW and the single-bucket RCCL all-reduce operate on.
+
+Not on the MI355X path (raise NotImplementedError): use_depthwise_separable=False (dense /
+grouped 3^3 conv, unet3d.py:26-34,46-49,57-60 — not used by any shipped config), and
+volumes whose D, H, W are not multiples of 8 (the pad branch of UpBlock, unet3d.py:130-138).
+"""
+import torch
+import torch.nn as nn
+
+from .. import engine as _engine
+from .. import _native as nat
+
+
+class DepthwiseSeparableConv3d(nn.Module):
+    """unet3d.py:12-23 — depthwise 3^3 (groups=C) followed by pointwise 1^3, no bias."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=1, bias=False):
+        super().__init__()
+        if kernel_size != 3 or stride != 1 or padding != 1 or bias:
+            raise NotImplementedError("MI355X path: depthwise 3x3x3, stride 1, padding 1, no bias")
+        self.depthwise = nn.Conv3d(in_channels, in_channels, kernel_size=kernel_size,
+                                   stride=stride, padding=padding, groups=in_channels, bias=bias)
+        self.pointwise = nn.Conv3d(in_channels, out_channels, kernel_size=1, bias=bias)
+
+    def forward(self, x):
+        raise RuntimeError("submodules are parameter containers; call Lightweight3DUNet")
+
+
+class GroupedConv3d(nn.Module):
+    """unet3d.py:26-34 (dead code under every shipped config)."""
+
+    def __init__(self, *a, **k):
+        raise NotImplementedError(
+            "GroupedConv3d (use_depthwise_separable=False) is not on the MI355X path yet "
+            "(SURVEY §8f rank 3)")
+
+
+class ResidualBlock(nn.Module):
+    """unet3d.py:37-93 — same submodule names (conv1, norm1, relu1, conv2, norm2, relu2, dropout,
+    shortcut) so parameter names match."""
+
+    def __init__(self, in_channels, out_channels, use_depthwise_separable=True,
+                 use_grouped=True, groups=8, dropout_p=0.1):
+        super().__init__()
+        if not use_depthwise_separable:
+            raise NotImplementedError(
+                "use_depthwise_separable=False (dense/grouped 3^3 conv) is not on the MI355X path "
+                "yet; every shipped config uses depthwise-separable convs (SURVEY §0.2)")
+        self.conv1 = DepthwiseSeparableConv3d(in_channels, out_channels, kernel_size=3, padding=1)
+        self.norm1 = nn.InstanceNorm3d(out_channels, affine=True)
+        self.relu1 = nn.LeakyReLU(0.01, inplace=True)
+        self.conv2 = DepthwiseSeparableConv3d(out_channels, out_channels, kernel_size=3, padding=1)
+        self.norm2 = nn.InstanceNorm3d(out_channels, affine=True)
+        self.relu2 = nn.LeakyReLU(0.01, inplace=True)
+        self.dropout = nn.Dropout3d(dropout_p) if dropout_p > 0 else None
+        if in_channels != out_channels:
+            self.shortcut = nn.Sequential(
+                nn.Conv3d(in_channels, out_channels, kernel_size=1, bias=False),
+                nn.InstanceNorm3d(out_channels, affine=True))
+        else:
+            self.shortcut = nn.Identity()
+
+    def forward(self, x):
+        raise RuntimeError("submodules are parameter containers; call Lightweight3DUNet")
+
+
+class DownBlock(nn.Module):
+    """unet3d.py:96-111"""
+
+    def __init__(self, in_channels, out_channels, use_depthwise_separable=True,
+                 use_grouped=True, groups=8, dropout_p=0.1):
+        super().__init__()
+        self.pool = nn.MaxPool3d(kernel_size=2, stride=2)
+        self.res_block = ResidualBlock(in_channels, out_channels,
+                                       use_depthwise_separable=use_depthwise_separable,
+                                       use_grouped=use_grouped, groups=groups, dropout_p=dropout_p)
+
+    def forward(self, x):
+        raise RuntimeError("submodules are parameter containers; call Lightweight3DUNet")
+
+
+class UpBlock(nn.Module):
+    """unet3d.py:114-143"""
+
+    def __init__(self, in_channels, out_channels, use_depthwise_separable=True,
+                 use_grouped=True, groups=8, dropout_p=0.1):
+        super().__init__()
+        self.up = nn.ConvTranspose3d(in_channels, in_channels // 2, kernel_size=2, stride=2)
+        self.res_block = ResidualBlock(in_channels, out_channels,
+                                       use_depthwise_separable=use_depthwise_separable,
+                                       use_grouped=use_grouped, groups=groups, dropout_p=dropout_p)
+
+    def forward(self, x, skip):
+        raise RuntimeError("submodules are parameter containers; call Lightweight3DUNet")
+
+
+class _UNetFunction(torch.autograd.Function):
+    """Whole-network autograd node: forward and backward are C-ABI kernel schedules."""
+
+    @staticmethod
+    def forward(ctx, model, x, *params):
+        flat = model._flat
+        p, sv = model.engine.forward(flat, x, training=model.training, dropout_p=model.dropout_p,
+                                     counter=model._rng_counter, save=True)
+        ctx.model = model
+        ctx.sv = sv
+        return p
+
+    @staticmethod
+    def backward(ctx, dp):
+        model = ctx.model
+        flat = model._flat
+        g = torch.empty_like(flat)
+        dx = model.engine.backward(flat, g, ctx.sv, dp.contiguous(), need_dx=ctx.needs_input_grad[1])
+        ctx.sv = None
+        grads = [g[off:off + n].view(shape) for (off, n, shape) in model._slices]
+        return (None, dx, *grads)
+
+
+class Lightweight3DUNet(nn.Module):
+    """unet3d.py:146-229 — lightweight 3D U-Net (16 -> 32 -> 64 -> 128) for lesion segmentation."""
+
+    def __init__(self, in_channels=1, out_channels=1, start_channels=16,
+                 encoder_channels=[16, 32, 64, 128],
+                 use_depthwise_separable=True, use_grouped=True, groups=8,
+                 dropout_p=0.1):
+        super().__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.encoder_channels = encoder_channels
+        self.dropout_p = float(dropout_p) if dropout_p > 0 else 0.0
+        kw = dict(use_depthwise_separable=use_depthwise_separable, use_grouped=use_grouped,
+                  groups=groups, dropout_p=dropout_p)
+        self.init_conv = ResidualBlock(in_channels, encoder_channels[0],
+                                       use_depthwise_separable=use_depthwise_separable,
+                                       use_grouped=False, groups=groups, dropout_p=dropout_p)
+        self.down1 = DownBlock(encoder_channels[0], encoder_channels[1], **kw)
+        self.down2 = DownBlock(encoder_channels[1], encoder_channels[2], **kw)
+        self.down3 = DownBlock(encoder_channels[2], encoder_channels[3], **kw)
+        self.bottleneck = ResidualBlock(encoder_channels[3], encoder_channels[3], **kw)
+        self.up1 = UpBlock(encoder_channels[3], encoder_channels[2], **kw)
+        self.up2 = UpBlock(encoder_channels[2], encoder_channels[1], **kw)
+        self.up3 = UpBlock(encoder_channels[1], encoder_channels[0], **kw)
+        self.out_conv = nn.Conv3d(encoder_channels[0], out_channels, kernel_size=1)
+        self.sigmoid = nn.Sigmoid()
+
+        self.engine = _engine.UNetEngine(encoder_channels, in_channels, out_channels)
+        names = [n for n, _ in self.named_parameters()]
+        if names != [n for n, _ in self.engine.layout]:
+            raise AssertionError("parameter registration order diverged from the engine layout")
+        self._slices = [self.engine.offsets[n] for n in names]
+        self._flatten()
+
+    # -------------------------------------------------------------- flat parameter storage
+    def _flatten(self):
+        """Re-home every parameter as a view of one contiguous buffer (after init or .to())."""
+        params = list(self.parameters())
+        dev = params[0].device
+        dt = params[0].dtype
+        flat = torch.empty(self.engine.numel, device=dev, dtype=dt)
+        with torch.no_grad():
+            for p, (off, n, shape) in zip(params, self._slices):
+                flat[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = flat[off:off + n].view(shape)
+        self._flat = flat
+        self._rng_counter = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def _is_flat(self):
+        base = self._flat.data_ptr()
+        for p, (off, n, shape) in zip(self.parameters(), self._slices):
+            if p.data_ptr() != base + off * p.element_size() or p.device != self._flat.device:
+                return False
+        return True
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._flatten()
+        return out
+
+    def flat_parameters(self):
+        """The single fp32 buffer every parameter is a view of (kernel + optimizer + RCCL view)."""
+        if not self._is_flat():
+            self._flatten()
+        return self._flat
+
+    def param_slices(self):
+        return dict(zip([n for n, _ in self.named_parameters()], self._slices))
+
+    # -------------------------------------------------------------- forward
+    def forward(self, x):
+        flat = self.flat_parameters()
+        if not x.is_cuda or flat.device != x.device:
+            raise nat.NativeError(
+                f"Lightweight3DUNet (MI355X path) needs input and model on the same ROCm device; "
+                f"got input on {x.device}, model on {flat.device}.  There is no CPU fallback.")
+        if flat.dtype != torch.float32:
+            raise NotImplementedError("the MI355X path computes in fp32")
+        x = x.float()
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            return _UNetFunction.apply(self, x, *self.parameters())
+        p, _ = self.engine.forward(flat, x, training=self.training, dropout_p=self.dropout_p,
+                                   counter=self._rng_counter, save=False)
+        return p
+
+    def count_parameters(self):
+        """Count total and trainable parameters (unet3d.py:225-229)"""
+        total = sum(p.numel() for p in self.parameters())
+        trainable = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        return {"total": total, "trainable": trainable}

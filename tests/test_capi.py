@@ -1,0 +1,81 @@
+"""The C-ABI library builds, loads without a GPU and exports every symbol include/l3u.h declares;
+the ctypes signature table matches the header (no compute calls here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "l3u.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    funcs = {}
+    for m in re.finditer(r"\bint\s+(l3u_\w+)\s*\(([^)]*)\)\s*;", src, flags=re.S):
+        args = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+        funcs[m.group(1)] = args
+    return funcs
+
+
+def test_header_parses():
+    f = header_functions()
+    assert "l3u_dw3_fwd" in f and "l3u_pw_fwd" in f and "l3u_ftl_bwd" in f
+    assert len(f) >= 25
+
+
+def test_library_exports_every_header_symbol():
+    from light_unet import _native
+    lib = _native.load()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    # and nothing is bound that the header does not declare
+    assert set(_native.exported_symbols()) == set(header_functions())
+
+
+def test_ctypes_signatures_match_header():
+    from light_unet import _native
+    hf = header_functions()
+    kind = {"P": ctypes.c_void_p, "I": ctypes.c_int, "L": ctypes.c_longlong,
+            "F": ctypes.c_float, "D": ctypes.c_double, "U": ctypes.c_ulonglong}
+
+    def ctype_of(decl):
+        d = decl.replace("const ", "").strip()
+        if "*" in d or d.startswith("hipStream_t"):
+            return kind["P"]
+        t = d.rsplit(" ", 1)[0].strip()
+        return {"int": kind["I"], "long long": kind["L"], "float": kind["F"], "double": kind["D"],
+                "unsigned long long": kind["U"]}[t]
+
+    for name, args in hf.items():
+        bound = _native._SIGS[name]
+        assert len(bound) == len(args), name
+        for a, b in zip(args, bound):
+            assert ctype_of(a) is b, (name, a, b)
+
+
+def test_host_queries_without_gpu():
+    from light_unet import _native
+    assert _native.query("l3u_abi_version") == 1
+    assert _native.query("l3u_dw3_nchunk", 48) == 12
+    assert _native.query("l3u_dw3_nchunk", 6) == 1
+    assert _native.query("l3u_pw_stat_nsb", 16, 48 ** 3) == 108
+
+
+def test_no_cpu_fallback_in_product_package():
+    """The product package never imports the oracle."""
+    pkg = os.path.join(ROOT, "light-3d-unet-front_amd", "light_unet")
+    for dp, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dp, f)).read()
+                assert "oracle" not in src.replace("oracle/", ""), f
+
+
+def test_require_device_rejects_cpu():
+    import torch
+    from light_unet import _native
+    with pytest.raises(_native.NativeError):
+        _native.require_device(torch.zeros(3))

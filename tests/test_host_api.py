@@ -1,0 +1,91 @@
+"""Drop-in host API (no GPU): same constructor, submodule tree, state_dict keys/shapes, default
+initialisation and error behaviour as the reference light_unet.models (unet3d.py, losses.py)."""
+import numpy as np
+import pytest
+import torch
+
+
+def test_param_names_shapes_and_count(golden):
+    from light_unet.models.unet3d import Lightweight3DUNet
+    z = golden("model_b1_48.npz")
+    m = Lightweight3DUNet()
+    keys = [k[2:] for k in z.files if k.startswith("w/")]
+    sd = m.state_dict()
+    assert list(sd) == keys
+    for k in keys:
+        assert tuple(sd[k].shape) == z["w/" + k].shape
+    assert m.count_parameters() == {"total": 217228, "trainable": 217228}
+    m5 = Lightweight3DUNet(encoder_channels=[32, 64, 128, 256])
+    assert m5.count_parameters()["total"] == 812284
+
+
+def test_default_init_matches_reference_seed42(golden):
+    """torch.manual_seed(42) (trainer.py:44) gives the reference's initial weights bit for bit
+    (the goldens perturb only the InstanceNorm affine parameters)."""
+    from light_unet.models.unet3d import Lightweight3DUNet
+    z = golden("model_b2_32.npz")
+    torch.manual_seed(42)
+    m = Lightweight3DUNet(dropout_p=0.0)
+    for k, v in m.state_dict().items():
+        if ".norm" in k or ".shortcut.1." in k:
+            continue
+        assert np.array_equal(v.numpy(), z["w/" + k]), k
+
+
+def test_parameters_are_views_of_one_flat_buffer():
+    from light_unet.models.unet3d import Lightweight3DUNet
+    m = Lightweight3DUNet()
+    flat = m.flat_parameters()
+    assert flat.numel() == 217228
+    base = flat.data_ptr()
+    for (name, p), (off, n, shape) in zip(m.named_parameters(), m._slices):
+        assert p.data_ptr() == base + 4 * off and tuple(p.shape) == tuple(shape)
+    # load_state_dict keeps the aliasing
+    sd = {k: torch.randn_like(v) for k, v in m.state_dict().items()}
+    m.load_state_dict(sd)
+    assert m._is_flat()
+    assert torch.equal(m.init_conv.conv1.depthwise.weight, sd["init_conv.conv1.depthwise.weight"])
+    assert torch.equal(flat[:27], sd["init_conv.conv1.depthwise.weight"].reshape(-1))
+    # dtype conversion re-flattens
+    m.double()
+    assert m._is_flat() and m.flat_parameters().dtype == torch.float64
+
+
+def test_forward_on_cpu_fails_loudly():
+    from light_unet import _native
+    from light_unet.models.unet3d import Lightweight3DUNet
+    m = Lightweight3DUNet()
+    with pytest.raises(_native.NativeError):
+        m(torch.zeros(1, 1, 48, 48, 48))
+
+
+def test_unsupported_configs_raise():
+    from light_unet.models.unet3d import Lightweight3DUNet
+    with pytest.raises(NotImplementedError):
+        Lightweight3DUNet(use_depthwise_separable=False)
+
+
+def test_loss_factory_and_errors():
+    from light_unet.models import losses
+    f = losses.get_loss_function({"name": "FocalTverskyLoss", "alpha": 0.7, "beta": 0.3, "gamma": 0.75})
+    assert isinstance(f, losses.FocalTverskyLoss) and f.gamma == 0.75
+    assert isinstance(losses.get_loss_function({"name": "DiceLoss"}), losses.DiceLoss)
+    assert isinstance(losses.get_loss_function({"use_combined_loss": True}), losses.CombinedLoss)
+    with pytest.raises(ValueError):
+        losses.get_loss_function({"name": "Nope"})
+    with pytest.raises(AssertionError):
+        losses.FocalTverskyLoss(alpha=0.6, beta=0.3)
+    with pytest.raises(Exception):
+        f(torch.rand(1, 1, 4, 4, 4), torch.rand(1, 1, 4, 4, 4))   # CPU tensors: no fallback
+    with pytest.raises(RuntimeError):
+        f(torch.rand(1, 1, 4, 4, 8)[..., ::2], torch.rand(1, 1, 4, 4, 4))  # non-contiguous (view)
+
+
+def test_engine_rejects_bad_shapes():
+    from light_unet.engine import UNetEngine
+    with pytest.raises(NotImplementedError):
+        UNetEngine.check_shape(torch.zeros(1, 1, 44, 48, 48))
+    with pytest.raises(ValueError):
+        UNetEngine.check_shape(torch.zeros(1, 2, 48, 48, 48))
+    with pytest.raises(NotImplementedError):
+        UNetEngine.check_shape(torch.zeros(1, 1, 8, 72, 72))

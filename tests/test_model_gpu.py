@@ -1,0 +1,207 @@
+"""Whole-network parity of the MI355X path against the golden fixtures made by the REFERENCE
+(tests/golden/make_goldens.py imports /root/reference by file path, fp64) and against the oracle.
+
+Tolerances (written here, as the north star asks):
+  * output probabilities: |HIP - golden| <= 1e-3 absolute (north star: 1e-3 fp32); observed ~1e-6.
+  * loss: |HIP - golden| <= 1e-4 relative.
+  * parameter gradients: the relative L2 error of the whole gradient vector (217,228 entries) vs
+    the fp64 golden must be <= max(1e-3, 2 * e32), e32 being the same error of the fp32 CPU
+    oracle (torch aten = the reference's own fp32 arithmetic) on the same inputs, and every
+    tensor's relative L2 error <= max(1e-2, 3 * its e32).  Why not an elementwise bound: at 48^3
+    about 1-4 of the 1.77M InstanceNorm outputs of a block lie within 1e-6 of the LeakyReLU kink,
+    and fp32 rounding (any fp32 implementation, the reference's included) decides which branch
+    they take; each flip changes that voxel's gradient 100x and spreads through the backward
+    convolutions (measured: HIP global error 7.6e-4 vs 1.1e-3 for CPU fp32 at 48^3; both 1.4e-5 at
+    32^3, tools/diag_model.py).  Scale-invariant tensors (1-channel conv -> InstanceNorm, e.g.
+    init_conv.shortcut.0.weight) have a true gradient ~0, which the e32 term absorbs.
+  * thresholded masks (p >= thr): bit-exact on every voxel farther than 1e-4 from the threshold.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import unet_oracle as U
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(z, enc, cuda, dropout_p=0.0):
+    from light_unet.models.unet3d import Lightweight3DUNet
+    m = Lightweight3DUNet(encoder_channels=list(enc), dropout_p=dropout_p)
+    sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w/")}
+    m.load_state_dict(sd)
+    return m.to(cuda), sd
+
+
+def _grad_errs(grads, z):
+    """per-tensor relative L2 errors and the global relative L2 error vs the fp64 golden"""
+    errs, num, den = {}, 0.0, 0.0
+    for k, g in grads.items():
+        gr = z["g/" + k].astype(np.float64)
+        d = np.linalg.norm(g.astype(np.float64) - gr)
+        errs[k] = d / max(np.linalg.norm(gr), 1e-30)
+        num += d * d
+        den += float(np.sum(gr * gr))
+    return errs, (num / den) ** 0.5
+
+
+def _cpu_fp32_errs(sd, z):
+    params = {k: v.clone().float().requires_grad_(True) for k, v in sd.items()}
+    out = U.unet_forward(params, torch.from_numpy(z["x"]))
+    loss = U.focal_tversky(out, torch.from_numpy(z["target"]))
+    loss.backward()
+    return _grad_errs({k: p.grad.numpy() for k, p in params.items()}, z)
+
+
+@pytest.mark.parametrize("fname", ["model_b2_32.npz", "model_b1_48.npz"])
+def test_model_matches_reference_golden(cuda, golden, fname):
+    from light_unet.models.losses import get_loss_function
+    z = golden(fname)
+    model, sd = _model(z, (16, 32, 64, 128), cuda)
+    model.train()
+    x = torch.from_numpy(z["x"]).to(cuda)
+    t = torch.from_numpy(z["target"]).to(cuda)
+    crit = get_loss_function({"name": "FocalTverskyLoss", "alpha": 0.7, "beta": 0.3, "gamma": 0.75})
+    out = model(x)
+    loss = crit(out, t)
+    model.zero_grad(set_to_none=True)
+    loss.backward()
+    torch.cuda.synchronize()
+    o = out.detach().cpu().numpy()
+    assert np.abs(o - z["out"]).max() <= 1e-3
+    assert abs(loss.item() - float(z["loss"])) <= 1e-4 * abs(float(z["loss"]))
+    grads = {k: p.grad.detach().cpu().numpy() for k, p in model.named_parameters()}
+    errs, gerr = _grad_errs(grads, z)
+    e32, g32 = _cpu_fp32_errs(sd, z)
+    assert gerr <= max(1e-3, 2 * g32), (gerr, g32)
+    bad = {k: (errs[k], e32[k]) for k in errs if errs[k] > max(1e-2, 3 * e32[k])}
+    assert not bad, f"gradient errors above tolerance: {bad}"
+    print(f"{fname}: out err {np.abs(o - z['out']).max():.2e}, grad L2 err {gerr:.2e} "
+          f"(cpu fp32 {g32:.2e}), worst tensor {max(errs.items(), key=lambda kv: kv[1])}")
+
+
+def test_model_c32_64_golden(cuda, golden):
+    """Config 5 architecture (32->256, 812,284 params) at 64^3: sampled outputs + grad norms."""
+    from light_unet.models.losses import FocalTverskyLoss
+    z = golden("model_c32_b1_64.npz")
+    model, _ = _model(z, (32, 64, 128, 256), cuda)
+    assert model.count_parameters()["total"] == int(z["n_params"]) == 812284
+    x = torch.from_numpy(z["x"]).to(cuda)
+    t = torch.from_numpy(z["target"]).to(cuda)
+    out = model(x)
+    loss = FocalTverskyLoss()(out, t)
+    loss.backward()
+    o = out.detach().cpu().numpy().reshape(-1)
+    assert np.abs(o[z["out_idx"]] - z["out_sample"]).max() <= 1e-3
+    assert abs(o.astype(np.float64).sum() - float(z["out_sum"])) <= 1e-5 * float(z["out_sum"])
+    assert abs(loss.item() - float(z["loss"])) <= 1e-4
+    gscale = max(float(z["gnorm/" + k]) for k, _ in model.named_parameters())
+    for k, p in model.named_parameters():
+        gn = float(np.linalg.norm(p.grad.detach().cpu().numpy().ravel()))
+        ref = float(z["gnorm/" + k])
+        assert abs(gn - ref) <= 1e-2 * ref + 1e-4 * gscale, (k, gn, ref)
+
+
+def test_dropout_masks_match_oracle(cuda, golden):
+    """Dropout3d on: the kernels' channel masks, fed to the oracle, reproduce the output."""
+    z = golden("model_b2_32.npz")
+    model, sd = _model(z, (16, 32, 64, 128), cuda, dropout_p=0.1)
+    model.train()
+    x = torch.from_numpy(z["x"]).to(cuda)
+    eng = model.engine
+    p, sv = eng.forward(model.flat_parameters(), x, training=True, dropout_p=0.1,
+                        counter=model._rng_counter)
+    masks = {}
+    total = dropped = 0
+    for name, b in sv["blk"].items():
+        k = b["recs"][1].view(x.shape[0], -1, 8)[..., 4].cpu()
+        uk = np.unique(k.numpy())
+        assert all(np.isclose(v, 0.0) or np.isclose(v, 1 / 0.9, rtol=1e-6) for v in uk), uk
+        masks[name] = (k > 0).double()
+        total += k.numel()
+        dropped += int((k == 0).sum())
+    assert 0 < dropped < total
+    ref = U.unet_forward({k: v.double() for k, v in sd.items()}, torch.from_numpy(z["x"]).double(),
+                         drop_masks=masks, drop_p=0.1)
+    assert np.abs(p.cpu().numpy() - ref.numpy()).max() <= 1e-3
+    # eval mode: no dropout, same as the p=0 golden
+    model.eval()
+    with torch.no_grad():
+        pe = model(x)
+    assert np.abs(pe.cpu().numpy() - z["out"]).max() <= 1e-3
+
+
+def test_backward_is_deterministic(cuda, golden):
+    z = golden("model_b2_32.npz")
+    model, _ = _model(z, (16, 32, 64, 128), cuda)
+    x = torch.from_numpy(z["x"]).to(cuda)
+    t = torch.from_numpy(z["target"]).to(cuda)
+    from light_unet.models.losses import FocalTverskyLoss
+    crit = FocalTverskyLoss()
+    outs = []
+    for _ in range(2):
+        model.zero_grad(set_to_none=True)
+        loss = crit(model(x), t)
+        loss.backward()
+        outs.append(torch.cat([p.grad.reshape(-1) for p in model.parameters()]).cpu())
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_trainstep_eager_graph_and_autograd_agree(cuda, golden):
+    """The engine-level TrainStep (bench path), its hipGraph replay and the autograd drop-in path
+    (model + criterion + torch.optim.AdamW, as trainer.py:227-232) follow the same trajectory."""
+    from light_unet.models.unet3d import Lightweight3DUNet
+    from light_unet.models.losses import FocalTverskyLoss
+    from light_unet.train_step import TrainStep
+    z = golden("model_b2_32.npz")
+    sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w/")}
+    x = torch.from_numpy(z["x"]).to(cuda)
+    t = torch.from_numpy(z["target"]).to(cuda)
+
+    def fresh():
+        m = Lightweight3DUNet(dropout_p=0.0)
+        m.load_state_dict(sd)
+        return m.to(cuda).train()
+
+    steps = 4
+    # (a) autograd drop-in path with torch.optim.AdamW
+    m_a = fresh()
+    opt = torch.optim.AdamW(m_a.parameters(), lr=1e-4, weight_decay=1e-5)
+    crit = FocalTverskyLoss()
+    la = []
+    for _ in range(steps):
+        loss = crit(m_a(x), t)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        la.append(loss.item())
+    # (b) TrainStep eager
+    m_b = fresh()
+    ts = TrainStep(m_b, lr=1e-4, weight_decay=1e-5)
+    lb = [ts(x, t).item() for _ in range(steps)]
+    # (c) TrainStep captured in a hipGraph (2 warmup steps are part of the trajectory)
+    m_c = fresh()
+    tc = TrainStep(m_c, lr=1e-4, weight_decay=1e-5)
+    xs, tsb = x.clone(), t.clone()
+    tc.capture(xs, tsb, warmup=2)
+    lc = []
+    for _ in range(steps - 2):
+        lc.append(tc.replay().item())
+    np.testing.assert_allclose(la, lb, rtol=1e-5)
+    np.testing.assert_allclose(lb[2:], lc, rtol=1e-6)
+    pa = m_a.flat_parameters().detach()
+    pb = m_b.flat_parameters().detach()
+    pc = m_c.flat_parameters().detach()
+    assert (pa - pb).abs().max().item() <= 3e-4 * steps
+    assert torch.equal(pb, pc), "graph replay must be bitwise identical to eager"
+
+
+def test_state_dict_roundtrip_and_reference_keys(cuda, golden):
+    z = golden("model_b1_48.npz")
+    model, sd = _model(z, (16, 32, 64, 128), cuda)
+    out_sd = model.state_dict()
+    assert list(out_sd) == [k[2:] for k in z.files if k.startswith("w/")]
+    for k, v in out_sd.items():
+        assert torch.equal(v.cpu(), sd[k])
+    with pytest.raises(Exception):
+        model(torch.zeros(1, 1, 48, 48, 48))   # CPU input on the MI355X path fails loudly

@@ -1,0 +1,488 @@
+"""Per-kernel numerics of the C-ABI library against float64 torch-CPU references of the same ops.
+
+Every kernel is called through the C ABI (light_unet._native -> libl3u_hip.so).  Shapes include
+ragged volumes (odd, non-multiple-of-4 sizes), strided batch views (zero-copy concat) and the
+48^3 / 24^3 production shapes.  Tolerances: fp32 kernels vs fp64 references, rel 1e-5 .. 1e-4 of
+the output scale (each output is a short fp32 dot product / stencil sum).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SLOPE = 0.01
+
+
+def nat():
+    from light_unet import _native
+    return _native
+
+
+def st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def close(a, b, rtol=1e-5, what=""):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    scale = max(b.abs().max().item(), 1e-30)
+    err = (a - b).abs().max().item() / scale
+    assert err <= rtol, f"{what}: max err {err:.3e} (rel to {scale:.3e}) > {rtol}"
+
+
+def make_rec(N, C, gen, drop=False):
+    mean = torch.randn(N, C, generator=gen, dtype=torch.float64) * 0.3
+    rstd = 0.5 + torch.rand(N, C, generator=gen, dtype=torch.float64)
+    g = 1 + 0.2 * torch.randn(N, C, generator=gen, dtype=torch.float64)
+    b = 0.2 * torch.randn(N, C, generator=gen, dtype=torch.float64)
+    k = torch.ones(N, C, dtype=torch.float64)
+    if drop:
+        k = torch.where(torch.rand(N, C, generator=gen) < 0.3, 0.0, 1 / 0.7).double()
+    rec = torch.zeros(N, C, 8, dtype=torch.float64)
+    rec[..., 0], rec[..., 1] = mean, rstd
+    rec[..., 2] = k * g * rstd
+    rec[..., 3] = k * b
+    rec[..., 4], rec[..., 5], rec[..., 6] = k, g, b
+    return rec
+
+
+def xform_ref(y, rec):
+    sc = rec[..., 2][:, :, None, None, None]
+    sh = rec[..., 3][:, :, None, None, None]
+    mu = rec[..., 0][:, :, None, None, None]
+    return F.leaky_relu(sc * (y - mu) + sh, SLOPE)
+
+
+# ------------------------------------------------------------------------------ depthwise
+DW_SHAPES = [(2, 3, 7, 6, 9), (1, 2, 5, 5, 5), (2, 4, 12, 12, 12), (4, 16, 48, 48, 48),
+             (2, 8, 6, 6, 6), (1, 2, 24, 24, 24), (1, 1, 64, 64, 64)]
+
+
+@pytest.mark.parametrize("shape", DW_SHAPES)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_dw3_fwd(cuda, shape, mode):
+    N, C, D, H, W = shape
+    gen = torch.Generator().manual_seed(1)
+    x = torch.randn(shape, generator=gen, dtype=torch.float64)
+    w = torch.randn(C, 1, 3, 3, 3, generator=gen, dtype=torch.float64)
+    rec = make_rec(N, C, gen, drop=True) if mode else None
+    a = xform_ref(x, rec) if mode else x
+    ref = F.conv3d(a, w, padding=1, groups=C)
+    # strided input view: embed x in a 2C-channel buffer (upper half) like a concat buffer
+    S = D * H * W
+    buf = torch.zeros(N, 2 * C, S, device=cuda)
+    buf[:, C:] = x.reshape(N, C, S).float().to(cuda)
+    y = torch.full((N, C, D, H, W), float("nan"), device=cuda)
+    wd = w.float().reshape(C, 27).to(cuda)
+    recd = rec.float().to(cuda) if mode else None
+    nat().call("l3u_dw3_fwd", buf.data_ptr() + 4 * C * S, 2 * C * S, wd.data_ptr(),
+               recd.data_ptr() if mode else None, y.data_ptr(), C * S, N, C, D, H, W, st())
+    torch.cuda.synchronize()
+    close(y, ref, 2e-6, f"dw3_fwd{shape} mode{mode}")
+
+
+@pytest.mark.parametrize("shape", DW_SHAPES)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_dw3_bwd(cuda, shape, mode):
+    N, C, D, H, W = shape
+    S = D * H * W
+    gen = torch.Generator().manual_seed(2)
+    x = torch.randn(shape, generator=gen, dtype=torch.float64)
+    w = torch.randn(C, 1, 3, 3, 3, generator=gen, dtype=torch.float64)
+    dz = torch.randn(shape, generator=gen, dtype=torch.float64)
+    rec = make_rec(N, C, gen, drop=True) if mode else None
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    if mode:
+        # reference: pre = IN-affine output (un-dropped), a = k * lrelu(pre)
+        k = rec[..., 4][:, :, None, None, None]
+        sc = (rec[..., 1] * rec[..., 5])[:, :, None, None, None]
+        sh = (rec[..., 6] - rec[..., 5] * rec[..., 1] * rec[..., 0])[:, :, None, None, None]
+        pre = (sc * xr + sh).detach().requires_grad_(True)
+        a = k * F.leaky_relu(pre, SLOPE)
+        out = F.conv3d(a, wr, padding=1, groups=C)
+        out.backward(dz)
+        dpre_ref = pre.grad
+        xhat = (x - rec[..., 0][:, :, None, None, None]) * rec[..., 1][:, :, None, None, None]
+        s1_ref = dpre_ref.sum(dim=(2, 3, 4))
+        s2_ref = (dpre_ref * xhat).sum(dim=(2, 3, 4))
+    else:
+        out = F.conv3d(xr, wr, padding=1, groups=C)
+        out.backward(dz)
+    nch = nat().query("l3u_dw3_nchunk", D)
+    xd = x.float().to(cuda)
+    dzd = dz.float().to(cuda)
+    wd = w.float().reshape(C, 27).to(cuda)
+    init = torch.randn(shape, generator=gen).to(cuda)
+    dx = init.clone()
+    dwp = torch.full((C * N * nch * 27,), float("nan"), device=cuda)
+    inp = torch.full((C * N * nch * 2,), float("nan"), dtype=torch.float64, device=cuda) if mode else None
+    recd = rec.float().to(cuda) if mode else None
+    acc = 0 if mode else 1
+    nat().call("l3u_dw3_bwd", dzd.data_ptr(), C * S, xd.data_ptr(), C * S, wd.data_ptr(),
+               recd.data_ptr() if mode else None, dx.data_ptr(), C * S, acc, dwp.data_ptr(),
+               inp.data_ptr() if mode else None, N, C, D, H, W, st())
+    torch.cuda.synchronize()
+    dwsum = dwp.view(C, N * nch, 27).double().sum(1).view(C, 1, 3, 3, 3)
+    close(dwsum, wr.grad, 1e-5, f"dw3_bwd dW {shape} mode{mode}")
+    if mode:
+        close(dx, dpre_ref, 2e-6, "dpre")
+        ip = inp.view(C, N, nch, 2).double().sum(2)
+        close(ip[..., 0].t(), s1_ref, 1e-5, "sum dpre")
+        close(ip[..., 1].t(), s2_ref, 1e-5, "sum dpre*xhat")
+    else:
+        close(dx, xr.grad + init.double().cpu(), 2e-6, f"dw3_bwd dX {shape}")
+
+
+# ------------------------------------------------------------------------------ pointwise GEMM
+PW_CASES = [(2, 1, 16, 7 * 6 * 9), (2, 16, 16, 1000), (4, 32, 16, 13824), (3, 16, 32, 216),
+            (2, 64, 128, 1728), (2, 128, 64, 216), (1, 128, 128, 216), (2, 32, 512, 216),
+            (1, 5, 7, 37)]
+
+
+@pytest.mark.parametrize("case", PW_CASES)
+@pytest.mark.parametrize("layout", [0, 1])
+def test_pw_fwd(cuda, case, layout):
+    N, K, J, S = case
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(N, K, S, generator=gen, dtype=torch.float64)
+    wm = torch.randn(J, K, generator=gen, dtype=torch.float64)   # Wm[j][k]
+    bias = torch.randn(J, generator=gen, dtype=torch.float64)
+    old = torch.randn(N, J, S, generator=gen, dtype=torch.float64)
+    ref = torch.einsum("jk,nks->njs", wm, x) + bias[None, :, None]
+    w_store = wm if layout == 0 else wm.t().contiguous()
+    xd, wdv, bd = x.float().to(cuda), w_store.float().contiguous().to(cuda), bias.float().to(cuda)
+    y = torch.full((N, J, S), float("nan"), device=cuda)
+    nsb = nat().query("l3u_pw_stat_nsb", J, S)
+    part = torch.full((N * J * nsb * 3,), float("nan"), device=cuda)
+    nat().call("l3u_pw_fwd", xd.data_ptr(), K * S, wdv.data_ptr(), layout, bd.data_ptr(),
+               y.data_ptr(), J * S, 0, part.data_ptr(), N, K, J, S, st())
+    torch.cuda.synchronize()
+    close(y, ref, 1e-5, f"pw_fwd {case} L{layout}")
+    # merged statistics == torch mean / biased var per (n, j)
+    p = part.view(N, J, nsb, 3).double().cpu()
+    cnt = p[..., 0].sum(-1)
+    mean = (p[..., 0] * p[..., 1]).sum(-1) / cnt
+    m2 = p[..., 2].sum(-1) + (p[..., 0] * (p[..., 1] - mean[..., None]) ** 2).sum(-1)
+    var = m2 / cnt
+    assert torch.all(cnt == S)
+    close(mean, ref.mean(-1), 1e-5, "stat mean")
+    close(var, ref.var(-1, unbiased=False), 1e-4, "stat var")
+    # accumulate, no bias, no stats
+    y2 = old.float().to(cuda)
+    nat().call("l3u_pw_fwd", xd.data_ptr(), K * S, wdv.data_ptr(), layout, None, y2.data_ptr(),
+               J * S, 1, None, N, K, J, S, st())
+    torch.cuda.synchronize()
+    close(y2, ref - bias[None, :, None] + old, 1e-5, "pw_fwd accumulate")
+
+
+@pytest.mark.parametrize("case", PW_CASES)
+def test_pw_bwd_weight(cuda, case):
+    N, K, J, S = case
+    gen = torch.Generator().manual_seed(4)
+    x = torch.randn(N, K, S, generator=gen, dtype=torch.float64)
+    dy = torch.randn(N, J, S, generator=gen, dtype=torch.float64)
+    ref = torch.einsum("njs,nks->jk", dy, x)
+    P = nat().query("l3u_pw_bwd_weight_nparts", N, S)
+    part = torch.full((P * J * K,), float("nan"), device=cuda)
+    xd, dyd = x.float().to(cuda), dy.float().to(cuda)
+    nat().call("l3u_pw_bwd_weight", dyd.data_ptr(), J * S, xd.data_ptr(), K * S, part.data_ptr(),
+               N, J, K, S, st())
+    torch.cuda.synchronize()
+    close(part.view(P, J, K).double().sum(0), ref, 1e-5, f"pw_bwd_weight {case}")
+
+
+# ------------------------------------------------------------------------------ InstanceNorm
+def test_in_finalize_and_dropout(cuda):
+    N, C, nsb = 3, 5, 7
+    gen = torch.Generator().manual_seed(5)
+    vals = torch.randn(N, C, nsb, 40, generator=gen, dtype=torch.float64) * 2 + 1
+    part = torch.stack([torch.full((N, C, nsb), 40.0, dtype=torch.float64), vals.mean(-1),
+                        ((vals - vals.mean(-1, keepdim=True)) ** 2).sum(-1)], -1)
+    gamma = torch.randn(C, generator=gen, dtype=torch.float64)
+    beta = torch.randn(C, generator=gen, dtype=torch.float64)
+    rec = torch.empty(N * C * 8, device=cuda)
+    pd = part.float().to(cuda)
+    gd, bd = gamma.float().to(cuda), beta.float().to(cuda)
+    nat().call("l3u_in_finalize", pd.data_ptr(), nsb, gd.data_ptr(), bd.data_ptr(), 0.0, 1, None, 0,
+               rec.data_ptr(), N, C, st())
+    torch.cuda.synchronize()
+    r = rec.view(N, C, 8).double().cpu()
+    flat = vals.reshape(N, C, -1)
+    mean, var = flat.mean(-1), flat.var(-1, unbiased=False)
+    rstd = 1 / torch.sqrt(var + 1e-5)
+    close(r[..., 0], mean, 1e-5, "mean")
+    close(r[..., 1], rstd, 1e-5, "rstd")
+    close(r[..., 2], gamma * rstd, 1e-5, "scale")
+    close(r[..., 3], beta.expand(N, C), 1e-6, "shift")
+    # dropout: channel keep mask with scale 1/(1-p), fraction ~ p, deterministic per step
+    N2, C2 = 64, 64
+    part2 = torch.tensor([1.0, 0.0, 1.0]).repeat(N2 * C2).to(cuda)
+    step = torch.tensor([7], dtype=torch.int32, device=cuda)
+    recs = []
+    for _ in range(2):
+        rr = torch.empty(N2 * C2 * 8, device=cuda)
+        nat().call("l3u_in_finalize", part2.data_ptr(), 1, None, None, 0.25, 123, step.data_ptr(), 3,
+                   rr.data_ptr(), N2, C2, st())
+        recs.append(rr.view(N2, C2, 8).cpu())
+    k = recs[0][..., 4]
+    assert torch.equal(recs[0], recs[1])
+    uk = np.unique(k.numpy())
+    assert all(np.isclose(v, 0.0) or np.isclose(v, 1 / 0.75, rtol=1e-6) for v in uk), uk
+    frac = (k == 0).double().mean().item()
+    assert 0.2 < frac < 0.3, frac
+    step += 1
+    rr = torch.empty(N2 * C2 * 8, device=cuda)
+    nat().call("l3u_in_finalize", part2.data_ptr(), 1, None, None, 0.25, 123, step.data_ptr(), 3,
+               rr.data_ptr(), N2, C2, st())
+    assert not torch.equal(rr.view(N2, C2, 8).cpu()[..., 4], k)
+
+
+@pytest.mark.parametrize("shortcut", [True, False])
+@pytest.mark.parametrize("shape", [(2, 3, 5, 6, 7), (2, 16, 12, 12, 12), (4, 16, 48, 48, 48)])
+def test_norm_act_fwd_bwd(cuda, shape, shortcut):
+    N, C, D, H, W = shape
+    S = D * H * W
+    gen = torch.Generator().manual_seed(6)
+    y2 = torch.randn(N, C, S, generator=gen, dtype=torch.float64)
+    r = torch.randn(N, C, S, generator=gen, dtype=torch.float64)
+    dout = torch.randn(N, C, S, generator=gen, dtype=torch.float64)
+    g2 = 1 + 0.3 * torch.randn(C, generator=gen, dtype=torch.float64)
+    b2 = 0.3 * torch.randn(C, generator=gen, dtype=torch.float64)
+    gr = 1 + 0.3 * torch.randn(C, generator=gen, dtype=torch.float64)
+    br = 0.3 * torch.randn(C, generator=gen, dtype=torch.float64)
+    y2r, rr = y2.clone().requires_grad_(True), r.clone().requires_grad_(True)
+    g2r, b2r, grr, brr = (t.clone().requires_grad_(True) for t in (g2, b2, gr, br))
+    res = F.instance_norm(rr, weight=grr, bias=brr, eps=1e-5) if shortcut else rr
+    out = F.leaky_relu(F.instance_norm(y2r, weight=g2r, bias=b2r, eps=1e-5) + res, SLOPE)
+    out.backward(dout)
+
+    def rec_of(v, g, b):
+        m = v.mean(-1)
+        rs = 1 / torch.sqrt(v.var(-1, unbiased=False) + 1e-5)
+        rc = torch.zeros(N, C, 8, dtype=torch.float64)
+        rc[..., 0], rc[..., 1] = m, rs
+        rc[..., 2] = g * rs
+        rc[..., 3] = b
+        rc[..., 4], rc[..., 5], rc[..., 6] = 1, g.expand(N, C), b.expand(N, C)
+        return rc.float().to(cuda)
+
+    rec2 = rec_of(y2, g2, b2)
+    recr = rec_of(r, gr, br) if shortcut else None
+    y2d, rd, dd = y2.float().to(cuda), r.float().to(cuda), dout.float().to(cuda)
+    o = torch.empty(N, C, S, device=cuda)
+    nat().call("l3u_norm_act_fwd", y2d.data_ptr(), C * S, rec2.data_ptr(), rd.data_ptr(), C * S,
+               recr.data_ptr() if shortcut else None, o.data_ptr(), C * S, N, C, S, st())
+    nb = nat().query("l3u_norm_act_nblocks", S)
+    part = torch.empty(C * N * nb * 3, dtype=torch.float64, device=cuda)
+    nat().call("l3u_norm_act_bwd_reduce", dd.data_ptr(), C * S, o.data_ptr(), C * S, y2d.data_ptr(),
+               C * S, rec2.data_ptr(), rd.data_ptr(), C * S, recr.data_ptr() if shortcut else None,
+               part.data_ptr(), N, C, S, st())
+    dy2 = torch.empty(N, C, S, device=cuda)
+    dr = torch.empty(N, C, S, device=cuda)
+    nat().call("l3u_norm_act_bwd_apply", dd.data_ptr(), C * S, o.data_ptr(), C * S,
+               y2d.data_ptr(), C * S, rec2.data_ptr(), rd.data_ptr(), C * S,
+               recr.data_ptr() if shortcut else None, part.data_ptr(), dy2.data_ptr(), C * S,
+               dr.data_ptr(), C * S, N, C, S, st())
+    torch.cuda.synchronize()
+    close(o, out, 2e-6, "norm_act out")
+    close(dy2, y2r.grad, 1e-4, "dy2")
+    close(dr, rr.grad, 1e-4, "dr")
+    p = part.view(C, N, nb, 3).double().sum((1, 2)).cpu()
+    close(p[:, 0], b2r.grad, 1e-5, "dbeta2")
+    close(p[:, 1], g2r.grad, 1e-5, "dgamma2")
+    if shortcut:
+        close(p[:, 2], grr.grad, 1e-5, "dgamma_r")
+
+
+def test_in_bwd_apply(cuda):
+    N, C, D, H, W = 2, 4, 6, 5, 7
+    S = D * H * W
+    gen = torch.Generator().manual_seed(7)
+    y = torch.randn(N, C, S, generator=gen, dtype=torch.float64)
+    dpre = torch.randn(N, C, S, generator=gen, dtype=torch.float64)
+    g = 1 + 0.3 * torch.randn(C, generator=gen, dtype=torch.float64)
+    b = 0.3 * torch.randn(C, generator=gen, dtype=torch.float64)
+    yr = y.clone().requires_grad_(True)
+    out = F.instance_norm(yr, weight=g, bias=b, eps=1e-5)
+    out.backward(dpre)
+    m = y.mean(-1)
+    rs = 1 / torch.sqrt(y.var(-1, unbiased=False) + 1e-5)
+    rec = torch.zeros(N, C, 8, dtype=torch.float64)
+    rec[..., 0], rec[..., 1], rec[..., 5] = m, rs, g.expand(N, C)
+    xhat = (y - m[..., None]) * rs[..., None]
+    nch = 3
+    part = torch.zeros(C, N, nch, 2, dtype=torch.float64)
+    part[:, :, 0, 0] = dpre.sum(-1).t()
+    part[:, :, 0, 1] = (dpre * xhat).sum(-1).t()
+    dd, yd = dpre.float().to(cuda), y.float().to(cuda)
+    recd, pd = rec.float().to(cuda), part.to(cuda)
+    nat().call("l3u_in_bwd_apply", dd.data_ptr(), C * S, yd.data_ptr(), C * S, recd.data_ptr(),
+               pd.data_ptr(), nch, dd.data_ptr(), C * S, N, C, S, st())
+    torch.cuda.synchronize()
+    close(dd, yr.grad, 1e-5, "in_bwd_apply")
+
+
+# ------------------------------------------------------------------------------ pool / convT
+@pytest.mark.parametrize("shape", [(2, 3, 6, 8, 10), (4, 16, 48, 48, 48), (1, 2, 7, 5, 9)])
+def test_maxpool(cuda, shape):
+    N, C, D, H, W = shape
+    gen = torch.Generator().manual_seed(8)
+    x = torch.randn(shape, generator=gen, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool3d(xr, 2, 2)
+    dy = torch.randn(y.shape, generator=gen, dtype=torch.float64)
+    add = torch.randn(shape, generator=gen, dtype=torch.float64)
+    y.backward(dy)
+    So = y.shape[2] * y.shape[3] * y.shape[4]
+    S = D * H * W
+    xd = x.float().to(cuda)
+    yd = torch.empty(N, C, So, device=cuda)
+    idx = torch.empty(N, C, So, dtype=torch.uint8, device=cuda)
+    nat().call("l3u_maxpool2_fwd", xd.data_ptr(), C * S, yd.data_ptr(), C * So, idx.data_ptr(),
+               N, C, D, H, W, st())
+    dyd, ad = dy.float().to(cuda), add.float().to(cuda)
+    dx = torch.empty(N, C, S, device=cuda)
+    nat().call("l3u_maxpool2_bwd", dyd.data_ptr(), C * So, idx.data_ptr(), ad.data_ptr(), C * S,
+               dx.data_ptr(), C * S, N, C, D, H, W, st())
+    torch.cuda.synchronize()
+    close(yd.view(y.shape), y, 1e-7, "maxpool fwd")
+    close(dx.view(shape), xr.grad + add, 1e-6, "maxpool bwd")
+
+
+@pytest.mark.parametrize("case", [(2, 8, 4, 3, 4, 5), (4, 32, 16, 24, 24, 24), (2, 128, 64, 6, 6, 6)])
+def test_convt(cuda, case):
+    N, Ci, Co, D, H, W = case
+    Si = D * H * W
+    So = 8 * Si
+    gen = torch.Generator().manual_seed(9)
+    x = torch.randn(N, Ci, D, H, W, generator=gen, dtype=torch.float64)
+    w = torch.randn(Ci, Co, 2, 2, 2, generator=gen, dtype=torch.float64)
+    b = torch.randn(Co, generator=gen, dtype=torch.float64)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    y = F.conv_transpose3d(xr, wr, br, stride=2)
+    dy = torch.randn(y.shape, generator=gen, dtype=torch.float64)
+    y.backward(dy)
+    xd, wd, bd = x.float().to(cuda), w.float().to(cuda), b.float().to(cuda)
+    yp = torch.empty(N, Co * 8, Si, device=cuda)
+    nat().call("l3u_pw_fwd", xd.data_ptr(), Ci * Si, wd.data_ptr(), 1, None, yp.data_ptr(),
+               Co * 8 * Si, 0, None, N, Ci, Co * 8, Si, st())
+    # write into the lower half of a concat buffer
+    cat = torch.zeros(N, 2 * Co, So, device=cuda)
+    nat().call("l3u_convt_d2s", yp.data_ptr(), bd.data_ptr(), cat.data_ptr(), 2 * Co * So, N, Co,
+               D, H, W, st())
+    dcat = torch.zeros(N, 2 * Co, So, device=cuda)
+    dcat[:, :Co] = dy.reshape(N, Co, So).float().to(cuda)
+    dyp = torch.empty(N, Co * 8, Si, device=cuda)
+    nat().call("l3u_convt_s2d", dcat.data_ptr(), 2 * Co * So, dyp.data_ptr(), N, Co, D, H, W, st())
+    dx = torch.empty(N, Ci, Si, device=cuda)
+    nat().call("l3u_pw_fwd", dyp.data_ptr(), Co * 8 * Si, wd.data_ptr(), 0, None, dx.data_ptr(),
+               Ci * Si, 0, None, N, Co * 8, Ci, Si, st())
+    P = nat().query("l3u_pw_bwd_weight_nparts", N, Si)
+    part = torch.empty(P * Ci * Co * 8, device=cuda)
+    nat().call("l3u_pw_bwd_weight", xd.data_ptr(), Ci * Si, dyp.data_ptr(), Co * 8 * Si,
+               part.data_ptr(), N, Ci, Co * 8, Si, st())
+    ncs = nat().query("l3u_chan_sum_nblocks", 8 * Si)
+    pb = torch.empty(Co * N * ncs, dtype=torch.float64, device=cuda)
+    nat().call("l3u_chan_sum", dyp.data_ptr(), Co * 8 * Si, pb.data_ptr(), N, Co, 8 * Si, st())
+    torch.cuda.synchronize()
+    close(cat[:, :Co].reshape(y.shape), y, 1e-5, "convT fwd")
+    assert torch.all(cat[:, Co:] == 0)
+    close(dx.view(x.shape), xr.grad, 1e-5, "convT dX")
+    close(part.view(P, Ci, Co * 8).double().sum(0).view(w.shape), wr.grad, 1e-5, "convT dW")
+    close(pb.view(Co, -1).double().sum(1), br.grad, 1e-5, "convT db")
+
+
+@pytest.mark.parametrize("case", [(2, 16, 7 * 6 * 9), (4, 16, 48 ** 3), (1, 32, 64 ** 3)])
+def test_outconv(cuda, case):
+    N, C, S = case
+    gen = torch.Generator().manual_seed(10)
+    h = torch.randn(N, C, S, generator=gen, dtype=torch.float64)
+    w = torch.randn(1, C, generator=gen, dtype=torch.float64) * 0.3
+    b = torch.randn(1, generator=gen, dtype=torch.float64)
+    hr, wr, br = (t.clone().requires_grad_(True) for t in (h, w, b))
+    p = torch.sigmoid(torch.einsum("oc,ncs->nos", wr, hr) + br[None, :, None])
+    dp = torch.randn(p.shape, generator=gen, dtype=torch.float64)
+    p.backward(dp)
+    hd, wd, bd = h.float().to(cuda), w.float().to(cuda), b.float().to(cuda)
+    pd = torch.empty(N, 1, S, device=cuda)
+    nat().call("l3u_outconv_fwd", hd.data_ptr(), C * S, wd.data_ptr(), bd.data_ptr(), pd.data_ptr(),
+               N, C, S, st())
+    nb = nat().query("l3u_outconv_nblocks", S)
+    part = torch.empty(N * nb * (C + 1), dtype=torch.float64, device=cuda)
+    dh = torch.empty(N, C, S, device=cuda)
+    dpd = dp.float().to(cuda)
+    nat().call("l3u_outconv_bwd", dpd.data_ptr(), pd.data_ptr(), hd.data_ptr(), C * S, wd.data_ptr(),
+               dh.data_ptr(), C * S, part.data_ptr(), N, C, S, st())
+    torch.cuda.synchronize()
+    close(pd, p, 1e-6, "outconv p")
+    close(dh, hr.grad, 1e-5, "outconv dh")
+    ps = part.view(N * nb, C + 1).double().sum(0).cpu()
+    close(ps[:C], wr.grad[0], 1e-5, "outconv dw")
+    close(ps[C:], br.grad, 1e-5, "outconv db")
+
+
+# ------------------------------------------------------------------------------ FTL
+@pytest.mark.parametrize("case", ["rand", "empty", "full", "sat", "params"])
+def test_ftl_golden(cuda, golden, case):
+    z = golden("ftl.npz")
+    p = torch.from_numpy(z[f"{case}/pred"]).to(cuda)
+    t = torch.from_numpy(z[f"{case}/target"]).to(cuda)
+    a, b, g = (float(v) for v in z[f"{case}/abg"])
+    n = p.numel()
+    nb = nat().query("l3u_ftl_nblocks", n)
+    part = torch.empty(nb * 3, device=cuda)
+    sums = torch.empty(3, dtype=torch.float64, device=cuda)
+    loss = torch.empty((), device=cuda)
+    nat().call("l3u_ftl_sums", p.data_ptr(), t.data_ptr(), n, part.data_ptr(), sums.data_ptr(), st())
+    nat().call("l3u_ftl_loss", sums.data_ptr(), a, b, g, 1e-6, loss.data_ptr(), st())
+    dp = torch.empty_like(p)
+    nat().call("l3u_ftl_bwd", p.data_ptr(), t.data_ptr(), n, sums.data_ptr(), a, b, g, 1e-6, None, 0,
+               dp.data_ptr(), st())
+    torch.cuda.synchronize()
+    assert abs(loss.item() - float(z[f"{case}/loss"])) <= 1e-6 * max(1.0, abs(float(z[f"{case}/loss"])))
+    close(dp, torch.from_numpy(z[f"{case}/dpred"]), 1e-5, f"ftl dpred {case}")
+
+
+# ------------------------------------------------------------------------------ AdamW
+def test_adamw_matches_torch(cuda):
+    gen = torch.Generator().manual_seed(11)
+    n = 10007
+    p0 = torch.randn(n, generator=gen)
+    ref = p0.clone().to(cuda).requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=1e-2)
+    p = p0.clone().to(cuda)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    step = torch.zeros(1, dtype=torch.int32, device=cuda)
+    lr = torch.tensor([1e-3], device=cuda)
+    for i in range(5):
+        g = torch.randn(n, generator=gen).to(cuda)
+        ref.grad = g.clone()
+        opt.step()
+        nat().call("l3u_adamw", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n,
+                   lr.data_ptr(), 0.9, 0.999, 1e-8, 1e-2, step.data_ptr(), 1.0, st())
+    torch.cuda.synchronize()
+    assert step.item() == 5
+    close(p, ref.detach(), 1e-6, "adamw")
+
+
+def test_reduce_segments(cuda):
+    src = torch.arange(1000, dtype=torch.float32, device=cuda)
+    src64 = torch.arange(500, dtype=torch.float64, device=cuda) * 0.5
+    items64 = torch.tensor([[4, 3, 1, 1, 2, 1, 0, 1]], dtype=torch.int64, device=cuda)
+    dst64 = torch.zeros(4, device=cuda)
+    nat().call("l3u_reduce_segments", src64.data_ptr(), items64.data_ptr(), 1, dst64.data_ptr(), st())
+    torch.cuda.synchronize()
+    assert dst64[1].item() == 0.5 * (4 + 5 + 6) and dst64[2].item() == 0.5 * (5 + 6 + 7)
+    items = torch.tensor([[0, 4, 10, 1, 3, 0, 0, 0],      # dst[0..2] = sum_i src[i*10 + t]
+                          [500, 2, 1, 100, 2, 5, 0, 0],   # dst[5..6] = src[500+100t] + src[501+100t]
+                          [7, 1, 1, 1, 1, 7, 1, 0]],      # dst[7] += src[7]
+                         dtype=torch.int64, device=cuda)
+    dst = torch.full((8,), -1.0, device=cuda)
+    nat().call("l3u_reduce_segments", src.data_ptr(), items.data_ptr(), 3, dst.data_ptr(), st())
+    torch.cuda.synchronize()
+    d = dst.cpu()
+    assert d[0] == 0 + 10 + 20 + 30 and d[1] == 1 + 11 + 21 + 31 and d[2] == 2 + 12 + 22 + 32
+    assert d[5] == 500 + 501 and d[6] == 600 + 601 and d[3] == -1 and d[7] == 6

@@ -1,0 +1,141 @@
+"""Diagnostic: per-block forward activations and backward output-gradients of the HIP engine vs
+the fp64 oracle on a golden fixture.  Usage: python tools/diag_model.py [model_b1_48.npz]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "light-3d-unet-front_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from oracle import unet_oracle as U  # noqa: E402
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().reshape(-1)
+    b = b.detach().double().cpu().reshape(-1)
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def main(fname="model_b1_48.npz", dtype=torch.float64):
+    from light_unet.models.unet3d import Lightweight3DUNet
+    z = np.load(os.path.join(ROOT, "tests", "golden", fname))
+    sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w/")}
+    dev = torch.device("cuda:0")
+    m = Lightweight3DUNet(dropout_p=0.0)
+    m.load_state_dict(sd)
+    m = m.to(dev).train()
+    x = torch.from_numpy(z["x"]).to(dev)
+    t = torch.from_numpy(z["target"]).to(dev)
+    eng = m.engine
+    eng.debug = {}
+    flat = m.flat_parameters()
+    p, sv = eng.forward(flat, x, training=True)
+    # oracle with retained block outputs
+    P = {k: v.to(dtype).requires_grad_(True) for k, v in sd.items()}
+    acts = {}
+    xo = torch.from_numpy(z["x"]).to(dtype)
+    x1 = U.residual_block(P, "init_conv.", xo); acts["init_conv."] = x1
+    x2 = U.down_block(P, "down1.", x1); acts["down1.res_block."] = x2
+    x3 = U.down_block(P, "down2.", x2); acts["down2.res_block."] = x3
+    x4 = U.down_block(P, "down3.", x3); acts["down3.res_block."] = x4
+    h = U.residual_block(P, "bottleneck.", x4); acts["bottleneck."] = h
+    h = U.up_block(P, "up1.", h, x3); acts["up1.res_block."] = h
+    h = U.up_block(P, "up2.", h, x2); acts["up2.res_block."] = h
+    h = U.up_block(P, "up3.", h, x1); acts["up3.res_block."] = h
+    for a in acts.values():
+        a.retain_grad()
+    po = torch.sigmoid(F.conv3d(h, P["out_conv.weight"], P["out_conv.bias"]))
+    loss = U.focal_tversky(po, torch.from_numpy(z["target"]).to(dtype))
+    loss.backward()
+    print(f"out rel err {rel(p, po):.3e}")
+    for name, b in sv["blk"].items():
+        o = b["out"]
+        N = o.t.shape[0]
+        S = o.ns // 1 if False else None
+        ov = o.t.reshape(-1)[o.off:].as_strided((N, o.C, acts[name].numel() // (N * o.C)),
+                                                 (o.ns, acts[name].numel() // (N * o.C), 1))
+        print(f"fwd {name:20s} rel err {rel(ov, acts[name]):.3e}")
+    # backward through the engine with the FTL gradient
+    from light_unet.models.losses import _ftl_sums
+    from light_unet import _native as nat
+    sums = _ftl_sums(p, t)
+    dp = torch.empty_like(p)
+    nat.call("l3u_ftl_bwd", p.data_ptr(), t.data_ptr(), p.numel(), sums.data_ptr(), 0.7, 0.3, 0.75,
+             1e-6, None, 0, dp.data_ptr(), nat.stream())
+    g = torch.empty_like(flat)
+    eng.backward(flat, g, sv, dp)
+    torch.cuda.synchronize()
+    for name in sv["blk"]:
+        d = eng.debug[name]
+        ref = acts[name].grad
+        N = ref.shape[0]
+        Sx = ref.numel() // (N * d.C)
+        dv = d.t.reshape(-1)[d.off:].as_strided((N, d.C, Sx), (d.ns, Sx, 1))
+        print(f"bwd d(out) {name:20s} rel err {rel(dv, ref):.3e}")
+    # block internals of up3 (fp64 reference from the engine's own saved forward inputs)
+    for name in ("up3.res_block.", "up2.res_block.", "init_conv."):
+        b = sv["blk"][name]
+        xv = b["x"]
+        N = xv.t.shape[0]
+        d_, h_, w_ = b["dims"]
+        S = d_ * h_ * w_
+        X = xv.t.reshape(-1)[xv.off:].as_strided((N, xv.C, S), (xv.ns, S, 1)).double().cpu()
+        X = X.reshape(N, xv.C, d_, h_, w_).requires_grad_(True)
+        dO = eng.debug[name]
+        dO = dO.t.reshape(-1)[dO.off:].as_strided((N, dO.C, S), (dO.ns, S, 1)).double().cpu()
+        dO = dO.reshape(N, dO.shape[1], d_, h_, w_)
+        pre = name
+        Pd = {k: v.double() for k, v in sd.items()}
+        cin = xv.C
+        r = F.conv3d(X, Pd[pre + "shortcut.0.weight"]) if pre + "shortcut.0.weight" in Pd else X
+        if r is not X:
+            r.retain_grad()
+            rn = F.instance_norm(r, weight=Pd[pre + "shortcut.1.weight"], bias=Pd[pre + "shortcut.1.bias"], eps=1e-5)
+        else:
+            rn = X
+        z1 = F.conv3d(X, Pd[pre + "conv1.depthwise.weight"], padding=1, groups=cin); z1.retain_grad()
+        y1 = F.conv3d(z1, Pd[pre + "conv1.pointwise.weight"]); y1.retain_grad()
+        a1 = F.leaky_relu(F.instance_norm(y1, weight=Pd[pre + "norm1.weight"], bias=Pd[pre + "norm1.bias"], eps=1e-5), 0.01)
+        z2 = F.conv3d(a1, Pd[pre + "conv2.depthwise.weight"], padding=1, groups=a1.shape[1]); z2.retain_grad()
+        y2 = F.conv3d(z2, Pd[pre + "conv2.pointwise.weight"]); y2.retain_grad()
+        out = F.leaky_relu(F.instance_norm(y2, weight=Pd[pre + "norm2.weight"], bias=Pd[pre + "norm2.bias"], eps=1e-5) + rn, 0.01)
+        out.backward(dO)
+        dd = eng.debug[name + "#"]
+        for key, ref in (("dy2", y2.grad), ("dz2", z2.grad), ("dy1", y1.grad), ("dz1", z1.grad),
+                         ("dx", X.grad)) + ((("dr", r.grad),) if r is not X else ()):
+            v = dd[key]
+            if hasattr(v, "ns"):
+                v = v.t.reshape(-1)[v.off:].as_strided((N, v.C, S), (v.ns, S, 1))
+            print(f"  {name} {key:4s} rel err {rel(v, ref):.3e}")
+    # kink statistics: InstanceNorm outputs within eps of the LeakyReLU kink
+    for name in ("up3.res_block.", "init_conv."):
+        b = sv["blk"][name]
+        rec1 = b["recs"][1].view(-1, 8).cpu().double()
+        y1 = b["y1"].double().cpu()
+        Nn, Cc = y1.shape[0], y1.shape[1]
+        pre = (y1.view(Nn, Cc, -1) - rec1[:, 0].view(Nn, Cc, 1)) * rec1[:, 2].view(Nn, Cc, 1) + rec1[:, 3].view(Nn, Cc, 1)
+        for eps in (1e-7, 1e-6, 1e-5):
+            print(f"  kinks {name} |pre|<{eps:g}: {int((pre.abs() < eps).sum())} of {pre.numel()}")
+    # fp32 CPU oracle on the same inputs for comparison
+    P32 = {k: v.float().requires_grad_(True) for k, v in sd.items()}
+    o32 = U.unet_forward(P32, torch.from_numpy(z["x"]))
+    U.focal_tversky(o32, torch.from_numpy(z["target"])).backward()
+    tot = [0.0, 0.0, 0.0]
+    for k, (off, n, shape) in eng.offsets.items():
+        ref = P[k].grad.double().reshape(-1)
+        gg = g[off:off + n].double().cpu()
+        cc = P32[k].grad.double().reshape(-1)
+        eg = float((gg - ref).norm() / ref.norm())
+        ec = float((cc - ref).norm() / ref.norm())
+        tot[0] += float((gg - ref).norm() ** 2)
+        tot[1] += float((cc - ref).norm() ** 2)
+        tot[2] += float(ref.norm() ** 2)
+        print(f"grad {k:45s} maxrel {rel(g[off:off + n], P[k].grad):.2e}  L2rel gpu {eg:.2e} cpu32 {ec:.2e}")
+    print(f"GLOBAL L2rel gpu {(tot[0] / tot[2]) ** 0.5:.3e} cpu32 {(tot[1] / tot[2]) ** 0.5:.3e}")
+
+
+if __name__ == "__main__":
+    main(*(sys.argv[1:2] or []))
