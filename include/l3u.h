@@ -35,14 +35,32 @@ extern "C" {
 
 int l3u_abi_version(void);
 
+/* Where an InstanceNorm record comes from when a consumer kernel finalizes it itself (no separate
+ * l3u_in_finalize launch): the (count, mean, M2) partials l3u_pw_fwd emitted for the producing
+ * GEMM, the affine parameters and the Dropout3d stream.  Every workgroup of the consumer merges
+ * the partials of its (n, c) in the same fixed order (identical values everywhere) and the first
+ * workgroup of each (n, c) stores the record to rec_out for the backward pass.                 */
+typedef struct l3u_norm_src {
+  const float* stat_part;      /* [N][C][nsb][3] */
+  int nsb;
+  int layer;                   /* dropout stream id */
+  const float* gamma;          /* [C] or NULL (1) */
+  const float* beta;           /* [C] or NULL (0) */
+  float drop_p;                /* 0: no dropout */
+  unsigned long long seed;
+  const int* step;             /* device step counter or NULL */
+  float* rec_out;              /* [N][C][8] or NULL */
+} l3u_norm_src;
+
 /* ---- depthwise 3x3x3 conv, stride 1, padding 1, no bias ------------------------------------
  * replaces nn.Conv3d(C, C, 3, 1, 1, groups=C, bias=False)
  *          (DepthwiseSeparableConv3d.depthwise, light_unet/models/unet3d.py:16-17, forward :21)
  * w: [C][27].  rec != NULL fuses a = lrelu(scale*(x-mean) + shift) into the input load (the
  * InstanceNorm1 + LeakyReLU + Dropout3d that precede conv2.depthwise, unet3d.py:84-89).      */
-int l3u_dw3_nchunk(int D);
-int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float* rec, float* y,
-                long long y_nstride, int N, int C, int D, int H, int W, hipStream_t stream);
+int l3u_dw3_nchunk(int D, int H, int W);   /* z/y chunks per (n, c): partial-sum count */
+int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float* rec,
+                const l3u_norm_src* src, float* y, long long y_nstride, int N, int C, int D,
+                int H, int W, hipStream_t stream);   /* src != NULL: finalize rec in-kernel */
 /* fused backward (autograd of the same module): dx = conv^T(dz) (accumulate != 0: dx += ...),
  * dw_part[C][N*nchunk][27] partial weight gradients.  rec != NULL: dx receives
  * dpre = dA * k * lrelu'(pre) and in_part[C][N][nchunk][2] (fp64) = {sum dpre, sum dpre*xhat}.*/
@@ -81,9 +99,12 @@ int l3u_in_finalize(const float* stat_part, int nsb, const float* gamma, const f
 /* block output: out = lrelu(scale2*(y2-mean2) + shift2 + R), R = r (rec_r == NULL, nn.Identity
  * shortcut) or scale_r*(r-mean_r) + shift_r (Conv1x1 + InstanceNorm shortcut)                        */
 int l3u_norm_act_nblocks(int S);
-int l3u_norm_act_fwd(const float* y2, long long y2_nstride, const float* rec2, const float* r,
-                     long long r_nstride, const float* rec_r, float* out, long long out_nstride,
-                     int N, int C, int S, hipStream_t stream);
+/* records come either ready (rec2 / rec_r) or are finalized in-kernel from src2 / src_r
+ * (then also stored to src->rec_out); shortcut == 0 means the identity residual (R = r).       */
+int l3u_norm_act_fwd(const float* y2, long long y2_nstride, const float* rec2,
+                     const l3u_norm_src* src2, const float* r, long long r_nstride,
+                     const float* rec_r, const l3u_norm_src* src_r, int shortcut, float* out,
+                     long long out_nstride, int N, int C, int S, hipStream_t stream);
 /* backward of the block tail: part[C][N][nblocks][3] (fp64) = {sum g, sum g*xhat2, sum g*xhat_r},
  * g = dout * lrelu'(out); then dy2 / dr (dr = g for the identity shortcut)                   */
 int l3u_norm_act_bwd_reduce(const float* dout, long long dout_nstride, const float* out,

@@ -71,6 +71,74 @@ L3U_DEV void chan_merge(float& n_a, float& mean_a, float& m2_a, float n_b, float
   n_a = n;
 }
 
+L3U_DEV unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Merge the (count, mean, M2) partials of one (n, c) with the 64 lanes of the calling wave
+// (lane-strided Chan merges, then a fixed xor tree) and build the 8-float record.  Every caller
+// for the same (n, c) gets bit-identical values.  Must be called by a full wave; returns the
+// record in `r` on every lane.
+L3U_DEV void finalize_record(const l3u_norm_src& s, int n, int c, int C, float r[kRec]) {
+  const int l = threadIdx.x & 63;
+  const float* p = s.stat_part + ((long long)n * C + c) * s.nsb * 3;
+  float cn = 0.f, mu = 0.f, m2 = 0.f;
+  for (int i = l; i < s.nsb; i += 64) chan_merge(cn, mu, m2, p[i * 3], p[i * 3 + 1], p[i * 3 + 2]);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float cb = __shfl_xor(cn, o, 64), mb = __shfl_xor(mu, o, 64), vb = __shfl_xor(m2, o, 64);
+    if (l & o) {   // merge in lane order so both partners compute the same value
+      float c2 = cb, mu2 = mb, v2 = vb;
+      chan_merge(c2, mu2, v2, cn, mu, m2);
+      cn = c2; mu = mu2; m2 = v2;
+    } else {
+      chan_merge(cn, mu, m2, cb, mb, vb);
+    }
+  }
+  const float var = cn > 0.f ? m2 / cn : 0.f;
+  const float rstd = 1.0f / sqrtf(var + kEps);
+  const float g = s.gamma ? s.gamma[c] : 1.f, b = s.beta ? s.beta[c] : 0.f;
+  float k = 1.f;
+  if (s.drop_p > 0.f) {
+    const int st = s.step ? *s.step : 0;
+    const unsigned long long h = splitmix64(s.seed ^ splitmix64(((unsigned long long)st << 32) ^
+                                                                ((unsigned long long)s.layer << 24) ^
+                                                                (unsigned long long)(n * C + c)));
+    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+    k = u < s.drop_p ? 0.f : 1.f / (1.f - s.drop_p);
+  }
+  r[0] = mu;
+  r[1] = rstd;
+  r[2] = k * g * rstd;
+  r[3] = k * b;
+  r[4] = k;
+  r[5] = g;
+  r[6] = b;
+  r[7] = 0.f;
+}
+
+// Workgroup-level: wave 0 finalizes, broadcasts through `sh8` (8 floats of LDS) and, if asked,
+// stores the record for the backward.  All threads must call it (contains a barrier).
+L3U_DEV void block_record(const l3u_norm_src& s, int n, int c, int C, bool store, float* sh8) {
+  if (threadIdx.x < 64) {
+    float r[kRec];
+    finalize_record(s, n, c, C, r);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int i = 0; i < kRec; ++i) sh8[i] = r[i];
+      if (store && s.rec_out) {
+        float* o = s.rec_out + ((long long)n * C + c) * kRec;
+#pragma unroll
+        for (int i = 0; i < kRec; ++i) o[i] = r[i];
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // XCD-aware block remap (guide §5.5 T1, bijective form): blocks that share halo planes / weight
 // tiles are consecutive in the logical order, and consecutive logical ids land on one XCD.
 L3U_DEV int xcd_remap(int bid, int nblocks) {

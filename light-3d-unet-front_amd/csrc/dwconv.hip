@@ -21,8 +21,8 @@ namespace {
 template <int MODE, int P>
 __global__ __launch_bounds__(256) void dw3_fwd_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w,
-    const float* __restrict__ rec, float* __restrict__ y, long long yns,
-    int C, int D, int H, int W, int TZ, int nchunk) {
+    const float* __restrict__ rec, l3u_norm_src src, int has_src, float* __restrict__ y,
+    long long yns, int C, int D, int H, int W, int TZ, int nchunk) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int HW = H * W, PW = W + 2, PP = (H + 2) * PW;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -39,9 +39,15 @@ __global__ __launch_bounds__(256) void dw3_fwd_kernel(
   for (int t = 0; t < 27; ++t) wk[t] = w[c * 27 + t];
   float sc = 1.f, sh = 0.f, mu = 0.f;
   if (MODE == 1) {
-    mu = rec[(long long)nc * kRec + 0];
-    sc = rec[(long long)nc * kRec + 2];
-    sh = rec[(long long)nc * kRec + 3];
+    if (has_src) {
+      float* s8 = lds + 2 * PP;
+      block_record(src, n, c, C, chunk == 0, s8);
+      mu = s8[0]; sc = s8[2]; sh = s8[3];
+    } else {
+      mu = rec[(long long)nc * kRec + 0];
+      sc = rec[(long long)nc * kRec + 2];
+      sh = rec[(long long)nc * kRec + 3];
+    }
   }
   for (int i = tid; i < 2 * PP; i += 256) lds[i] = 0.f;
 
@@ -281,6 +287,338 @@ __global__ __launch_bounds__(256) void dw3_bwd_kernel(
 
 int pick_tz(int D) { return D <= 8 ? D : 4; }
 
+// ------------------------------------------------------------------------------------------------
+// x-quad variants (W % 4 == 0, every production shape): a workgroup owns (n, c, TZ z-planes,
+// RB rows); a thread owns 4 consecutive x of one row.  Global traffic is float4 per lane (one
+// 16-B load per input quad per plane, one 16-B store per output quad), the LDS plane image has
+// rows [4 zero pad | W | 4 zero pad] so the quad lands 16-B aligned (ds_write_b128) and the 3x6
+// neighbourhood of a quad is 3 ds_read_b128 + 6 ds_read_b32 (vs 36 scalar reads).
+// ------------------------------------------------------------------------------------------------
+struct QGeom {
+  int WQ, RS, RB, ny, TZ, nz, threads;
+};
+
+QGeom qgeom(int D, int H, int W) {
+  QGeom g;
+  g.WQ = W / 4;
+  g.RS = W + 8;
+  const int maxrows = 256 / g.WQ;
+  g.ny = (H + maxrows - 1) / maxrows;
+  g.RB = (H + g.ny - 1) / g.ny;
+  g.TZ = D >= 32 ? 8 : (D >= 8 ? 4 : D);
+  g.nz = (D + g.TZ - 1) / g.TZ;
+  g.threads = ((g.RB * g.WQ + 63) / 64) * 64;
+  return g;
+}
+
+bool use_quads(int H, int W) {
+  if (W % 4 != 0 || W < 4 || W > 1024 || H < 1) return false;
+  const int WQ = W / 4, maxrows = 256 / WQ;
+  const int ny = (H + maxrows - 1) / maxrows, RB = (H + ny - 1) / ny;
+  const int threads = ((RB * WQ + 63) / 64) * 64;
+  return (RB + 2) * WQ <= 2 * threads;   // register staging: <= 2 quads per thread per plane
+}
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// the 6 values of LDS row `row` around the quad at column ox: cols ox-1 .. ox+4
+L3U_DEV void q_row(const float* plane, int row, int RS, int ox, float v[6]) {
+  const float* b = plane + row * RS + 4 + ox;
+  const f4 m = *reinterpret_cast<const f4*>(b);
+  v[0] = b[-1];
+  v[1] = m[0]; v[2] = m[1]; v[3] = m[2]; v[4] = m[3];
+  v[5] = b[4];
+}
+
+// block decode shared by both quad kernels
+struct QBlock {
+  int n, c, nc, z0, z1, y0, rows, oy, ox, ck;
+  bool own;
+};
+
+L3U_DEV QBlock q_decode(int C, int D, int H, int RB, int ny, int TZ, int nz, int WQ) {
+  QBlock b;
+  int t = xcd_remap(blockIdx.x, gridDim.x);
+  b.ck = t % (ny * nz);
+  const int yb = t % ny; t /= ny;
+  const int zb = t % nz; t /= nz;
+  b.nc = t;
+  b.c = t % C;
+  b.n = t / C;
+  b.z0 = zb * TZ;
+  b.z1 = min(b.z0 + TZ, D);
+  b.y0 = yb * RB;
+  b.rows = min(RB, H - b.y0);
+  const int q = threadIdx.x;
+  b.own = q < b.rows * WQ;
+  b.oy = b.own ? q / WQ : 0;
+  b.ox = b.own ? (q - b.oy * WQ) * 4 : 0;
+  return b;
+}
+
+// Register-staged plane loads (issue early, commit to LDS one step later: the global-load
+// latency hides under the previous plane's stencil).  A thread stages at most 2 quads per plane:
+// the host guarantees (RB + 2) * WQ <= 2 * blockDim.
+struct QPre {
+  f4 v[2];
+};
+
+L3U_DEV void q_fetch(QPre& p, const float* src, int y0, int rows, int H, int W, int WQ) {
+  const int nq = (rows + 2) * WQ;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = threadIdx.x + k * blockDim.x;
+    if (q < nq) {
+      const int lr = q / WQ, x = (q - lr * WQ) * 4, y = y0 - 1 + lr;
+      if (y >= 0 && y < H) p.v[k] = *reinterpret_cast<const f4*>(src + (long long)y * W + x);
+    }
+  }
+}
+
+template <int MODE>
+L3U_DEV void q_commit(const QPre& p, float* plane, int y0, int rows, int H, int WQ, int RS,
+                      float sc, float mu, float sh) {
+  const int nq = (rows + 2) * WQ;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = threadIdx.x + k * blockDim.x;
+    if (q < nq) {
+      const int lr = q / WQ, x = (q - lr * WQ) * 4, y = y0 - 1 + lr;
+      if (y >= 0 && y < H) {
+        f4 v = p.v[k];
+        if (MODE == 1) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(sc, v[i] - mu, sh));
+        }
+        *reinterpret_cast<f4*>(plane + lr * RS + 4 + x) = v;
+      }
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void dw3q_fwd_kernel(
+    const float* __restrict__ x, long long xns, const float* __restrict__ w,
+    const float* __restrict__ rec, l3u_norm_src src, int has_src, float* __restrict__ y,
+    long long yns, int C, int D, int H, int W, int RB, int ny, int TZ, int nz) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int WQ = W >> 2, RS = W + 8, PP = (RB + 2) * RS, HW = H * W;
+  const QBlock b = q_decode(C, D, H, RB, ny, TZ, nz, WQ);
+  const float* xp = x + (long long)b.n * xns + (long long)b.c * D * HW;
+  float* yp = y + (long long)b.n * yns + (long long)b.c * D * HW;
+  float wk[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t) wk[t] = w[b.c * 27 + t];
+  float sc = 1.f, sh = 0.f, mu = 0.f;
+  if (MODE == 1) {
+    if (has_src) {
+      float* s8 = lds + 2 * PP;
+      block_record(src, b.n, b.c, C, b.ck == 0, s8);
+      mu = s8[0]; sc = s8[2]; sh = s8[3];
+    } else {
+      mu = rec[(long long)b.nc * kRec + 0];
+      sc = rec[(long long)b.nc * kRec + 2];
+      sh = rec[(long long)b.nc * kRec + 3];
+    }
+  }
+  for (int i = threadIdx.x; i < 2 * PP; i += blockDim.x) lds[i] = 0.f;
+  __syncthreads();
+  f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0;
+  const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
+  QPre pre;
+  q_fetch(pre, xp + (long long)zlo * HW, b.y0, b.rows, H, W, WQ);
+  for (int zi = zlo; zi <= zhi; ++zi) {
+    float* buf = lds + (zi & 1) * PP;
+    q_commit<MODE>(pre, buf, b.y0, b.rows, H, WQ, RS, sc, mu, sh);
+    if (zi < zhi) q_fetch(pre, xp + (long long)(zi + 1) * HW, b.y0, b.rows, H, W, WQ);
+    __syncthreads();
+    if (b.own) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        float v[6];
+        q_row(buf, b.oy + r, RS, b.ox, v);
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const float w0 = wk[r * 3 + dx], w1 = wk[9 + r * 3 + dx], w2 = wk[18 + r * 3 + dx];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            a2[i] = fmaf(w0, v[i + dx], a2[i]);   // input plane zi -> output zi+1 (kd=0)
+            a1[i] = fmaf(w1, v[i + dx], a1[i]);   //                -> output zi   (kd=1)
+            a0[i] = fmaf(w2, v[i + dx], a0[i]);   //                -> output zi-1 (kd=2)
+          }
+        }
+      }
+      const int zo = zi - 1;
+      if (zo >= b.z0 && zo < b.z1)
+        *reinterpret_cast<f4*>(yp + (long long)zo * HW + (long long)(b.y0 + b.oy) * W + b.ox) = a0;
+    }
+    a0 = a1;
+    a1 = a2;
+    a2 = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  // the last owned plane when the slab ends at the volume end (no plane z1 to drive the store)
+  if (b.own && b.z1 == D && D - 1 >= b.z0 && zhi == D - 1) {
+    *reinterpret_cast<f4*>(yp + (long long)(D - 1) * HW + (long long)(b.y0 + b.oy) * W + b.ox) = a0;
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void dw3q_bwd_kernel(
+    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
+    const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
+    long long dxns, int accumulate, float* __restrict__ dw_part, double* __restrict__ in_part,
+    int N, int C, int D, int H, int W, int RB, int ny, int TZ, int nz) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int WQ = W >> 2, RS = W + 8, PP = (RB + 2) * RS, HW = H * W;
+  const QBlock b = q_decode(C, D, H, RB, ny, TZ, nz, WQ);
+  const long long cofs = (long long)b.c * D * HW;
+  const float* dzp = dz + (long long)b.n * dzns + cofs;
+  const float* xp = x + (long long)b.n * xns + cofs;
+  float* dxp = dx + (long long)b.n * dxns + cofs;
+  float* dzb = lds;             // 2 planes
+  float* ab = lds + 2 * PP;     // 2 planes
+  float wk[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t) wk[t] = w[b.c * 27 + t];
+  float sc = 1.f, sh = 0.f, kk = 1.f, mean = 0.f, rstd = 1.f;
+  if (MODE == 1) {
+    const float* r = rec + (long long)b.nc * kRec;
+    mean = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];
+  }
+  for (int i = threadIdx.x; i < 4 * PP; i += blockDim.x) lds[i] = 0.f;
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  f4 d0 = zero4, d1 = zero4, d2 = zero4;      // dA planes zd-1, zd, zd+1
+  f4 g0 = zero4, g1 = zero4, g2 = zero4;      // own dZ of planes zd-2, zd-1, zd (owned only)
+  float gw[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t) gw[t] = 0.f;
+  double s1 = 0.0, s2 = 0.0;
+  const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
+  const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
+  const int nsteps = b.z1 - b.z0 + 3;
+  QPre pz, pa;     // staged dZ plane zd and A plane za of the NEXT step
+  {
+    const int zd = b.z0 - 1, za = zd - 1;
+    if (zd >= zlo && zd <= zhi) q_fetch(pz, dzp + (long long)zd * HW, b.y0, b.rows, H, W, WQ);
+    if (za >= zlo && za <= zhi) q_fetch(pa, xp + (long long)za * HW, b.y0, b.rows, H, W, WQ);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int zd = b.z0 - 1 + s, za = zd - 1;
+    float* dbuf = dzb + (s & 1) * PP;
+    float* abuf = ab + (s & 1) * PP;
+    const bool ldz = zd >= zlo && zd <= zhi;
+    const bool la = za >= zlo && za <= zhi;
+    if (ldz) q_commit<0>(pz, dbuf, b.y0, b.rows, H, WQ, RS, 1.f, 0.f, 0.f);
+    if (la) q_commit<MODE>(pa, abuf, b.y0, b.rows, H, WQ, RS, sc, mean, sh);
+    // issue the next step's plane loads and this step's epilogue loads before the barrier
+    if (zd + 1 >= zlo && zd + 1 <= zhi) q_fetch(pz, dzp + (long long)(zd + 1) * HW, b.y0, b.rows, H, W, WQ);
+    if (za + 1 >= zlo && za + 1 <= zhi) q_fetch(pa, xp + (long long)(za + 1) * HW, b.y0, b.rows, H, W, WQ);
+    const int zf = zd - 1;   // dA plane zf completes in this step
+    const bool fin = b.own && zf >= b.z0 && zf < b.z1;
+    f4 epi = zero4;
+    if (fin && (MODE == 1 || accumulate))
+      epi = *reinterpret_cast<const f4*>((MODE == 1 ? xp : dxp) + (long long)zf * HW + qofs);
+    __syncthreads();
+    const bool zd_owned = zd >= b.z0 && zd < b.z1;
+    if (b.own) {
+      g0 = g1;
+      g1 = g2;
+      g2 = zero4;
+      if (ldz) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          float v[6];
+          q_row(dbuf, b.oy + r, RS, b.ox, v);
+          if (r == 1 && zd_owned) g2 = f4{v[1], v[2], v[3], v[4]};
+#pragma unroll
+          for (int dxi = 0; dxi < 3; ++dxi) {
+            const int tf = (2 - r) * 3 + (2 - dxi);   // flipped in-plane tap
+            const float w0 = wk[tf], w1 = wk[9 + tf], w2 = wk[18 + tf];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              d0[i] = fmaf(w0, v[i + dxi], d0[i]);
+              d1[i] = fmaf(w1, v[i + dxi], d1[i]);
+              d2[i] = fmaf(w2, v[i + dxi], d2[i]);
+            }
+          }
+        }
+      }
+      if (la) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          float u[6];
+          q_row(abuf, b.oy + r, RS, b.ox, u);
+#pragma unroll
+          for (int dxi = 0; dxi < 3; ++dxi) {
+            float a = gw[r * 3 + dxi], bb = gw[9 + r * 3 + dxi], cc = gw[18 + r * 3 + dxi];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              a = fmaf(g2[i], u[i + dxi], a);     // dZ plane za+1 (kd=0)
+              bb = fmaf(g1[i], u[i + dxi], bb);   // dZ plane za   (kd=1)
+              cc = fmaf(g0[i], u[i + dxi], cc);   // dZ plane za-1 (kd=2)
+            }
+            gw[r * 3 + dxi] = a;
+            gw[9 + r * 3 + dxi] = bb;
+            gw[18 + r * 3 + dxi] = cc;
+          }
+        }
+      }
+      if (fin) {
+        float* dst = dxp + (long long)zf * HW + qofs;
+        if (MODE == 1) {
+          const f4 yv = epi;
+          f4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float pre = fmaf(sc, yv[i] - mean, sh);
+            const float dp = d0[i] * kk * lrelu_d(pre);
+            o[i] = dp;
+            s1 += dp;
+            s2 += (double)dp * ((yv[i] - mean) * rstd);
+          }
+          *reinterpret_cast<f4*>(dst) = o;
+        } else {
+          f4 o = d0;
+          if (accumulate) o += epi;
+          *reinterpret_cast<f4*>(dst) = o;
+        }
+      }
+    }
+    d0 = d1;
+    d1 = d2;
+    d2 = zero4;
+  }
+  // workgroup reduction (fixed order) of the 27 taps and the 2 fp64 IN sums
+  __syncthreads();
+  float* red = lds;                                        // [nwaves][27]
+  double* redd = reinterpret_cast<double*>(lds + 4 * 32);  // [nwaves][2], after [4][32] floats
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int t = 0; t < 27; ++t) {
+    const float r = wave_sum(gw[t]);
+    if (ln == 0) red[wv * 32 + t] = r;
+  }
+  if (MODE == 1) {
+    const double r1 = wave_sum_d(s1), r2 = wave_sum_d(s2);
+    if (ln == 0) { redd[wv * 2] = r1; redd[wv * 2 + 1] = r2; }
+  }
+  __syncthreads();
+  const int nchunk = nz * ny;
+  const int ck = xcd_remap(blockIdx.x, gridDim.x) % nchunk;   // (zb, yb) chunk within (n, c)
+  if (threadIdx.x < 27) {
+    float r = 0.f;
+    for (int k = 0; k < nw; ++k) r += red[k * 32 + threadIdx.x];
+    dw_part[((long long)b.c * N * nchunk + (long long)b.n * nchunk + ck) * 27 + threadIdx.x] = r;
+  }
+  if (MODE == 1 && threadIdx.x >= 32 && threadIdx.x < 34) {
+    const int j = threadIdx.x - 32;
+    double r = 0.0;
+    for (int k = 0; k < nw; ++k) r += redd[k * 2 + j];
+    in_part[(((long long)b.c * N + b.n) * nchunk + ck) * 2 + j] = r;
+  }
+}
+
 }  // namespace
 
 #define DW_DISPATCH_P(KERNEL, MODE, ...)                                               \
@@ -297,17 +635,37 @@ int pick_tz(int D) { return D <= 8 ? D : 4; }
 
 extern "C" {
 
-int l3u_dw3_nchunk(int D) { return (D + pick_tz(D) - 1) / pick_tz(D); }
+int l3u_dw3_nchunk(int D, int H, int W) {
+  if (use_quads(H, W)) {
+    const QGeom g = qgeom(D, H, W);
+    return g.nz * g.ny;
+  }
+  return (D + pick_tz(D) - 1) / pick_tz(D);
+}
 
-int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float* rec, float* y,
-                long long y_nstride, int N, int C, int D, int H, int W, hipStream_t stream) {
-  L3U_REQUIRE(N > 0 && C > 0 && D > 0 && H > 0 && W > 0 && H * W <= 4096);
+int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float* rec,
+                const l3u_norm_src* src, float* y, long long y_nstride, int N, int C, int D,
+                int H, int W, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && D > 0 && H > 0 && W > 0);
+  const l3u_norm_src z{};
+  const l3u_norm_src s = src ? *src : z;
+  const int has = src ? 1 : 0;
+  const bool xf = rec != nullptr || src != nullptr;
+  if (use_quads(H, W) && x_nstride % 4 == 0 && y_nstride % 4 == 0) {
+    const QGeom g = qgeom(D, H, W);
+    const size_t lds = (2 * (size_t)(g.RB + 2) * g.RS + 8) * sizeof(float);
+    dim3 grid(N * C * g.nz * g.ny), block(g.threads);
+    if (xf) hipLaunchKernelGGL(dw3q_fwd_kernel<1>, grid, block, lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, C, D, H, W, g.RB, g.ny, g.TZ, g.nz);
+    else hipLaunchKernelGGL(dw3q_fwd_kernel<0>, grid, block, lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, C, D, H, W, g.RB, g.ny, g.TZ, g.nz);
+    L3U_CHECK_LAUNCH();
+  }
+  L3U_REQUIRE(H * W <= 4096);
   const int TZ = pick_tz(D), nchunk = (D + TZ - 1) / TZ;
   const int P = (H * W + 255) / 256;
-  const size_t lds = 2 * (size_t)(H + 2) * (W + 2) * sizeof(float);
+  const size_t lds = (2 * (size_t)(H + 2) * (W + 2) + 8) * sizeof(float);
   dim3 grid(N * C * nchunk), block(256);
-  if (rec) DW_DISPATCH_P(dw3_fwd_kernel, 1, grid, block, lds, stream, x, x_nstride, w, rec, y, y_nstride, C, D, H, W, TZ, nchunk);
-  else DW_DISPATCH_P(dw3_fwd_kernel, 0, grid, block, lds, stream, x, x_nstride, w, rec, y, y_nstride, C, D, H, W, TZ, nchunk);
+  if (xf) DW_DISPATCH_P(dw3_fwd_kernel, 1, grid, block, lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, C, D, H, W, TZ, nchunk);
+  else DW_DISPATCH_P(dw3_fwd_kernel, 0, grid, block, lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, C, D, H, W, TZ, nchunk);
   L3U_CHECK_LAUNCH();
 }
 
@@ -315,8 +673,18 @@ int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long
                 const float* w, const float* rec, float* dx, long long dx_nstride, int accumulate,
                 float* dw_part, double* in_part, int N, int C, int D, int H, int W,
                 hipStream_t stream) {
-  L3U_REQUIRE(N > 0 && C > 0 && D > 0 && H > 0 && W > 0 && H * W <= 4096);
+  L3U_REQUIRE(N > 0 && C > 0 && D > 0 && H > 0 && W > 0);
   L3U_REQUIRE(rec == nullptr || in_part != nullptr);
+  if (use_quads(H, W) && x_nstride % 4 == 0 && dz_nstride % 4 == 0 && dx_nstride % 4 == 0) {
+    const QGeom g = qgeom(D, H, W);
+    size_t lds = 4 * (size_t)(g.RB + 2) * g.RS * sizeof(float);
+    if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch
+    dim3 grid(N * C * g.nz * g.ny), block(g.threads);
+    if (rec) hipLaunchKernelGGL(dw3q_bwd_kernel<1>, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part, in_part, N, C, D, H, W, g.RB, g.ny, g.TZ, g.nz);
+    else hipLaunchKernelGGL(dw3q_bwd_kernel<0>, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part, in_part, N, C, D, H, W, g.RB, g.ny, g.TZ, g.nz);
+    L3U_CHECK_LAUNCH();
+  }
+  L3U_REQUIRE(H * W <= 4096);
   const int TZ = pick_tz(D), nchunk = (D + TZ - 1) / TZ;
   const int P = (H * W + 255) / 256;
   size_t lds = 4 * (size_t)(H + 2) * (W + 2) * sizeof(float);

@@ -295,11 +295,29 @@ __global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __res
   const long long base = it[0] + t * it[3];
   const long long cnt = it[1], is = it[2];
   double s = 0.0;
+  // loads are issued 16 at a time (memory-level parallelism); the adds stay in index order
   if (it[7]) {
-    const double* sd = reinterpret_cast<const double*>(src);
-    for (long long i = 0; i < cnt; ++i) s += sd[base + i * is];
+    const double* sd = reinterpret_cast<const double*>(src) + base;
+    long long i = 0;
+    for (; i + 16 <= cnt; i += 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = sd[(i + u) * is];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (; i < cnt; ++i) s += sd[i * is];
   } else {
-    for (long long i = 0; i < cnt; ++i) s += src[base + i * is];
+    const float* sf = src + base;
+    long long i = 0;
+    for (; i + 16 <= cnt; i += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = sf[(i + u) * is];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (; i < cnt; ++i) s += sf[i * is];
   }
   float* d = dst + it[5] + t;
   *d = it[6] ? (float)((double)*d + s) : (float)s;

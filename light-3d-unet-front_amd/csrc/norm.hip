@@ -13,74 +13,44 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-L3U_DEV unsigned long long splitmix64(unsigned long long z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
 // one wave per (n, c)
-__global__ __launch_bounds__(256) void in_finalize_kernel(
-    const float* __restrict__ part, int nsb, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float drop_p, unsigned long long seed,
-    const int* __restrict__ step, int layer, float* __restrict__ rec, int NC, int C) {
+__global__ __launch_bounds__(256) void in_finalize_kernel(l3u_norm_src src, int NC, int C) {
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
   if (wid >= NC) return;
-  const float* p = part + (long long)wid * nsb * 3;
-  float cn = 0.f, mu = 0.f, m2 = 0.f;
-  for (int i = l; i < nsb; i += 64) chan_merge(cn, mu, m2, p[i * 3], p[i * 3 + 1], p[i * 3 + 2]);
+  float r[kRec];
+  finalize_record(src, wid / C, wid % C, C, r);
+  if (l == 0) {
+    float* o = src.rec_out + (long long)wid * kRec;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float cb = __shfl_xor(cn, o, 64), mb = __shfl_xor(mu, o, 64), vb = __shfl_xor(m2, o, 64);
-    // merge in lane order so both partners compute the same value
-    if (l & o) {
-      float c2 = cb, mu2 = mb, v2 = vb;
-      chan_merge(c2, mu2, v2, cn, mu, m2);
-      cn = c2; mu = mu2; m2 = v2;
-    } else {
-      chan_merge(cn, mu, m2, cb, mb, vb);
-    }
+    for (int i = 0; i < kRec; ++i) o[i] = r[i];
   }
-  if (l != 0) return;
-  const int c = wid % C, n = wid / C;
-  const float var = cn > 0.f ? m2 / cn : 0.f;
-  const float rstd = 1.0f / sqrtf(var + kEps);
-  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-  float k = 1.f;
-  if (drop_p > 0.f) {
-    const int st = step ? *step : 0;
-    const unsigned long long h = splitmix64(seed ^ splitmix64(((unsigned long long)st << 32) ^
-                                                              ((unsigned long long)layer << 24) ^
-                                                              (unsigned long long)(n * C + c)));
-    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
-    k = u < drop_p ? 0.f : 1.f / (1.f - drop_p);
-  }
-  float* r = rec + (long long)wid * kRec;
-  r[0] = mu;
-  r[1] = rstd;
-  r[2] = k * g * rstd;
-  r[3] = k * b;
-  r[4] = k;
-  r[5] = g;
-  r[6] = b;
-  r[7] = 0.f;
 }
 
-// out = lrelu(scale2*y2 + shift2 + R),  R = r (identity shortcut) or scale_r*r + shift_r
-template <bool VEC>
+// out = lrelu(scale2*(y2-mean2) + shift2 + R),  R = r (identity) or scale_r*(r-mean_r) + shift_r.
+// With HAS_SRC the records are finalized here from the GEMM partials (no in_finalize launch);
+// workgroup x == 0 of each (n, c) stores them for the backward.
+template <bool VEC, bool HAS_SRC>
 __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
-    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
-    const float* __restrict__ r, long long rns, const float* __restrict__ recr,
-    float* __restrict__ out, long long ons, int C, int S) {
+    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2, l3u_norm_src src2,
+    const float* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
+    int shortcut, float* __restrict__ out, long long ons, int C, int S) {
+  __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
-  const float m2 = rec2[(long long)nc * kRec + 0];
-  const float a2 = rec2[(long long)nc * kRec + 2], b2 = rec2[(long long)nc * kRec + 3];
-  float ar = 1.f, br = 0.f, mr = 0.f;
-  if (recr) {
-    mr = recr[(long long)nc * kRec + 0];
-    ar = recr[(long long)nc * kRec + 2];
-    br = recr[(long long)nc * kRec + 3];
+  float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f;
+  if (HAS_SRC) {
+    block_record(src2, n, c, C, blockIdx.x == 0, sh);
+    if (shortcut) block_record(srcr, n, c, C, blockIdx.x == 0, sh + 8);
+    m2 = sh[0]; a2 = sh[2]; b2 = sh[3];
+    if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; }
+  } else {
+    m2 = rec2[(long long)nc * kRec + 0];
+    a2 = rec2[(long long)nc * kRec + 2];
+    b2 = rec2[(long long)nc * kRec + 3];
+    if (shortcut) {
+      mr = recr[(long long)nc * kRec + 0];
+      ar = recr[(long long)nc * kRec + 2];
+      br = recr[(long long)nc * kRec + 3];
+    }
   }
   const float* yp = y2 + (long long)n * y2ns + (long long)c * S;
   const float* rp = r + (long long)n * rns + (long long)c * S;
@@ -242,23 +212,30 @@ extern "C" {
 int l3u_in_finalize(const float* stat_part, int nsb, const float* gamma, const float* beta,
                     float drop_p, unsigned long long seed, const int* step, int layer, float* rec,
                     int N, int C, hipStream_t stream) {
-  L3U_REQUIRE(N > 0 && C > 0 && nsb > 0 && drop_p >= 0.f && drop_p < 1.f);
+  L3U_REQUIRE(N > 0 && C > 0 && nsb > 0 && drop_p >= 0.f && drop_p < 1.f && rec != nullptr);
   const int NC = N * C;
-  hipLaunchKernelGGL(in_finalize_kernel, dim3((NC + 3) / 4), dim3(256), 0, stream, stat_part, nsb,
-                     gamma, beta, drop_p, seed, step, layer, rec, NC, C);
+  l3u_norm_src src{stat_part, nsb, layer, gamma, beta, drop_p, seed, step, rec};
+  hipLaunchKernelGGL(in_finalize_kernel, dim3((NC + 3) / 4), dim3(256), 0, stream, src, NC, C);
   L3U_CHECK_LAUNCH();
 }
 
 int l3u_norm_act_nblocks(int S) { return elem_blocks(S); }
 
-int l3u_norm_act_fwd(const float* y2, long long y2_nstride, const float* rec2, const float* r,
-                     long long r_nstride, const float* rec_r, float* out, long long out_nstride,
-                     int N, int C, int S, hipStream_t stream) {
+int l3u_norm_act_fwd(const float* y2, long long y2_nstride, const float* rec2,
+                     const l3u_norm_src* src2, const float* r, long long r_nstride,
+                     const float* rec_r, const l3u_norm_src* src_r, int shortcut, float* out,
+                     long long out_nstride, int N, int C, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
+  L3U_REQUIRE(src2 ? (!shortcut || src_r) : (rec2 && (!shortcut || rec_r)));
   const bool vec = S % 4 == 0 && y2_nstride % 4 == 0 && r_nstride % 4 == 0 && out_nstride % 4 == 0;
   dim3 grid(elem_blocks(S), N * C);
-  if (vec) hipLaunchKernelGGL(norm_act_fwd_kernel<true>, grid, dim3(256), 0, stream, y2, y2_nstride, rec2, r, r_nstride, rec_r, out, out_nstride, C, S);
-  else hipLaunchKernelGGL(norm_act_fwd_kernel<false>, grid, dim3(256), 0, stream, y2, y2_nstride, rec2, r, r_nstride, rec_r, out, out_nstride, C, S);
+  const l3u_norm_src z{};
+  const l3u_norm_src s2 = src2 ? *src2 : z, sr = src_r ? *src_r : z;
+#define NAF(V_, S_) hipLaunchKernelGGL((norm_act_fwd_kernel<V_, S_>), grid, dim3(256), 0, stream, y2, \
+      y2_nstride, rec2, s2, r, r_nstride, rec_r, sr, shortcut, out, out_nstride, C, S)
+  if (src2) { if (vec) NAF(true, true); else NAF(false, true); }
+  else { if (vec) NAF(true, false); else NAF(false, false); }
+#undef NAF
   L3U_CHECK_LAUNCH();
 }
 

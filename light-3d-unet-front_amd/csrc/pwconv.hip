@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
     lds[kr * WS + j] = v;
   }
   __syncthreads();
-#pragma unroll 2
+#pragma unroll 8
   for (int k0 = kc0; k0 < kc1; k0 += 4) {
     const int kk = k0 + lk;
     f4 a[NSW];
@@ -184,6 +184,134 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
   }
 }
 
+// Small-volume variant (per-sample S < 8192: the 12^3 / 6^3 levels): the 4 waves of a workgroup
+// share ONE 64-voxel tile and split the reduction dimension K (k-steps interleaved by wave), then
+// combine through LDS in a fixed order; weights are read straight from L2 (they are tiny and
+// every workgroup re-reads them).  This turns an 8-workgroup grid into hundreds.
+template <int NC, bool VEC>
+__global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
+    const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
+    const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
+    float* __restrict__ stat_part, int K, int Nout, int S, int nsb) {
+  constexpr int CO_BLK = 16 * NC;
+  constexpr int T = NC * 16;   // accumulator floats per lane
+  extern __shared__ __attribute__((aligned(16))) float lds[];   // [3 waves][64 lanes][T]
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
+  const int sb = blockIdx.x, co0 = blockIdx.y * CO_BLK, n = blockIdx.z;
+  const float* xn = x + (long long)n * xns;
+  const int s = sb * 64 + 4 * lr;
+  const int ksteps = (K + 3) >> 2;
+  f4 acc[NC][4];
+#pragma unroll
+  for (int m = 0; m < NC; ++m)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[m][q] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int ks = wave; ks < ksteps; ks += 4) {
+    const int kk = 4 * ks + lk;
+    f4 a = {0.f, 0.f, 0.f, 0.f};
+    if (kk < K) {
+      const float* src = xn + (long long)kk * S + s;
+      if (VEC) {
+        if (s < S) a = *reinterpret_cast<const f4*>(src);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (s + q < S) a[q] = src[q];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < NC; ++m) {
+      const int co = co0 + 16 * m + lr;
+      float b = 0.f;
+      if (kk < K && co < Nout) b = wl == 0 ? w[(long long)co * K + kk] : w[(long long)kk * Nout + co];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[m][q] = mfma4(a[q], b, acc[m][q]);
+    }
+  }
+  if (wave > 0) {
+    float* dst = lds + ((wave - 1) * 64 + l) * T;
+#pragma unroll
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[(m * 4 + q) * 4 + r] = acc[m][q][r];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int wv = 0; wv < 3; ++wv) {
+    const float* src = lds + (wv * 64 + l) * T;
+#pragma unroll
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[m][q][r] += src[(m * 4 + q) * 4 + r];
+  }
+  // epilogue (one wave): lane holds Y[co0+16m+lr][sb*64 + 16lk + 4r + q]
+  float* yn = y + (long long)n * yns;
+  const int cnt = min(64, S - sb * 64);
+#pragma unroll
+  for (int m = 0; m < NC; ++m) {
+    const int co = co0 + 16 * m + lr;
+    const bool cok = co < Nout;
+    const float bv = (bias && cok) ? bias[co] : 0.f;
+    float lsum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int sv = sb * 64 + 16 * lk + 4 * r;
+      f4 v = f4{acc[m][0][r], acc[m][1][r], acc[m][2][r], acc[m][3][r]} + bv;
+      float* dst = yn + (long long)co * S + sv;
+      if (cok) {
+        if (VEC) {
+          if (sv < S) {
+            if (accumulate) v += *reinterpret_cast<const f4*>(dst);
+            *reinterpret_cast<f4*>(dst) = v;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (sv + q < S) {
+              if (accumulate) v[q] += dst[q];
+              dst[q] = v[q];
+            }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[m][q][r] = v[q];
+        if (sv + q < S) lsum += v[q];
+      }
+    }
+    if (stat_part != nullptr) {
+      lsum += __shfl_xor(lsum, 16, 64);
+      lsum += __shfl_xor(lsum, 32, 64);
+      const float mean = lsum / (float)cnt;
+      float m2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int sv = sb * 64 + 16 * lk + 4 * r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (sv + q < S) {
+            const float d = acc[m][q][r] - mean;
+            m2 = fmaf(d, d, m2);
+          }
+      }
+      m2 += __shfl_xor(m2, 16, 64);
+      m2 += __shfl_xor(m2, 32, 64);
+      if (lk == 0 && cok) {
+        float* o = stat_part + (((long long)n * Nout + co) * nsb + sb) * 3;
+        o[0] = (float)cnt;
+        o[1] = mean;
+        o[2] = m2;
+      }
+    }
+  }
+}
+
 // dW[j][k] partial over one voxel chunk of one sample.  A = dY (rows j), B = X^T (cols k),
 // the MFMA k-dimension is the voxel: lane l loads float4 dY[j0+16mo+(l&15)][s+4(l>>4)..+3] and
 // X[k0+16mi+(l&15)][s+4(l>>4)..+3]; component q feeds MFMA q.
@@ -207,6 +335,7 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 #pragma unroll
     for (int b = 0; b < NK; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
 
+#pragma unroll 4
   for (int s = s_lo + wave * 16; s < s_hi; s += 64) {
     const int sl = s + 4 * lk;
     f4 av[NJ], bv[NK];
@@ -278,6 +407,8 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 
 int pw_sch(int S) { return S >= 4096 ? 1024 : (S >= 1024 ? 512 : 256); }
 
+bool pw_use_ks(int S) { return S < 8192; }
+
 }  // namespace
 
 extern "C" {
@@ -287,6 +418,28 @@ int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout
                float* stat_part, int N, int K, int Nout, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && K > 0 && Nout > 0 && S > 0);
   const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (y_nstride % 4 == 0);
+  if (pw_use_ks(S)) {
+    // co tile: as wide as possible while keeping >= 256 workgroups
+    const int nsb = (S + 63) / 64;
+    int NC = Nout <= 16 ? 1 : (Nout <= 32 ? 2 : 4);
+    while (NC > 1 && (long long)nsb * ((Nout + 16 * NC - 1) / (16 * NC)) * N < 256) NC >>= 1;
+    const size_t lds = 3 * 64 * (size_t)NC * 16 * sizeof(float);
+    dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), N), block(256);
+#define PWK(NC_)                                                                                  \
+  do {                                                                                            \
+    if (vec) hipLaunchKernelGGL((pw_fwd_ks_kernel<NC_, true>), grid, block, lds, stream, x,      \
+                                x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, \
+                                K, Nout, S, nsb);                                                  \
+    else hipLaunchKernelGGL((pw_fwd_ks_kernel<NC_, false>), grid, block, lds, stream, x,         \
+                            x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K,  \
+                            Nout, S, nsb);                                                         \
+  } while (0)
+    if (NC == 1) PWK(1);
+    else if (NC == 2) PWK(2);
+    else PWK(4);
+#undef PWK
+    L3U_CHECK_LAUNCH();
+  }
   const int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
   const int NC = CO_BLK / 16, NSW = 4 / NC, TSB = 256 * NSW;
   const int nsb = (S + TSB - 1) / TSB;
@@ -313,6 +466,7 @@ int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout
 }
 
 int l3u_pw_stat_nsb(int Nout, int S) {
+  if (pw_use_ks(S)) return (S + 63) / 64;
   const int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
   const int TSB = 256 * (4 / (CO_BLK / 16));
   return (S + TSB - 1) / TSB;
@@ -328,8 +482,15 @@ int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, lon
   L3U_REQUIRE(N > 0 && J > 0 && K > 0 && S > 0);
   const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (dy_nstride % 4 == 0);
   const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
-  const int NJ = J <= 16 ? 1 : (J <= 32 ? 2 : 4);
-  const int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
+  int NJ = J <= 16 ? 1 : (J <= 32 ? 2 : 4);
+  int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
+  // shrink the output tile until the grid has enough workgroups to fill the chip
+  for (;;) {
+    const long long nb = (long long)N * nsc * ((J + 16 * NJ - 1) / (16 * NJ)) *
+                         ((K + 16 * NK - 1) / (16 * NK));
+    if (nb >= 512 || (NJ == 1 && NK == 1)) break;
+    if (NJ >= NK) NJ >>= 1; else NK >>= 1;
+  }
   const int ntj = (J + 16 * NJ - 1) / (16 * NJ), ntk = (K + 16 * NK - 1) / (16 * NK);
   const size_t lds = 64 * (size_t)NJ * NK * 4 * sizeof(float);
   dim3 grid(N * nsc, ntj * ntk), block(256);

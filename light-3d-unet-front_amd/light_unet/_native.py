@@ -22,8 +22,8 @@ U64 = ctypes.c_ulonglong
 # name -> argtypes (stream is always the trailing void*; every function returns int hipError_t)
 _SIGS = {
     "l3u_abi_version": [],
-    "l3u_dw3_nchunk": [I],
-    "l3u_dw3_fwd": [P, L, P, P, P, L, I, I, I, I, I, P],
+    "l3u_dw3_nchunk": [I, I, I],
+    "l3u_dw3_fwd": [P, L, P, P, P, P, L, I, I, I, I, I, P],
     "l3u_dw3_bwd": [P, L, P, L, P, P, P, L, I, P, P, I, I, I, I, I, P],
     "l3u_pw_stat_nsb": [I, I],
     "l3u_pw_fwd": [P, L, P, I, P, P, L, I, P, I, I, I, I, P],
@@ -31,7 +31,7 @@ _SIGS = {
     "l3u_pw_bwd_weight": [P, L, P, L, P, I, I, I, I, P],
     "l3u_in_finalize": [P, I, P, P, F, U64, P, I, P, I, I, P],
     "l3u_norm_act_nblocks": [I],
-    "l3u_norm_act_fwd": [P, L, P, P, L, P, P, L, I, I, I, P],
+    "l3u_norm_act_fwd": [P, L, P, P, P, L, P, P, I, P, L, I, I, I, P],
     "l3u_norm_act_bwd_reduce": [P, L, P, L, P, L, P, P, L, P, P, I, I, I, P],
     "l3u_norm_act_bwd_apply": [P, L, P, L, P, L, P, P, L, P, P, P, L, P, L, I, I, I, P],
     "l3u_in_bwd_apply": [P, L, P, L, P, P, I, P, L, I, I, I, P],
@@ -61,6 +61,17 @@ _lib = None
 
 class NativeError(RuntimeError):
     pass
+
+
+class NormSrc(ctypes.Structure):
+    """struct l3u_norm_src (include/l3u.h): where a consumer kernel finalizes an InstanceNorm
+    record from.  Pass `norm_src_ptr(s)`; keep the object alive across the call."""
+    _fields_ = [("stat_part", P), ("nsb", I), ("layer", I), ("gamma", P), ("beta", P),
+                ("drop_p", F), ("seed", U64), ("step", P), ("rec_out", P)]
+
+
+def norm_src_ptr(s):
+    return None if s is None else ctypes.addressof(s)
 
 
 def load():

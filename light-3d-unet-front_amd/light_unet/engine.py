@@ -243,11 +243,11 @@ class UNetEngine:
         sv["blk"] = blk
         return p, (sv if save else None)
 
-    def _stats_and_finalize(self, flat, name_g, name_b, stat_off, nsb, rec, N, C, drop, cptr, layer, st):
-        g = self._w(flat, name_g)
-        b = self._w(flat, name_b)
-        self._call("l3u_in_finalize", self.fwd_arena.ptr(stat_off), nsb, g, b, float(drop),
-                   self.seed, cptr, layer, rec, N, C, st)
+    def _src(self, flat, norm_prefix, stat_off, nsb, rec_out, drop, cptr, layer):
+        """l3u_norm_src for an InstanceNorm whose statistics partials sit at stat_off."""
+        return nat.NormSrc(self.fwd_arena.ptr(stat_off), nsb, layer,
+                           self._w(flat, norm_prefix + "weight"), self._w(flat, norm_prefix + "bias"),
+                           float(drop), self.seed, cptr or 0, rec_out)
 
     def _block_fwd(self, flat, pre, layer, x, out, dims, drop, cptr, st, dev):
         """ResidualBlock.forward (unet3d.py:77-93) into the view `out`."""
@@ -262,13 +262,15 @@ class UNetEngine:
         rec_r, rec1, rec2 = (recs[0].data_ptr(), recs[1].data_ptr(), recs[2].data_ptr())
         sv = {"x": x, "out": out, "recs": recs}
         shortcut = self._has(pre + "shortcut.0.weight")
+        # InstanceNorm records are finalized inside their consumer kernels from the GEMM
+        # partials (l3u_norm_src); `recs` receives them for the backward pass.
+        src_r = src2 = None
         if shortcut:
             r = e(N, cout, S)
             so = self.fwd_arena.alloc(N * cout * nsb * 3)
             self._call("l3u_pw_fwd", x.p, x.ns, self._w(flat, pre + "shortcut.0.weight"), 0, None,
                        r.data_ptr(), cout * S, 0, self.fwd_arena.ptr(so), N, cin, cout, S, st)
-            self._stats_and_finalize(flat, pre + "shortcut.1.weight", pre + "shortcut.1.bias", so,
-                                     nsb, rec_r, N, cout, 0.0, cptr, 0, st)
+            src_r = self._src(flat, pre + "shortcut.1.", so, nsb, rec_r, 0.0, cptr, 0)
             rv = V(r, 0, cout * S, cout)
             sv["r"] = rv
         else:
@@ -276,24 +278,23 @@ class UNetEngine:
             sv["r"] = None
         z1 = e(N, cin, S)
         self._call("l3u_dw3_fwd", x.p, x.ns, self._w(flat, pre + "conv1.depthwise.weight"), None,
-                   z1.data_ptr(), cin * S, N, cin, d, h, w, st)
+                   None, z1.data_ptr(), cin * S, N, cin, d, h, w, st)
         y1 = e(N, cout, S)
         s1 = self.fwd_arena.alloc(N * cout * nsb * 3)
         self._call("l3u_pw_fwd", z1.data_ptr(), cin * S, self._w(flat, pre + "conv1.pointwise.weight"),
                    0, None, y1.data_ptr(), cout * S, 0, self.fwd_arena.ptr(s1), N, cin, cout, S, st)
-        self._stats_and_finalize(flat, pre + "norm1.weight", pre + "norm1.bias", s1, nsb, rec1, N,
-                                 cout, drop, cptr, 1 + layer, st)
+        src1 = self._src(flat, pre + "norm1.", s1, nsb, rec1, drop, cptr, 1 + layer)
         z2 = e(N, cout, S)
         self._call("l3u_dw3_fwd", y1.data_ptr(), cout * S, self._w(flat, pre + "conv2.depthwise.weight"),
-                   rec1, z2.data_ptr(), cout * S, N, cout, d, h, w, st)
+                   None, nat.norm_src_ptr(src1), z2.data_ptr(), cout * S, N, cout, d, h, w, st)
         y2 = e(N, cout, S)
         s2 = self.fwd_arena.alloc(N * cout * nsb * 3)
         self._call("l3u_pw_fwd", z2.data_ptr(), cout * S, self._w(flat, pre + "conv2.pointwise.weight"),
                    0, None, y2.data_ptr(), cout * S, 0, self.fwd_arena.ptr(s2), N, cout, cout, S, st)
-        self._stats_and_finalize(flat, pre + "norm2.weight", pre + "norm2.bias", s2, nsb, rec2, N,
-                                 cout, 0.0, cptr, 0, st)
-        self._call("l3u_norm_act_fwd", y2.data_ptr(), cout * S, rec2, rv.p, rv.ns,
-                   rec_r if shortcut else None, out.p, out.ns, N, cout, S, st)
+        src2 = self._src(flat, pre + "norm2.", s2, nsb, rec2, 0.0, cptr, 0)
+        self._call("l3u_norm_act_fwd", y2.data_ptr(), cout * S, None, nat.norm_src_ptr(src2), rv.p,
+                   rv.ns, None, nat.norm_src_ptr(src_r), 1 if shortcut else 0, out.p, out.ns, N,
+                   cout, S, st)
         sv.update(z1=z1, y1=y1, z2=z2, y2=y2, dims=dims, shortcut=shortcut)
         return sv
 
@@ -445,7 +446,7 @@ class UNetEngine:
                    N, cout, cout, S, st)
         self._seg(pp2, npw, cout * cout, 1, cout * cout, pre + "conv2.pointwise.weight")
         # (3) conv2.depthwise backward fused with LeakyReLU/Dropout/IN1 backward partials
-        nch = nat.query("l3u_dw3_nchunk", d)
+        nch = nat.query("l3u_dw3_nchunk", d, h, w)
         pd2 = A.alloc(cout * N * nch * 27)
         pi1 = A.alloc(2 * cout * N * nch * 2)          # fp64 partials
         pid = pi1 // 2

@@ -57,7 +57,9 @@ def xform_ref(y, rec):
 
 # ------------------------------------------------------------------------------ depthwise
 DW_SHAPES = [(2, 3, 7, 6, 9), (1, 2, 5, 5, 5), (2, 4, 12, 12, 12), (4, 16, 48, 48, 48),
-             (2, 8, 6, 6, 6), (1, 2, 24, 24, 24), (1, 1, 64, 64, 64)]
+             (2, 8, 6, 6, 6), (1, 2, 24, 24, 24), (1, 1, 64, 64, 64),
+             # x-quad path edge cases: H not a multiple of the row strip, odd D, WQ odd
+             (2, 3, 7, 10, 8), (1, 2, 9, 52, 20), (2, 2, 33, 4, 4), (1, 3, 3, 8, 12)]
 
 
 @pytest.mark.parametrize("shape", DW_SHAPES)
@@ -78,9 +80,43 @@ def test_dw3_fwd(cuda, shape, mode):
     wd = w.float().reshape(C, 27).to(cuda)
     recd = rec.float().to(cuda) if mode else None
     nat().call("l3u_dw3_fwd", buf.data_ptr() + 4 * C * S, 2 * C * S, wd.data_ptr(),
-               recd.data_ptr() if mode else None, y.data_ptr(), C * S, N, C, D, H, W, st())
+               recd.data_ptr() if mode else None, None, y.data_ptr(), C * S, N, C, D, H, W, st())
     torch.cuda.synchronize()
     close(y, ref, 2e-6, f"dw3_fwd{shape} mode{mode}")
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 7, 10, 8), (4, 16, 48, 48, 48), (2, 8, 6, 6, 6)])
+def test_dw3_fwd_inkernel_finalize(cuda, shape):
+    """rec finalized inside the stencil kernel from GEMM partials == l3u_in_finalize + rec path,
+    and the record stored for the backward equals the standalone finalize (incl. dropout)."""
+    N, C, D, H, W = shape
+    S = D * H * W
+    gen = torch.Generator().manual_seed(12)
+    y1 = (torch.randn(N, C, S, generator=gen) * 2 + 0.5).to(cuda)
+    nsb = 5
+    chunks = torch.tensor_split(y1.double().cpu(), nsb, dim=2)
+    part = torch.stack([torch.stack([torch.full((N, C), float(ch.shape[2]), dtype=torch.float64),
+                                     ch.mean(2), ((ch - ch.mean(2, keepdim=True)) ** 2).sum(2)], -1)
+                        for ch in chunks], 2).float().contiguous().to(cuda)
+    gamma = (1 + 0.2 * torch.randn(C, generator=gen)).to(cuda)
+    beta = (0.2 * torch.randn(C, generator=gen)).to(cuda)
+    step = torch.tensor([3], dtype=torch.int32, device=cuda)
+    w = torch.randn(C, 27, generator=gen).to(cuda)
+    rec_a = torch.empty(N * C * 8, device=cuda)
+    nat().call("l3u_in_finalize", part.data_ptr(), nsb, gamma.data_ptr(), beta.data_ptr(), 0.3, 77,
+               step.data_ptr(), 5, rec_a.data_ptr(), N, C, st())
+    ya = torch.empty(N, C, S, device=cuda)
+    nat().call("l3u_dw3_fwd", y1.data_ptr(), C * S, w.data_ptr(), rec_a.data_ptr(), None,
+               ya.data_ptr(), C * S, N, C, D, H, W, st())
+    rec_b = torch.full((N * C * 8,), float("nan"), device=cuda)
+    src = nat().NormSrc(part.data_ptr(), nsb, 5, gamma.data_ptr(), beta.data_ptr(), 0.3, 77,
+                        step.data_ptr(), rec_b.data_ptr())
+    yb = torch.empty(N, C, S, device=cuda)
+    nat().call("l3u_dw3_fwd", y1.data_ptr(), C * S, w.data_ptr(), None, nat().norm_src_ptr(src),
+               yb.data_ptr(), C * S, N, C, D, H, W, st())
+    torch.cuda.synchronize()
+    assert torch.equal(rec_a, rec_b)
+    assert torch.equal(ya, yb)
 
 
 @pytest.mark.parametrize("shape", DW_SHAPES)
@@ -111,7 +147,7 @@ def test_dw3_bwd(cuda, shape, mode):
     else:
         out = F.conv3d(xr, wr, padding=1, groups=C)
         out.backward(dz)
-    nch = nat().query("l3u_dw3_nchunk", D)
+    nch = nat().query("l3u_dw3_nchunk", D, H, W)
     xd = x.float().to(cuda)
     dzd = dz.float().to(cuda)
     wd = w.float().reshape(C, 27).to(cuda)
@@ -273,8 +309,27 @@ def test_norm_act_fwd_bwd(cuda, shape, shortcut):
     recr = rec_of(r, gr, br) if shortcut else None
     y2d, rd, dd = y2.float().to(cuda), r.float().to(cuda), dout.float().to(cuda)
     o = torch.empty(N, C, S, device=cuda)
-    nat().call("l3u_norm_act_fwd", y2d.data_ptr(), C * S, rec2.data_ptr(), rd.data_ptr(), C * S,
-               recr.data_ptr() if shortcut else None, o.data_ptr(), C * S, N, C, S, st())
+    nat().call("l3u_norm_act_fwd", y2d.data_ptr(), C * S, rec2.data_ptr(), None, rd.data_ptr(),
+               C * S, recr.data_ptr() if shortcut else None, None, 1 if shortcut else 0,
+               o.data_ptr(), C * S, N, C, S, st())
+    # same output when the records are finalized in-kernel from (count, mean, M2) partials
+    def src_of(v, g, b, rec_out):
+        part = torch.stack([torch.full((N, C), float(S), dtype=torch.float64), v.mean(-1),
+                            ((v - v.mean(-1, keepdim=True)) ** 2).sum(-1)], -1).float().to(cuda)
+        gd, bd = g.float().to(cuda), b.float().to(cuda)
+        return nat().NormSrc(part.data_ptr(), 1, 0, gd.data_ptr(), bd.data_ptr(), 0.0, 0, None,
+                             rec_out.data_ptr()), (part, gd, bd)
+    ro2 = torch.empty(N * C * 8, device=cuda)
+    ror = torch.empty(N * C * 8, device=cuda)
+    s2, keep2 = src_of(y2, g2, b2, ro2)
+    sr, keepr = src_of(r, gr, br, ror)
+    o2 = torch.empty(N, C, S, device=cuda)
+    nat().call("l3u_norm_act_fwd", y2d.data_ptr(), C * S, None, nat().norm_src_ptr(s2), rd.data_ptr(),
+               C * S, None, nat().norm_src_ptr(sr) if shortcut else None, 1 if shortcut else 0,
+               o2.data_ptr(), C * S, N, C, S, st())
+    torch.cuda.synchronize()
+    close(o2, out, 2e-6, "norm_act out (in-kernel finalize)")
+    close(ro2.view(N, C, 8)[..., :4], rec2.view(N, C, 8)[..., :4], 1e-5, "stored rec2")
     nb = nat().query("l3u_norm_act_nblocks", S)
     part = torch.empty(C * N * nb * 3, dtype=torch.float64, device=cuda)
     nat().call("l3u_norm_act_bwd_reduce", dd.data_ptr(), C * S, o.data_ptr(), C * S, y2d.data_ptr(),
