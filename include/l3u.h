@@ -57,7 +57,7 @@ typedef struct l3u_norm_src {
  *          (DepthwiseSeparableConv3d.depthwise, light_unet/models/unet3d.py:16-17, forward :21)
  * w: [C][27].  rec != NULL fuses a = lrelu(scale*(x-mean) + shift) into the input load (the
  * InstanceNorm1 + LeakyReLU + Dropout3d that precede conv2.depthwise, unet3d.py:84-89).      */
-int l3u_dw3_nchunk(int D, int H, int W);   /* z/y chunks per (n, c): partial-sum count */
+int l3u_dw3_nchunk(int N, int C, int D, int H, int W);   /* z/y chunks per (n, c) */
 int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float* rec,
                 const l3u_norm_src* src, float* y, long long y_nstride, int N, int C, int D,
                 int H, int W, hipStream_t stream);   /* src != NULL: finalize rec in-kernel */

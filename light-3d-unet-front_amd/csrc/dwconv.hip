@@ -298,14 +298,18 @@ struct QGeom {
   int WQ, RS, RB, ny, TZ, nz, threads;
 };
 
-QGeom qgeom(int D, int H, int W) {
+// TZ adapts to the problem: a workgroup's slab is a serial chain of TZ+2 dependent plane steps,
+// so when (n, c, y-strip) alone gives too few workgroups the slabs get thinner (more halo
+// re-reads, served from L2, but shorter chains and more workgroups in flight).
+QGeom qgeom(int N, int C, int D, int H, int W) {
   QGeom g;
   g.WQ = W / 4;
   g.RS = W + 8;
   const int maxrows = 256 / g.WQ;
   g.ny = (H + maxrows - 1) / maxrows;
   g.RB = (H + g.ny - 1) / g.ny;
-  g.TZ = D >= 32 ? 8 : (D >= 8 ? 4 : D);
+  g.TZ = D >= 32 ? 8 : (D > 8 ? 4 : 8);   // TZ in {2, 4, 8}: compile-time in the kernels
+  while (g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < 2048) g.TZ >>= 1;
   g.nz = (D + g.TZ - 1) / g.TZ;
   g.threads = ((g.RB * g.WQ + 63) / 64) * 64;
   return g;
@@ -363,40 +367,49 @@ struct QPre {
   f4 v[2];
 };
 
-L3U_DEV void q_fetch(QPre& p, const float* src, int y0, int rows, int H, int W, int WQ) {
+// Per-thread staging map, computed once: global offset (within a plane) and LDS offset of the
+// thread's <= 2 quads.  Loads are issued UNCONDITIONALLY from clamped, always-valid addresses
+// (branch-free straight-line loads let the compiler count vmcnt exactly instead of draining
+// the whole pipeline with vmcnt(0)); the validity mask is applied at commit.
+struct QMap {
+  int goff[2], loff[2];
+  bool ok[2];
+};
+
+L3U_DEV QMap q_map(int y0, int rows, int H, int W, int WQ, int RS) {
+  QMap m;
   const int nq = (rows + 2) * WQ;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int q = threadIdx.x + k * blockDim.x;
-    if (q < nq) {
-      const int lr = q / WQ, x = (q - lr * WQ) * 4, y = y0 - 1 + lr;
-      if (y >= 0 && y < H) p.v[k] = *reinterpret_cast<const f4*>(src + (long long)y * W + x);
-    }
+    const int qc = q < nq ? q : 0;
+    const int lr = qc / WQ, x = (qc - lr * WQ) * 4, y = y0 - 1 + lr;
+    m.ok[k] = q < nq && y >= 0 && y < H;
+    m.goff[k] = min(max(y, 0), H - 1) * W + x;
+    m.loff[k] = lr * RS + 4 + x;
   }
+  return m;
+}
+
+L3U_DEV void q_fetch(QPre& p, const float* plane, const QMap& m) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) p.v[k] = *reinterpret_cast<const f4*>(plane + m.goff[k]);
 }
 
 template <int MODE>
-L3U_DEV void q_commit(const QPre& p, float* plane, int y0, int rows, int H, int WQ, int RS,
-                      float sc, float mu, float sh) {
-  const int nq = (rows + 2) * WQ;
+L3U_DEV void q_commit(const QPre& p, float* lplane, const QMap& m, float sc, float mu, float sh) {
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    const int q = threadIdx.x + k * blockDim.x;
-    if (q < nq) {
-      const int lr = q / WQ, x = (q - lr * WQ) * 4, y = y0 - 1 + lr;
-      if (y >= 0 && y < H) {
-        f4 v = p.v[k];
-        if (MODE == 1) {
+    f4 v = p.v[k];
+    if (MODE == 1) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(sc, v[i] - mu, sh));
-        }
-        *reinterpret_cast<f4*>(plane + lr * RS + 4 + x) = v;
-      }
+      for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(sc, v[i] - mu, sh));
     }
+    if (m.ok[k]) *reinterpret_cast<f4*>(lplane + m.loff[k]) = v;
   }
 }
 
-template <int MODE>
+template <int MODE, int TZC>
 __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w,
     const float* __restrict__ rec, l3u_norm_src src, int has_src, float* __restrict__ y,
@@ -425,14 +438,23 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
   __syncthreads();
   f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0;
   const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
-  QPre pre;
-  q_fetch(pre, xp + (long long)zlo * HW, b.y0, b.rows, H, W, WQ);
-  for (int zi = zlo; zi <= zhi; ++zi) {
-    float* buf = lds + (zi & 1) * PP;
-    q_commit<MODE>(pre, buf, b.y0, b.rows, H, WQ, RS, sc, mu, sh);
-    if (zi < zhi) q_fetch(pre, xp + (long long)(zi + 1) * HW, b.y0, b.rows, H, W, WQ);
+  // two planes staged in registers ahead of the one being consumed (2-deep load pipeline)
+  const QMap qm = q_map(b.y0, b.rows, H, W, WQ, RS);
+  auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };   // loads always issue
+  // step t consumes input plane zi = z0-1+t; the step count is a compile-time constant and the
+  // loop is fully unrolled, so the staged registers never move (no back-edge copies that would
+  // force a vmcnt(0) drain of the pipeline)
+  QPre p0, p1;
+  q_fetch(p0, xp + zc(b.z0 - 1), qm);
+  q_fetch(p1, xp + zc(b.z0), qm);
+  auto step = [&](int t, QPre& pre) {
+    const int zi = b.z0 - 1 + t;
+    const bool in = zi >= zlo && zi <= zhi;
+    float* buf = lds + (t & 1) * PP;
+    if (in) q_commit<MODE>(pre, buf, qm, sc, mu, sh);
+    q_fetch(pre, xp + zc(zi + 2), qm);
     __syncthreads();
-    if (b.own) {
+    if (b.own && in) {
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         float v[6];
@@ -448,21 +470,22 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
           }
         }
       }
-      const int zo = zi - 1;
-      if (zo >= b.z0 && zo < b.z1)
-        *reinterpret_cast<f4*>(yp + (long long)zo * HW + (long long)(b.y0 + b.oy) * W + b.ox) = a0;
     }
+    const int zo = zi - 1;   // output plane zo has all three input planes now
+    if (b.own && zo >= b.z0 && zo < b.z1)
+      *reinterpret_cast<f4*>(yp + (long long)zo * HW + (long long)(b.y0 + b.oy) * W + b.ox) = a0;
     a0 = a1;
     a1 = a2;
     a2 = f4{0.f, 0.f, 0.f, 0.f};
-  }
-  // the last owned plane when the slab ends at the volume end (no plane z1 to drive the store)
-  if (b.own && b.z1 == D && D - 1 >= b.z0 && zhi == D - 1) {
-    *reinterpret_cast<f4*>(yp + (long long)(D - 1) * HW + (long long)(b.y0 + b.oy) * W + b.ox) = a0;
+  };
+#pragma unroll
+  for (int t = 0; t < TZC + 2; t += 2) {
+    step(t, p0);
+    step(t + 1, p1);
   }
 }
 
-template <int MODE>
+template <int MODE, int TZC>
 __global__ __launch_bounds__(256) void dw3q_bwd_kernel(
     const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
@@ -495,30 +518,37 @@ __global__ __launch_bounds__(256) void dw3q_bwd_kernel(
   double s1 = 0.0, s2 = 0.0;
   const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
   const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
-  const int nsteps = b.z1 - b.z0 + 3;
-  QPre pz, pa;     // staged dZ plane zd and A plane za of the NEXT step
+  constexpr int nsteps = TZC + 3;   // compile-time step count: the step loop fully unrolls
+  // staged dZ / A planes of the next two steps (2-deep register pipeline)
+  QPre pz0, pa0, pz1, pa1;
+  const QMap qm = q_map(b.y0, b.rows, H, W, WQ, RS);
+  auto in_rng = [&](int z) { return z >= zlo && z <= zhi; };
+  auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };  // clamped plane offset
   {
     const int zd = b.z0 - 1, za = zd - 1;
-    if (zd >= zlo && zd <= zhi) q_fetch(pz, dzp + (long long)zd * HW, b.y0, b.rows, H, W, WQ);
-    if (za >= zlo && za <= zhi) q_fetch(pa, xp + (long long)za * HW, b.y0, b.rows, H, W, WQ);
+    q_fetch(pz0, dzp + zc(zd), qm);
+    q_fetch(pa0, xp + zc(za), qm);
+    q_fetch(pz1, dzp + zc(zd + 1), qm);
+    q_fetch(pa1, xp + zc(za + 1), qm);
   }
   __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
+  auto step = [&](int s, QPre& pz, QPre& pa) {
     const int zd = b.z0 - 1 + s, za = zd - 1;
     float* dbuf = dzb + (s & 1) * PP;
     float* abuf = ab + (s & 1) * PP;
-    const bool ldz = zd >= zlo && zd <= zhi;
-    const bool la = za >= zlo && za <= zhi;
-    if (ldz) q_commit<0>(pz, dbuf, b.y0, b.rows, H, WQ, RS, 1.f, 0.f, 0.f);
-    if (la) q_commit<MODE>(pa, abuf, b.y0, b.rows, H, WQ, RS, sc, mean, sh);
-    // issue the next step's plane loads and this step's epilogue loads before the barrier
-    if (zd + 1 >= zlo && zd + 1 <= zhi) q_fetch(pz, dzp + (long long)(zd + 1) * HW, b.y0, b.rows, H, W, WQ);
-    if (za + 1 >= zlo && za + 1 <= zhi) q_fetch(pa, xp + (long long)(za + 1) * HW, b.y0, b.rows, H, W, WQ);
+    const bool ldz = in_rng(zd);
+    const bool la = in_rng(za);
+    if (ldz) q_commit<0>(pz, dbuf, qm, 1.f, 0.f, 0.f);
+    if (la) q_commit<MODE>(pa, abuf, qm, sc, mean, sh);
+    // issue the loads of step s+2 and this step's epilogue load before the barrier; all loads
+    // are unconditional (clamped addresses) so the waits stay counted, never vmcnt(0)
+    q_fetch(pz, dzp + zc(zd + 2), qm);
+    q_fetch(pa, xp + zc(za + 2), qm);
     const int zf = zd - 1;   // dA plane zf completes in this step
     const bool fin = b.own && zf >= b.z0 && zf < b.z1;
     f4 epi = zero4;
-    if (fin && (MODE == 1 || accumulate))
-      epi = *reinterpret_cast<const f4*>((MODE == 1 ? xp : dxp) + (long long)zf * HW + qofs);
+    if (MODE == 1 || accumulate)
+      epi = *reinterpret_cast<const f4*>((MODE == 1 ? xp : dxp) + (long long)min(max(zf, 0), D - 1) * HW + qofs);
     __syncthreads();
     const bool zd_owned = zd >= b.z0 && zd < b.z1;
     if (b.own) {
@@ -588,6 +618,11 @@ __global__ __launch_bounds__(256) void dw3q_bwd_kernel(
     d0 = d1;
     d1 = d2;
     d2 = zero4;
+  };
+#pragma unroll
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, pz0, pa0);
+    if (s + 1 < nsteps) step(s + 1, pz1, pa1);
   }
   // workgroup reduction (fixed order) of the 27 taps and the 2 fp64 IN sums
   __syncthreads();
@@ -635,9 +670,9 @@ __global__ __launch_bounds__(256) void dw3q_bwd_kernel(
 
 extern "C" {
 
-int l3u_dw3_nchunk(int D, int H, int W) {
+int l3u_dw3_nchunk(int N, int C, int D, int H, int W) {
   if (use_quads(H, W)) {
-    const QGeom g = qgeom(D, H, W);
+    const QGeom g = qgeom(N, C, D, H, W);
     return g.nz * g.ny;
   }
   return (D + pick_tz(D) - 1) / pick_tz(D);
@@ -652,11 +687,14 @@ int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float
   const int has = src ? 1 : 0;
   const bool xf = rec != nullptr || src != nullptr;
   if (use_quads(H, W) && x_nstride % 4 == 0 && y_nstride % 4 == 0) {
-    const QGeom g = qgeom(D, H, W);
+    const QGeom g = qgeom(N, C, D, H, W);
     const size_t lds = (2 * (size_t)(g.RB + 2) * g.RS + 8) * sizeof(float);
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
-    if (xf) hipLaunchKernelGGL(dw3q_fwd_kernel<1>, grid, block, lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, C, D, H, W, g.RB, g.ny, g.TZ, g.nz);
-    else hipLaunchKernelGGL(dw3q_fwd_kernel<0>, grid, block, lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, C, D, H, W, g.RB, g.ny, g.TZ, g.nz);
+#define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<M_, T_>), grid, block, lds, stream, x, \
+      x_nstride, w, rec, s, has, y, y_nstride, C, D, H, W, g.RB, g.ny, g.TZ, g.nz)
+    if (xf) { if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
+    else { if (g.TZ == 8) DWQF(0, 8); else if (g.TZ == 4) DWQF(0, 4); else DWQF(0, 2); }
+#undef DWQF
     L3U_CHECK_LAUNCH();
   }
   L3U_REQUIRE(H * W <= 4096);
@@ -676,12 +714,16 @@ int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long
   L3U_REQUIRE(N > 0 && C > 0 && D > 0 && H > 0 && W > 0);
   L3U_REQUIRE(rec == nullptr || in_part != nullptr);
   if (use_quads(H, W) && x_nstride % 4 == 0 && dz_nstride % 4 == 0 && dx_nstride % 4 == 0) {
-    const QGeom g = qgeom(D, H, W);
+    const QGeom g = qgeom(N, C, D, H, W);
     size_t lds = 4 * (size_t)(g.RB + 2) * g.RS * sizeof(float);
     if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
-    if (rec) hipLaunchKernelGGL(dw3q_bwd_kernel<1>, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part, in_part, N, C, D, H, W, g.RB, g.ny, g.TZ, g.nz);
-    else hipLaunchKernelGGL(dw3q_bwd_kernel<0>, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part, in_part, N, C, D, H, W, g.RB, g.ny, g.TZ, g.nz);
+#define DWQB(M_, T_) hipLaunchKernelGGL((dw3q_bwd_kernel<M_, T_>), grid, block, lds, stream, dz, \
+      dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part, in_part, N, C, D, H, W, \
+      g.RB, g.ny, g.TZ, g.nz)
+    if (rec) { if (g.TZ == 8) DWQB(1, 8); else if (g.TZ == 4) DWQB(1, 4); else DWQB(1, 2); }
+    else { if (g.TZ == 8) DWQB(0, 8); else if (g.TZ == 4) DWQB(0, 4); else DWQB(0, 2); }
+#undef DWQB
     L3U_CHECK_LAUNCH();
   }
   L3U_REQUIRE(H * W <= 4096);

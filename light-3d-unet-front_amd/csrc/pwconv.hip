@@ -407,7 +407,7 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 
 int pw_sch(int S) { return S >= 4096 ? 1024 : (S >= 1024 ? 512 : 256); }
 
-bool pw_use_ks(int S) { return S < 8192; }
+bool pw_use_ks(int S) { return S < 32768; }
 
 }  // namespace
 

@@ -22,7 +22,7 @@ U64 = ctypes.c_ulonglong
 # name -> argtypes (stream is always the trailing void*; every function returns int hipError_t)
 _SIGS = {
     "l3u_abi_version": [],
-    "l3u_dw3_nchunk": [I, I, I],
+    "l3u_dw3_nchunk": [I, I, I, I, I],
     "l3u_dw3_fwd": [P, L, P, P, P, P, L, I, I, I, I, I, P],
     "l3u_dw3_bwd": [P, L, P, L, P, P, P, L, I, P, P, I, I, I, I, I, P],
     "l3u_pw_stat_nsb": [I, I],

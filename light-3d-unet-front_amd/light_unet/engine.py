@@ -446,7 +446,7 @@ class UNetEngine:
                    N, cout, cout, S, st)
         self._seg(pp2, npw, cout * cout, 1, cout * cout, pre + "conv2.pointwise.weight")
         # (3) conv2.depthwise backward fused with LeakyReLU/Dropout/IN1 backward partials
-        nch = nat.query("l3u_dw3_nchunk", d, h, w)
+        nch = nat.query("l3u_dw3_nchunk", N, cout, d, h, w)
         pd2 = A.alloc(cout * N * nch * 27)
         pi1 = A.alloc(2 * cout * N * nch * 2)          # fp64 partials
         pid = pi1 // 2
@@ -476,11 +476,12 @@ class UNetEngine:
             self._call("l3u_pw_bwd_weight", drv.p, drv.ns, x.p, x.ns, A.ptr(ppr), N, cout, cin, S, st)
             self._seg(ppr, npw, cout * cin, 1, cout * cin, pre + "shortcut.0.weight")
         # (6) conv1.depthwise backward accumulates into d(input)
-        pd1 = A.alloc(cin * N * nch * 27)
+        nch1 = nat.query("l3u_dw3_nchunk", N, cin, d, h, w)
+        pd1 = A.alloc(cin * N * nch1 * 27)
         self._call("l3u_dw3_bwd", dz1.data_ptr(), cin * S, x.p, x.ns,
                    self._w(flat, pre + "conv1.depthwise.weight"), None, dxv.p, dxv.ns, 1, A.ptr(pd1),
                    None, N, cin, d, h, w, st)
-        self._seg_dw(pd1, N * nch, cin, pre + "conv1.depthwise.weight")
+        self._seg_dw(pd1, N * nch1, cin, pre + "conv1.depthwise.weight")
         if self.debug is not None and not self._dry:
             self.debug[pre + "#"] = {"dy2": dy2, "dr": drv, "dz2": dz2, "dy1": dy1, "dz1": dz1,
                                      "dx": dxv}

@@ -147,7 +147,7 @@ def test_dw3_bwd(cuda, shape, mode):
     else:
         out = F.conv3d(xr, wr, padding=1, groups=C)
         out.backward(dz)
-    nch = nat().query("l3u_dw3_nchunk", D, H, W)
+    nch = nat().query("l3u_dw3_nchunk", N, C, D, H, W)
     xd = x.float().to(cuda)
     dzd = dz.float().to(cuda)
     wd = w.float().reshape(C, 27).to(cuda)
