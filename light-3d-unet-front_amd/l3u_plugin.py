@@ -1,0 +1,72 @@
+"""Installs the MI355X hot path into an existing reference `light_unet` package.
+
+The reference Trainer / Inferencer import the model and loss by module path
+(trainer.py:16-17, inferencer.py:13) next to modules this build does not replace
+(light_unet.datasets, light_unet.core.config, light_unet.models.metrics).  Both packages are
+called `light_unet`, so this build is loaded under the alias `l3u_amd` (its modules only use
+relative imports) and its classes are bound into the reference's module objects:
+
+    import l3u_plugin
+    l3u_plugin.install()                       # before `from light_unet.core.trainer import Trainer`
+    from light_unet.core.trainer import Trainer
+
+After install():
+    light_unet.models.unet3d.Lightweight3DUNet      -> l3u_amd.models.unet3d.Lightweight3DUNet
+    light_unet.models.losses.FocalTverskyLoss       -> l3u_amd.models.losses.FocalTverskyLoss
+    light_unet.models.losses.get_loss_function      -> l3u_amd.models.losses.get_loss_function
+    light_unet.models.Lightweight3DUNet / get_loss_function (package re-exports, models/__init__.py:6-8)
+Everything else in the reference package is left untouched.
+"""
+import importlib
+import importlib.util
+import os
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ALIAS = "l3u_amd"
+
+REPLACED = {
+    "light_unet.models.unet3d": ("Lightweight3DUNet",),
+    "light_unet.models.losses": ("FocalTverskyLoss", "get_loss_function"),
+    "light_unet.models": ("Lightweight3DUNet", "FocalTverskyLoss", "get_loss_function"),
+}
+
+
+def load():
+    """This build's package, imported as `l3u_amd` (no clash with the reference's light_unet)."""
+    if ALIAS in sys.modules:
+        return sys.modules[ALIAS]
+    pkg_dir = os.path.join(_HERE, "light_unet")
+    spec = importlib.util.spec_from_file_location(
+        ALIAS, os.path.join(pkg_dir, "__init__.py"), submodule_search_locations=[pkg_dir])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[ALIAS] = mod
+    spec.loader.exec_module(mod)
+    importlib.import_module(ALIAS + ".models.unet3d")
+    importlib.import_module(ALIAS + ".models.losses")
+    return mod
+
+
+def install():
+    """Bind this build's model and loss into the already-importable reference package.
+    Returns {module: [names]} of what was replaced.  Raises ImportError when the reference's
+    light_unet.models.{unet3d,losses} cannot be imported (nothing is half-installed)."""
+    amd = load()
+    src = {
+        "Lightweight3DUNet": sys.modules[ALIAS + ".models.unet3d"].Lightweight3DUNet,
+        "FocalTverskyLoss": sys.modules[ALIAS + ".models.losses"].FocalTverskyLoss,
+        "get_loss_function": sys.modules[ALIAS + ".models.losses"].get_loss_function,
+    }
+    mods = {}
+    for modname in ("light_unet.models.unet3d", "light_unet.models.losses"):
+        mods[modname] = importlib.import_module(modname)
+    pkg = sys.modules.get("light_unet.models")
+    if pkg is not None:
+        mods["light_unet.models"] = pkg
+    done = {}
+    for modname, mod in mods.items():
+        for name in REPLACED[modname]:
+            setattr(mod, name, src[name])
+        done[modname] = list(REPLACED[modname])
+    amd.installed_into = done
+    return done

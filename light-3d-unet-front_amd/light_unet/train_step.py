@@ -14,9 +14,9 @@ Both collectives are RCCL over xGMI (torch.distributed backend "nccl") on one fl
 24 B and 0.87 MB (3.25 MB for the 32->256 model) per step.
 """
 import torch
-import torch.distributed as dist
 
 from . import _native as nat
+from .exchange import check_mode, exchange_ftl_sums, exchange_grads, world_size
 from .optim import FlatAdamW
 
 
@@ -29,8 +29,7 @@ class TrainStep:
         self.gamma = float(loss_cfg.get("gamma", 0.75))
         self.smooth = float(loss_cfg.get("smooth", 1e-6))
         assert abs(self.alpha + self.beta - 1.0) < 1e-6
-        if ftl_mode not in ("exact", "local"):
-            raise ValueError("ftl_mode must be 'exact' or 'local'")
+        check_mode(ftl_mode)
         self.model = model
         self.engine = model.engine
         self.flat = model.flat_parameters()
@@ -38,8 +37,7 @@ class TrainStep:
         self.opt = FlatAdamW(self.flat, self.gflat, lr=lr, betas=betas, eps=eps,
                              weight_decay=weight_decay)
         self.group = group
-        self.world = dist.get_world_size(group) if (group is not None or (
-            dist.is_available() and dist.is_initialized())) else 1
+        self.world = world_size(group)
         self.ftl_mode = ftl_mode
         dev = self.flat.device
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
@@ -68,15 +66,10 @@ class TrainStep:
         self.engine.backward(self.flat, self.gflat, sv, dp, need_dx=False)
 
     def _grad_exchange(self):
-        if self.world > 1:
-            if self.ftl_mode == "local":
-                dist.all_reduce(self.gflat, op=dist.ReduceOp.AVG, group=self.group)
-            else:
-                dist.all_reduce(self.gflat, op=dist.ReduceOp.SUM, group=self.group)
+        exchange_grads(self.gflat, self.ftl_mode, self.group)
 
     def _sums_exchange(self, sums):
-        if self.world > 1 and self.ftl_mode == "exact":
-            dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=self.group)
+        exchange_ftl_sums(sums, self.ftl_mode, self.group)
 
     # ----------------------------------------------------------------- eager step
     def __call__(self, x, t):

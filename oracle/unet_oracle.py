@@ -89,13 +89,18 @@ def focal_tversky(pred, target, alpha=0.7, beta=0.3, gamma=0.75, smooth=1e-6):
     return (1 - ti) ** gamma
 
 
-def ftl_grad_closed_form(pred, target, alpha=0.7, beta=0.3, gamma=0.75, smooth=1e-6):
-    """dL/dp_i in closed form; depends only on t_i and the 3 global sums."""
+def ftl_sums(pred, target):
+    """(tp, fp, fn) of losses.py:40-42 as a float64 [3] tensor."""
     p = pred.reshape(-1).double()
     t = target.reshape(-1).double()
-    tp = (p * t).sum()
-    fp = (p * (1 - t)).sum()
-    fn = ((1 - p) * t).sum()
+    return torch.stack([(p * t).sum(), (p * (1 - t)).sum(), ((1 - p) * t).sum()])
+
+
+def ftl_grad_closed_form(pred, target, alpha=0.7, beta=0.3, gamma=0.75, smooth=1e-6, sums=None):
+    """dL/dp_i in closed form; depends only on t_i and the 3 global sums.
+    `sums` overrides the (tp, fp, fn) of `pred` (e.g. the all-reduced sums of a sharded batch)."""
+    t = target.reshape(-1).double()
+    tp, fp, fn = (sums if sums is not None else ftl_sums(pred, target)).double()
     dn = tp + alpha * fn + beta * fp + smooth
     ti = (tp + smooth) / dn
     dti = (t * dn - (tp + smooth) * (t * (1 - alpha) + beta * (1 - t))) / (dn * dn)
