@@ -288,59 +288,82 @@ __global__ __launch_bounds__(256) void dw3_bwd_kernel(
 int pick_tz(int D) { return D <= 8 ? D : 4; }
 
 // ------------------------------------------------------------------------------------------------
-// x-quad variants (W % 4 == 0, every production shape): a workgroup owns (n, c, TZ z-planes,
-// RB rows); a thread owns 4 consecutive x of one row.  Global traffic is float4 per lane (one
-// 16-B load per input quad per plane, one 16-B store per output quad), the LDS plane image has
-// rows [4 zero pad | W | 4 zero pad] so the quad lands 16-B aligned (ds_write_b128) and the 3x6
-// neighbourhood of a quad is 3 ds_read_b128 + 6 ds_read_b32 (vs 36 scalar reads).
+// x-quad variants (W % 4 == 0, 4 <= W <= 256: every production shape).  A workgroup owns
+// (n, c, TZ z-planes, RB rows); a thread owns 4 consecutive x of one row and each wave owns RPW
+// WHOLE rows (RPW = 64 / (W/4)).  Global traffic is float4 per lane (one 16-B load per input
+// quad per plane, one 16-B store per output quad).  The LDS plane image is unpadded
+// [RB+2 rows][W]: the quad of each row is one conflict-free ds_read_b128 (a wave's lanes read
+// contiguous 16-B slots), and the x-neighbours of a quad come from the adjacent lanes through
+// DPP wave shifts (zero at row ends = the conv's zero padding) instead of 4-way bank-conflicted
+// 4-byte LDS reads.  Planes outside the volume are committed as zeros, so the stencil never
+// branches on z; input planes are staged through registers PD steps ahead of their use.
 // ------------------------------------------------------------------------------------------------
+// occupancy target (waves per SIMD; the IN-fused MODE 1 needs more registers and runs at 2) and
+// register prefetch depth of the quad backward kernel; dW taps as scalar or x-pair partial sums
+// (measured on MI355X, tools/kbench.py: scalar / 3 waves / depth 1 is the fastest at the model's
+// shapes)
+#ifndef L3U_DWB_WAVES
+#define L3U_DWB_WAVES 3
+#endif
+#ifndef L3U_DWB_PD
+#define L3U_DWB_PD 1
+#endif
+#ifndef L3U_GW_SCALAR
+#define L3U_GW_SCALAR 1
+#endif
+
 struct QGeom {
-  int WQ, RS, RB, ny, TZ, nz, threads;
+  int WQ, RPW, NW, RB, ny, TZ, nz, threads;
 };
 
-// TZ adapts to the problem: a workgroup's slab is a serial chain of TZ+2 dependent plane steps,
-// so when (n, c, y-strip) alone gives too few workgroups the slabs get thinner (more halo
-// re-reads, served from L2, but shorter chains and more workgroups in flight).
+// rows per block: the wave count (1..4) that wastes the fewest row slots over ny strips
 QGeom qgeom(int N, int C, int D, int H, int W) {
   QGeom g;
   g.WQ = W / 4;
-  g.RS = W + 8;
-  const int maxrows = 256 / g.WQ;
-  g.ny = (H + maxrows - 1) / maxrows;
-  g.RB = (H + g.ny - 1) / g.ny;
+  g.RPW = 64 / g.WQ;
+  int best = 1;
+  double beff = -1.0;
+  for (int nw = 1; nw <= 4; ++nw) {
+    if ((nw - 1) * g.RPW >= H) break;   // a wave with no row at all
+    const int rb = nw * g.RPW, ny = (H + rb - 1) / rb;
+    const double eff = (double)H / (ny * rb);
+    if (eff > beff + 1e-9) { beff = eff; best = nw; }
+  }
+  g.NW = best;
+  g.RB = best * g.RPW;
+  g.ny = (H + g.RB - 1) / g.RB;
+  g.threads = 64 * best;
   g.TZ = D >= 32 ? 8 : (D > 8 ? 4 : 8);   // TZ in {2, 4, 8}: compile-time in the kernels
-  while (g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < 2048) g.TZ >>= 1;
+  while (g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < 1024) g.TZ >>= 1;
   g.nz = (D + g.TZ - 1) / g.TZ;
-  g.threads = ((g.RB * g.WQ + 63) / 64) * 64;
   return g;
 }
 
 bool use_quads(int H, int W) {
-  if (W % 4 != 0 || W < 4 || W > 1024 || H < 1) return false;
-  const int WQ = W / 4, maxrows = 256 / WQ;
-  const int ny = (H + maxrows - 1) / maxrows, RB = (H + ny - 1) / ny;
-  const int threads = ((RB * WQ + 63) / 64) * 64;
-  return (RB + 2) * WQ <= 2 * threads;   // register staging: <= 2 quads per thread per plane
+  if (W % 4 != 0 || W < 4 || W > 256 || H < 1) return false;
+  const QGeom g = qgeom(1, 1, 1, H, W);
+  return (g.RB + 2) * g.WQ <= 2 * g.threads;   // register staging: <= 2 quads per thread
 }
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
-// the 6 values of LDS row `row` around the quad at column ox: cols ox-1 .. ox+4
-L3U_DEV void q_row(const float* plane, int row, int RS, int ox, float v[6]) {
-  const float* b = plane + row * RS + 4 + ox;
-  const f4 m = *reinterpret_cast<const f4*>(b);
-  v[0] = b[-1];
-  v[1] = m[0]; v[2] = m[1]; v[3] = m[2]; v[4] = m[3];
-  v[5] = b[4];
+L3U_DEV f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+L3U_DEV float lane_prev(float v) {   // value of lane l-1 (DPP wave_shr:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+L3U_DEV float lane_next(float v) {   // value of lane l+1 (DPP wave_shl:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
 // block decode shared by both quad kernels
 struct QBlock {
   int n, c, nc, z0, z1, y0, rows, oy, ox, ck;
-  bool own;
+  bool own, el, er;
 };
 
-L3U_DEV QBlock q_decode(int C, int D, int H, int RB, int ny, int TZ, int nz, int WQ) {
+L3U_DEV QBlock q_decode(int C, int D, int H, int RB, int RPW, int ny, int TZ, int nz, int WQ) {
   QBlock b;
   int t = xcd_remap(blockIdx.x, gridDim.x);
   b.ck = t % (ny * nz);
@@ -353,16 +376,28 @@ L3U_DEV QBlock q_decode(int C, int D, int H, int RB, int ny, int TZ, int nz, int
   b.z1 = min(b.z0 + TZ, D);
   b.y0 = yb * RB;
   b.rows = min(RB, H - b.y0);
-  const int q = threadIdx.x;
-  b.own = q < b.rows * WQ;
-  b.oy = b.own ? q / WQ : 0;
-  b.ox = b.own ? (q - b.oy * WQ) * 4 : 0;
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int lr = ln / WQ, qx = ln - lr * WQ;
+  const int oy = wv * RPW + lr;
+  b.own = lr < RPW && oy < b.rows;
+  b.oy = b.own ? oy : 0;     // idle lanes read a valid row and never store
+  b.ox = qx * 4;
+  b.el = qx == 0;
+  b.er = qx == WQ - 1;
   return b;
 }
 
-// Register-staged plane loads (issue early, commit to LDS one step later: the global-load
-// latency hides under the previous plane's stencil).  A thread stages at most 2 quads per plane:
-// the host guarantees (RB + 2) * WQ <= 2 * blockDim.
+// the 6 values around the quad of LDS row `row`: v[0] = x-1 .. v[5] = x+4.  Every lane of the
+// wave must execute this (DPP reads the neighbouring lanes).
+L3U_DEV void q_nbr(const float* plane, int row, int W, int ox, bool el, bool er, float v[6]) {
+  const f4 m = *reinterpret_cast<const f4*>(plane + row * W + ox);
+  const float l = lane_prev(m[3]), r = lane_next(m[0]);
+  v[0] = el ? 0.f : l;
+  v[1] = m[0]; v[2] = m[1]; v[3] = m[2]; v[4] = m[3];
+  v[5] = er ? 0.f : r;
+}
+
+// Register-staged plane loads (issued early, committed to LDS when their step comes up).
 struct QPre {
   f4 v[2];
 };
@@ -370,13 +405,14 @@ struct QPre {
 // Per-thread staging map, computed once: global offset (within a plane) and LDS offset of the
 // thread's <= 2 quads.  Loads are issued UNCONDITIONALLY from clamped, always-valid addresses
 // (branch-free straight-line loads let the compiler count vmcnt exactly instead of draining
-// the whole pipeline with vmcnt(0)); the validity mask is applied at commit.
+// the whole pipeline with vmcnt(0)); the validity mask is applied at commit.  LDS rows outside
+// the volume (y = -1, y = H) are never written and stay zero.
 struct QMap {
   int goff[2], loff[2];
   bool ok[2];
 };
 
-L3U_DEV QMap q_map(int y0, int rows, int H, int W, int WQ, int RS) {
+L3U_DEV QMap q_map(int y0, int rows, int H, int W, int WQ) {
   QMap m;
   const int nq = (rows + 2) * WQ;
 #pragma unroll
@@ -386,7 +422,7 @@ L3U_DEV QMap q_map(int y0, int rows, int H, int W, int WQ, int RS) {
     const int lr = qc / WQ, x = (qc - lr * WQ) * 4, y = y0 - 1 + lr;
     m.ok[k] = q < nq && y >= 0 && y < H;
     m.goff[k] = min(max(y, 0), H - 1) * W + x;
-    m.loff[k] = lr * RS + 4 + x;
+    m.loff[k] = lr * W + x;
   }
   return m;
 }
@@ -396,27 +432,40 @@ L3U_DEV void q_fetch(QPre& p, const float* plane, const QMap& m) {
   for (int k = 0; k < 2; ++k) p.v[k] = *reinterpret_cast<const f4*>(plane + m.goff[k]);
 }
 
-template <int MODE>
-L3U_DEV void q_commit(const QPre& p, float* lplane, const QMap& m, float sc, float mu, float sh) {
+// commit a staged plane to LDS (zeros for a plane outside the needed z range)
+template <bool XF>
+L3U_DEV void q_commit(const QPre& p, float* lplane, const QMap& m, bool in, float sc, float mu,
+                      float sh) {
+  // out of range: XF folds the zero into the transform (lrelu(0*(v-mu) + 0) = 0), plain
+  // planes multiply by 0 (two v_pk_mul per quad instead of four selects)
+  const float keep = in ? 1.f : 0.f;
+  sc *= keep;
+  sh *= keep;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     f4 v = p.v[k];
-    if (MODE == 1) {
+    if (XF) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(sc, v[i] - mu, sh));
+    } else {
+      v *= keep;
     }
     if (m.ok[k]) *reinterpret_cast<f4*>(lplane + m.loff[k]) = v;
   }
 }
 
+// keeps a value materialised at this point of the step (see the bwd kernel)
+template <typename T>
+L3U_DEV void pin(T& v) { asm volatile("" : "+v"(v)); }
+
 template <int MODE, int TZC>
 __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w,
     const float* __restrict__ rec, l3u_norm_src src, int has_src, float* __restrict__ y,
-    long long yns, int C, int D, int H, int W, int RB, int ny, int TZ, int nz) {
+    long long yns, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int WQ = W >> 2, RS = W + 8, PP = (RB + 2) * RS, HW = H * W;
-  const QBlock b = q_decode(C, D, H, RB, ny, TZ, nz, WQ);
+  const int WQ = W >> 2, PP = (RB + 2) * W, HW = H * W;
+  const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
   const float* xp = x + (long long)b.n * xns + (long long)b.c * D * HW;
   float* yp = y + (long long)b.n * yns + (long long)b.c * D * HW;
   float wk[27];
@@ -438,42 +487,41 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
   __syncthreads();
   f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0;
   const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
-  // two planes staged in registers ahead of the one being consumed (2-deep load pipeline)
-  const QMap qm = q_map(b.y0, b.rows, H, W, WQ, RS);
+  const QMap qm = q_map(b.y0, b.rows, H, W, WQ);
   auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };   // loads always issue
+  const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
   // step t consumes input plane zi = z0-1+t; the step count is a compile-time constant and the
-  // loop is fully unrolled, so the staged registers never move (no back-edge copies that would
-  // force a vmcnt(0) drain of the pipeline)
+  // loop is fully unrolled, so the two staged registers never move (no back-edge copies that
+  // would force a vmcnt(0) drain of the pipeline)
   QPre p0, p1;
   q_fetch(p0, xp + zc(b.z0 - 1), qm);
   q_fetch(p1, xp + zc(b.z0), qm);
   auto step = [&](int t, QPre& pre) {
     const int zi = b.z0 - 1 + t;
-    const bool in = zi >= zlo && zi <= zhi;
     float* buf = lds + (t & 1) * PP;
-    if (in) q_commit<MODE>(pre, buf, qm, sc, mu, sh);
+    q_commit<MODE == 1>(pre, buf, qm, zi >= zlo && zi <= zhi, sc, mu, sh);
     q_fetch(pre, xp + zc(zi + 2), qm);
     __syncthreads();
-    if (b.own && in) {
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        float v[6];
-        q_row(buf, b.oy + r, RS, b.ox, v);
+    for (int r = 0; r < 3; ++r) {
+      float v[6];
+      q_nbr(buf, b.oy + r, W, b.ox, b.el, b.er, v);
 #pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-          const float w0 = wk[r * 3 + dx], w1 = wk[9 + r * 3 + dx], w2 = wk[18 + r * 3 + dx];
+      for (int dx = 0; dx < 3; ++dx) {
+        const float w0 = wk[r * 3 + dx], w1 = wk[9 + r * 3 + dx], w2 = wk[18 + r * 3 + dx];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            a2[i] = fmaf(w0, v[i + dx], a2[i]);   // input plane zi -> output zi+1 (kd=0)
-            a1[i] = fmaf(w1, v[i + dx], a1[i]);   //                -> output zi   (kd=1)
-            a0[i] = fmaf(w2, v[i + dx], a0[i]);   //                -> output zi-1 (kd=2)
-          }
+        for (int i = 0; i < 4; ++i) {
+          a2[i] = fmaf(w0, v[i + dx], a2[i]);   // input plane zi -> output zi+1 (kd=0)
+          a1[i] = fmaf(w1, v[i + dx], a1[i]);   //                -> output zi   (kd=1)
+          a0[i] = fmaf(w2, v[i + dx], a0[i]);   //                -> output zi-1 (kd=2)
         }
       }
     }
+    pin(a1);
+    pin(a2);
     const int zo = zi - 1;   // output plane zo has all three input planes now
     if (b.own && zo >= b.z0 && zo < b.z1)
-      *reinterpret_cast<f4*>(yp + (long long)zo * HW + (long long)(b.y0 + b.oy) * W + b.ox) = a0;
+      *reinterpret_cast<f4*>(yp + (long long)zo * HW + qofs) = a0;
     a0 = a1;
     a1 = a2;
     a2 = f4{0.f, 0.f, 0.f, 0.f};
@@ -485,15 +533,17 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
   }
 }
 
-template <int MODE, int TZC>
-__global__ __launch_bounds__(256) void dw3q_bwd_kernel(
+// MODE 0: dx = conv^T(dz);  MODE 1: fused IN/LeakyReLU/Dropout backward (dx = dpre, IN sums);
+// MODE 2: dx += conv^T(dz).  PD: register prefetch depth in planes (1 or 2).
+template <int MODE, int TZC, int PD = L3U_DWB_PD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 2 : L3U_DWB_WAVES))) void dw3q_bwd_kernel(
     const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
-    long long dxns, int accumulate, float* __restrict__ dw_part, double* __restrict__ in_part,
-    int N, int C, int D, int H, int W, int RB, int ny, int TZ, int nz) {
+    long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part,
+    int N, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int WQ = W >> 2, RS = W + 8, PP = (RB + 2) * RS, HW = H * W;
-  const QBlock b = q_decode(C, D, H, RB, ny, TZ, nz, WQ);
+  const int WQ = W >> 2, PP = (RB + 2) * W, HW = H * W;
+  const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
   const long long cofs = (long long)b.c * D * HW;
   const float* dzp = dz + (long long)b.n * dzns + cofs;
   const float* xp = x + (long long)b.n * xns + cofs;
@@ -512,109 +562,112 @@ __global__ __launch_bounds__(256) void dw3q_bwd_kernel(
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
   f4 d0 = zero4, d1 = zero4, d2 = zero4;      // dA planes zd-1, zd, zd+1
   f4 g0 = zero4, g1 = zero4, g2 = zero4;      // own dZ of planes zd-2, zd-1, zd (owned only)
-  float gw[27];
+  f2 gw[27];   // dW taps as x-pair partial sums (.x + .y at the end)
 #pragma unroll
-  for (int t = 0; t < 27; ++t) gw[t] = 0.f;
+  for (int t = 0; t < 27; ++t) gw[t] = f2{0.f, 0.f};
   double s1 = 0.0, s2 = 0.0;
   const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
   const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
   constexpr int nsteps = TZC + 3;   // compile-time step count: the step loop fully unrolls
-  // staged dZ / A planes of the next two steps (2-deep register pipeline)
   QPre pz0, pa0, pz1, pa1;
-  const QMap qm = q_map(b.y0, b.rows, H, W, WQ, RS);
+  const QMap qm = q_map(b.y0, b.rows, H, W, WQ);
   auto in_rng = [&](int z) { return z >= zlo && z <= zhi; };
   auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };  // clamped plane offset
   {
     const int zd = b.z0 - 1, za = zd - 1;
     q_fetch(pz0, dzp + zc(zd), qm);
     q_fetch(pa0, xp + zc(za), qm);
-    q_fetch(pz1, dzp + zc(zd + 1), qm);
-    q_fetch(pa1, xp + zc(za + 1), qm);
+    if (PD == 2) {
+      q_fetch(pz1, dzp + zc(zd + 1), qm);
+      q_fetch(pa1, xp + zc(za + 1), qm);
+    }
   }
   __syncthreads();
   auto step = [&](int s, QPre& pz, QPre& pa) {
     const int zd = b.z0 - 1 + s, za = zd - 1;
     float* dbuf = dzb + (s & 1) * PP;
     float* abuf = ab + (s & 1) * PP;
-    const bool ldz = in_rng(zd);
-    const bool la = in_rng(za);
-    if (ldz) q_commit<0>(pz, dbuf, qm, 1.f, 0.f, 0.f);
-    if (la) q_commit<MODE>(pa, abuf, qm, sc, mean, sh);
-    // issue the loads of step s+2 and this step's epilogue load before the barrier; all loads
+    q_commit<false>(pz, dbuf, qm, in_rng(zd), 1.f, 0.f, 0.f);
+    q_commit<MODE == 1>(pa, abuf, qm, in_rng(za), sc, mean, sh);
+    // issue the loads of step s+PD and this step's epilogue load before the barrier; all loads
     // are unconditional (clamped addresses) so the waits stay counted, never vmcnt(0)
-    q_fetch(pz, dzp + zc(zd + 2), qm);
-    q_fetch(pa, xp + zc(za + 2), qm);
+    q_fetch(pz, dzp + zc(zd + PD), qm);
+    q_fetch(pa, xp + zc(za + PD), qm);
     const int zf = zd - 1;   // dA plane zf completes in this step
     const bool fin = b.own && zf >= b.z0 && zf < b.z1;
     f4 epi = zero4;
-    if (MODE == 1 || accumulate)
+    if (MODE != 0)
       epi = *reinterpret_cast<const f4*>((MODE == 1 ? xp : dxp) + (long long)min(max(zf, 0), D - 1) * HW + qofs);
     __syncthreads();
-    const bool zd_owned = zd >= b.z0 && zd < b.z1;
-    if (b.own) {
-      g0 = g1;
-      g1 = g2;
-      g2 = zero4;
-      if (ldz) {
+    const bool zd_owned = b.own && zd >= b.z0 && zd < b.z1;
+    g0 = g1;
+    g1 = g2;
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          float v[6];
-          q_row(dbuf, b.oy + r, RS, b.ox, v);
-          if (r == 1 && zd_owned) g2 = f4{v[1], v[2], v[3], v[4]};
+    for (int r = 0; r < 3; ++r) {
+      float v[6];
+      q_nbr(dbuf, b.oy + r, W, b.ox, b.el, b.er, v);
+      if (r == 1) g2 = zd_owned ? f4{v[1], v[2], v[3], v[4]} : zero4;
 #pragma unroll
-          for (int dxi = 0; dxi < 3; ++dxi) {
-            const int tf = (2 - r) * 3 + (2 - dxi);   // flipped in-plane tap
-            const float w0 = wk[tf], w1 = wk[9 + tf], w2 = wk[18 + tf];
+      for (int dxi = 0; dxi < 3; ++dxi) {
+        const int tf = (2 - r) * 3 + (2 - dxi);   // flipped in-plane tap
+        const float w0 = wk[tf], w1 = wk[9 + tf], w2 = wk[18 + tf];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              d0[i] = fmaf(w0, v[i + dxi], d0[i]);
-              d1[i] = fmaf(w1, v[i + dxi], d1[i]);
-              d2[i] = fmaf(w2, v[i + dxi], d2[i]);
-            }
-          }
-        }
-      }
-      if (la) {
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          float u[6];
-          q_row(abuf, b.oy + r, RS, b.ox, u);
-#pragma unroll
-          for (int dxi = 0; dxi < 3; ++dxi) {
-            float a = gw[r * 3 + dxi], bb = gw[9 + r * 3 + dxi], cc = gw[18 + r * 3 + dxi];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              a = fmaf(g2[i], u[i + dxi], a);     // dZ plane za+1 (kd=0)
-              bb = fmaf(g1[i], u[i + dxi], bb);   // dZ plane za   (kd=1)
-              cc = fmaf(g0[i], u[i + dxi], cc);   // dZ plane za-1 (kd=2)
-            }
-            gw[r * 3 + dxi] = a;
-            gw[9 + r * 3 + dxi] = bb;
-            gw[18 + r * 3 + dxi] = cc;
-          }
-        }
-      }
-      if (fin) {
-        float* dst = dxp + (long long)zf * HW + qofs;
-        if (MODE == 1) {
-          const f4 yv = epi;
-          f4 o;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float pre = fmaf(sc, yv[i] - mean, sh);
-            const float dp = d0[i] * kk * lrelu_d(pre);
-            o[i] = dp;
-            s1 += dp;
-            s2 += (double)dp * ((yv[i] - mean) * rstd);
-          }
-          *reinterpret_cast<f4*>(dst) = o;
-        } else {
-          f4 o = d0;
-          if (accumulate) o += epi;
-          *reinterpret_cast<f4*>(dst) = o;
+        for (int i = 0; i < 4; ++i) {
+          d0[i] = fmaf(w0, v[i + dxi], d0[i]);
+          d1[i] = fmaf(w1, v[i + dxi], d1[i]);
+          d2[i] = fmaf(w2, v[i + dxi], d2[i]);
         }
       }
     }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      float u[6];
+      q_nbr(abuf, b.oy + r, W, b.ox, b.el, b.er, u);
+#pragma unroll
+      for (int dxi = 0; dxi < 3; ++dxi) {
+#if L3U_GW_SCALAR
+        float a = gw[r * 3 + dxi].x, bb = gw[9 + r * 3 + dxi].x, cc = gw[18 + r * 3 + dxi].x;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          a = fmaf(g2[i], u[i + dxi], a);     // dZ plane za+1 (kd=0)
+          bb = fmaf(g1[i], u[i + dxi], bb);   // dZ plane za   (kd=1)
+          cc = fmaf(g0[i], u[i + dxi], cc);   // dZ plane za-1 (kd=2)
+        }
+        gw[r * 3 + dxi].x = a;
+        gw[9 + r * 3 + dxi].x = bb;
+        gw[18 + r * 3 + dxi].x = cc;
+        continue;
+#endif
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {   // x-pairs (2h, 2h+1): one v_pk_fma_f32 per tap and kd
+          const f2 uu = {u[2 * h + dxi], u[2 * h + 1 + dxi]};
+          gw[r * 3 + dxi] = pfma(f2{g2[2 * h], g2[2 * h + 1]}, uu, gw[r * 3 + dxi]);            // kd=0
+          gw[9 + r * 3 + dxi] = pfma(f2{g1[2 * h], g1[2 * h + 1]}, uu, gw[9 + r * 3 + dxi]);    // kd=1
+          gw[18 + r * 3 + dxi] = pfma(f2{g0[2 * h], g0[2 * h + 1]}, uu, gw[18 + r * 3 + dxi]);  // kd=2
+        }
+      }
+    }
+    // pin the accumulators at the end of the step: without a use here the compiler sinks the
+    // dW FMAs (whose only use is the final reduction) past later barriers, keeping every
+    // step's LDS operands live at once
+#pragma unroll
+    for (int t = 0; t < 27; ++t) pin(gw[t]);
+    pin(d1);
+    pin(d2);
+    f4 o = d0;
+    if (MODE == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pre = fmaf(sc, epi[i] - mean, sh);
+        const float dp = o[i] * kk * lrelu_d(pre);
+        o[i] = dp;
+        s1 += fin ? (double)dp : 0.0;
+        s2 += fin ? (double)dp * ((epi[i] - mean) * rstd) : 0.0;
+      }
+    } else if (MODE == 2) {
+      o += epi;
+    }
+    if (fin) *reinterpret_cast<f4*>(dxp + (long long)zf * HW + qofs) = o;
     d0 = d1;
     d1 = d2;
     d2 = zero4;
@@ -622,7 +675,10 @@ __global__ __launch_bounds__(256) void dw3q_bwd_kernel(
 #pragma unroll
   for (int s = 0; s < nsteps; s += 2) {
     step(s, pz0, pa0);
-    if (s + 1 < nsteps) step(s + 1, pz1, pa1);
+    if (s + 1 < nsteps) {
+      if (PD == 2) step(s + 1, pz1, pa1);
+      else step(s + 1, pz0, pa0);
+    }
   }
   // workgroup reduction (fixed order) of the 27 taps and the 2 fp64 IN sums
   __syncthreads();
@@ -631,7 +687,7 @@ __global__ __launch_bounds__(256) void dw3q_bwd_kernel(
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, nw = blockDim.x >> 6;
 #pragma unroll
   for (int t = 0; t < 27; ++t) {
-    const float r = wave_sum(gw[t]);
+    const float r = wave_sum(gw[t].x + gw[t].y);
     if (ln == 0) red[wv * 32 + t] = r;
   }
   if (MODE == 1) {
@@ -639,8 +695,8 @@ __global__ __launch_bounds__(256) void dw3q_bwd_kernel(
     if (ln == 0) { redd[wv * 2] = r1; redd[wv * 2 + 1] = r2; }
   }
   __syncthreads();
+  const int ck = b.ck;   // (zb, yb) chunk within (n, c)
   const int nchunk = nz * ny;
-  const int ck = xcd_remap(blockIdx.x, gridDim.x) % nchunk;   // (zb, yb) chunk within (n, c)
   if (threadIdx.x < 27) {
     float r = 0.f;
     for (int k = 0; k < nw; ++k) r += red[k * 32 + threadIdx.x];
@@ -688,10 +744,10 @@ int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float
   const bool xf = rec != nullptr || src != nullptr;
   if (use_quads(H, W) && x_nstride % 4 == 0 && y_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
-    const size_t lds = (2 * (size_t)(g.RB + 2) * g.RS + 8) * sizeof(float);
+    const size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
 #define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<M_, T_>), grid, block, lds, stream, x, \
-      x_nstride, w, rec, s, has, y, y_nstride, C, D, H, W, g.RB, g.ny, g.TZ, g.nz)
+      x_nstride, w, rec, s, has, y, y_nstride, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
     if (xf) { if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
     else { if (g.TZ == 8) DWQF(0, 8); else if (g.TZ == 4) DWQF(0, 4); else DWQF(0, 2); }
 #undef DWQF
@@ -713,16 +769,20 @@ int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long
                 hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && D > 0 && H > 0 && W > 0);
   L3U_REQUIRE(rec == nullptr || in_part != nullptr);
+  L3U_REQUIRE(rec == nullptr || accumulate == 0);
   if (use_quads(H, W) && x_nstride % 4 == 0 && dz_nstride % 4 == 0 && dx_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
-    size_t lds = 4 * (size_t)(g.RB + 2) * g.RS * sizeof(float);
+    size_t lds = 4 * (size_t)(g.RB + 2) * W * sizeof(float);
     if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
 #define DWQB(M_, T_) hipLaunchKernelGGL((dw3q_bwd_kernel<M_, T_>), grid, block, lds, stream, dz, \
-      dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part, in_part, N, C, D, H, W, \
-      g.RB, g.ny, g.TZ, g.nz)
-    if (rec) { if (g.TZ == 8) DWQB(1, 8); else if (g.TZ == 4) DWQB(1, 4); else DWQB(1, 2); }
-    else { if (g.TZ == 8) DWQB(0, 8); else if (g.TZ == 4) DWQB(0, 4); else DWQB(0, 2); }
+      dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
+      g.RPW, g.ny, g.TZ, g.nz)
+#define DWQB_T(M_) do { if (g.TZ == 8) DWQB(M_, 8); else if (g.TZ == 4) DWQB(M_, 4); else DWQB(M_, 2); } while (0)
+    if (rec) DWQB_T(1);
+    else if (accumulate) DWQB_T(2);
+    else DWQB_T(0);
+#undef DWQB_T
 #undef DWQB
     L3U_CHECK_LAUNCH();
   }

@@ -229,26 +229,28 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
       for (int q = 0; q < 4; ++q) acc[m][q] = mfma4(a[q], b, acc[m][q]);
     }
   }
+  // cross-wave combine through LDS, value-major ([wave][value][lane]: consecutive lanes hit
+  // consecutive banks, conflict-free), added in fixed wave order
   if (wave > 0) {
-    float* dst = lds + ((wave - 1) * 64 + l) * T;
+    float* dst = lds + (wave - 1) * T * 64 + l;
 #pragma unroll
     for (int m = 0; m < NC; ++m)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dst[(m * 4 + q) * 4 + r] = acc[m][q][r];
+        for (int r = 0; r < 4; ++r) dst[((m * 4 + q) * 4 + r) * 64] = acc[m][q][r];
   }
   __syncthreads();
   if (wave != 0) return;
 #pragma unroll
   for (int wv = 0; wv < 3; ++wv) {
-    const float* src = lds + (wv * 64 + l) * T;
+    const float* src = lds + wv * T * 64 + l;
 #pragma unroll
     for (int m = 0; m < NC; ++m)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[m][q][r] += src[(m * 4 + q) * 4 + r];
+        for (int r = 0; r < 4; ++r) acc[m][q][r] += src[((m * 4 + q) * 4 + r) * 64];
   }
   // epilogue (one wave): lane holds Y[co0+16m+lr][sb*64 + 16lk + 4r + q]
   float* yn = y + (long long)n * yns;
@@ -319,7 +321,7 @@ template <int NJ, int NK, bool VEC>
 __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
     const float* __restrict__ dy, long long dyns, const float* __restrict__ x, long long xns,
     float* __restrict__ part, int J, int K, int S, int SCH, int nsc) {
-  constexpr int TJ = 16 * NJ, TK = 16 * NK, T = NJ * NK * 4;
+  constexpr int TJ = 16 * NJ, TK = 16 * NK;
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [64][T]
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const int sc = blockIdx.x % nsc, n = blockIdx.x / nsc;
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 #pragma unroll
         for (int b = 0; b < NK; ++b) acc[a][b] = mfma4(av[a][q], bv[b][q], acc[a][b]);
   }
-  // fixed-order cross-wave reduction through LDS
+  // fixed-order cross-wave reduction through LDS (value-major [value][lane]: conflict-free)
   for (int wv = 0; wv < 4; ++wv) {
     if (wave == wv) {
 #pragma unroll
@@ -385,7 +387,7 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
         for (int b = 0; b < NK; ++b)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int idx = l * T + (a * NK + b) * 4 + r;
+            const int idx = ((a * NK + b) * 4 + r) * 64 + l;
             lds[idx] = wv == 0 ? acc[a][b][r] : lds[idx] + acc[a][b][r];
           }
     }
@@ -400,12 +402,22 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int jj = j0 + 16 * a + 4 * lk + r, kk = k0 + 16 * b + lr;
-          if (jj < J && kk < K) o[(long long)jj * K + kk] = lds[l * T + (a * NK + b) * 4 + r];
+          if (jj < J && kk < K) o[(long long)jj * K + kk] = lds[((a * NK + b) * 4 + r) * 64 + l];
         }
   }
 }
 
-int pw_sch(int S) { return S >= 4096 ? 1024 : (S >= 1024 ? 512 : 256); }
+#ifndef L3U_PW_SCH_MAX
+#define L3U_PW_SCH_MAX 512
+#endif
+#ifndef L3U_PW_NSW_MAX
+#define L3U_PW_NSW_MAX 1
+#endif
+int pw_sch(int S) { return S >= 4096 ? L3U_PW_SCH_MAX : (S >= 1024 ? 512 : 256); }
+
+// voxel sub-tiles per wave of pw_fwd_kernel: fewer for narrow outputs so that big volumes
+// still launch enough workgroups (>= 4 per CU at one sample)
+int pw_nsw(int NC) { const int n = 4 / NC; return n < L3U_PW_NSW_MAX ? n : L3U_PW_NSW_MAX; }
 
 bool pw_use_ks(int S) { return S < 32768; }
 
@@ -441,7 +453,7 @@ int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout
     L3U_CHECK_LAUNCH();
   }
   const int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
-  const int NC = CO_BLK / 16, NSW = 4 / NC, TSB = 256 * NSW;
+  const int NC = CO_BLK / 16, NSW = pw_nsw(NC), TSB = 256 * NSW;
   const int nsb = (S + TSB - 1) / TSB;
   const int WS = (CO_BLK % 32 == 16) ? CO_BLK : CO_BLK + 16;
   const int Kp = (K + 3) & ~3;
@@ -458,8 +470,8 @@ int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout
                             x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part,   \
                             K, Nout, S, nsb);                                                    \
   } while (0)
-  if (NC == 1) PWF(1, 4);
-  else if (NC == 2) PWF(2, 2);
+  if (NC == 1) { if (NSW == 4) PWF(1, 4); else if (NSW == 2) PWF(1, 2); else PWF(1, 1); }
+  else if (NC == 2) { if (NSW == 2) PWF(2, 2); else PWF(2, 1); }
   else PWF(4, 1);
 #undef PWF
   L3U_CHECK_LAUNCH();
@@ -468,7 +480,7 @@ int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout
 int l3u_pw_stat_nsb(int Nout, int S) {
   if (pw_use_ks(S)) return (S + 63) / 64;
   const int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
-  const int TSB = 256 * (4 / (CO_BLK / 16));
+  const int TSB = 256 * pw_nsw(CO_BLK / 16);
   return (S + TSB - 1) / TSB;
 }
 
