@@ -27,10 +27,27 @@ constexpr int kRec = 8;
 L3U_DEV float lrelu(float v) { return v > 0.f ? v : v * kSlope; }
 L3U_DEV float lrelu_d(float pre) { return pre > 0.f ? 1.f : kSlope; }   // torch: x > 0 ? 1 : slope
 
+// Wave-wide sums without LDS traffic: DPP butterflies inside each 16-lane row (quad_perm xor 1,
+// xor 2, half-mirror, mirror), then the gfx950 permlane16/32 swaps across rows.  Every lane ends
+// with the same value, summed in the same order (a+b == b+a), so the result is deterministic.
+template <int CTRL>
+L3U_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+L3U_DEV float swap_sum16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+L3U_DEV float swap_sum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 L3U_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror
+  v += dpp_f<0x140>(v);   // row_mirror
+  return swap_sum32(swap_sum16(v));
 }
 
 // Block-wide sum for 256-thread blocks; every thread gets the result.  `red` >= 4 floats of LDS.
@@ -43,10 +60,30 @@ L3U_DEV float block_sum256(float v, float* red) {
   return red[0] + red[1] + red[2] + red[3];
 }
 
+template <int CTRL>
+L3U_DEV double dpp_d(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffffu), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+L3U_DEV double swap_sum_d(double v, bool row16) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = (unsigned)(u & 0xffffffffu), hi = (unsigned)(u >> 32);
+  const auto rl = row16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                        : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto rh = row16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                        : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const double a = __longlong_as_double((long long)(((unsigned long long)rh[0] << 32) | rl[0]));
+  const double b = __longlong_as_double((long long)(((unsigned long long)rh[1] << 32) | rl[1]));
+  return a + b;
+}
 L3U_DEV double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  return swap_sum_d(swap_sum_d(v, true), false);
 }
 
 // Block-wide fp64 sum for 256-thread blocks (cross-block gradient sums of InstanceNorm backward

@@ -333,11 +333,20 @@ QGeom qgeom(int N, int C, int D, int H, int W) {
   g.RB = best * g.RPW;
   g.ny = (H + g.RB - 1) / g.RB;
   g.threads = 64 * best;
-  g.TZ = D >= 32 ? 8 : (D > 8 ? 4 : 8);   // TZ in {2, 4, 8}: compile-time in the kernels
-  while (g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < 1024) g.TZ >>= 1;
+#ifndef L3U_TZ16_MIN_D
+#define L3U_TZ16_MIN_D 48
+#endif
+  g.TZ = D >= L3U_TZ16_MIN_D ? 16 : (D >= 32 ? 8 : (D > 8 ? 4 : 8));   // compile-time in the kernels
+  while (g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < 1024) g.TZ >>= 1;   // {16, 8, 4, 2}
   g.nz = (D + g.TZ - 1) / g.TZ;
   return g;
 }
+
+#ifndef L3U_DW_SPLIT_MIN_PLANE
+#define L3U_DW_SPLIT_MIN_PLANE 0
+#endif
+// backward as two passes (data gradient, weight gradient) for planes of at least this size
+bool dw_split(int H, int W) { return H * W >= L3U_DW_SPLIT_MIN_PLANE; }
 
 bool use_quads(int H, int W) {
   if (W % 4 != 0 || W < 4 || W > 256 || H < 1) return false;
@@ -458,34 +467,47 @@ L3U_DEV void q_commit(const QPre& p, float* lplane, const QMap& m, bool in, floa
 template <typename T>
 L3U_DEV void pin(T& v) { asm volatile("" : "+v"(v)); }
 
-template <int MODE, int TZC>
+// One pass of the 27-tap stencil over a (n, c, slab, strip) tile, input plane by input plane.
+//   XF  = 1: the input is transformed on load, a = lrelu(scale*(x-mean)+shift) (IN1 + LeakyReLU
+//            + Dropout3d before conv2.depthwise); the record is finalized in-kernel when has_src
+//   EPI = 0: forward, y = conv(x)
+//   EPI = 1: backward data of the IN-fused conv2: the stencil runs with the FLIPPED taps over dZ
+//            (conv^T), and the epilogue emits dpre = dA * k * lrelu'(pre), pre = scale*(ep-mean)
+//            + shift (ep = the saved pre-IN activation), plus the fp64 IN-backward sums
+//            in_part[c][n][chunk] = {sum dpre, sum dpre*xhat}
+//   EPI = 2: backward data, y += conv^T(x)      EPI = 3: backward data, y = conv^T(x)
+template <int XF, int EPI, int TZC>
 __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w,
     const float* __restrict__ rec, l3u_norm_src src, int has_src, float* __restrict__ y,
-    long long yns, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
+    long long yns, const float* __restrict__ ep, long long epns, double* __restrict__ in_part,
+    int N, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
+  constexpr bool FLIP = EPI != 0;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int WQ = W >> 2, PP = (RB + 2) * W, HW = H * W;
   const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
-  const float* xp = x + (long long)b.n * xns + (long long)b.c * D * HW;
-  float* yp = y + (long long)b.n * yns + (long long)b.c * D * HW;
+  const long long cofs = (long long)b.c * D * HW;
+  const float* xp = x + (long long)b.n * xns + cofs;
+  float* yp = y + (long long)b.n * yns + cofs;
+  const float* epp = (EPI == 1 || EPI == 2) ? ep + (long long)b.n * epns + cofs : nullptr;
   float wk[27];
 #pragma unroll
-  for (int t = 0; t < 27; ++t) wk[t] = w[b.c * 27 + t];
-  float sc = 1.f, sh = 0.f, mu = 0.f;
-  if (MODE == 1) {
+  for (int t = 0; t < 27; ++t) wk[t] = w[b.c * 27 + (FLIP ? 26 - t : t)];
+  float sc = 1.f, sh = 0.f, mu = 0.f, rstd = 1.f, kk = 1.f;
+  if (XF || EPI == 1) {
     if (has_src) {
       float* s8 = lds + 2 * PP;
       block_record(src, b.n, b.c, C, b.ck == 0, s8);
-      mu = s8[0]; sc = s8[2]; sh = s8[3];
+      mu = s8[0]; rstd = s8[1]; sc = s8[2]; sh = s8[3]; kk = s8[4];
     } else {
-      mu = rec[(long long)b.nc * kRec + 0];
-      sc = rec[(long long)b.nc * kRec + 2];
-      sh = rec[(long long)b.nc * kRec + 3];
+      const float* r = rec + (long long)b.nc * kRec;
+      mu = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];
     }
   }
   for (int i = threadIdx.x; i < 2 * PP; i += blockDim.x) lds[i] = 0.f;
   __syncthreads();
   f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0;
+  float s1 = 0.f, s2 = 0.f;   // per-thread sums over <= 4*TZ voxels; widened to fp64 per block
   const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
   const QMap qm = q_map(b.y0, b.rows, H, W, WQ);
   auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };   // loads always issue
@@ -499,8 +521,11 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
   auto step = [&](int t, QPre& pre) {
     const int zi = b.z0 - 1 + t;
     float* buf = lds + (t & 1) * PP;
-    q_commit<MODE == 1>(pre, buf, qm, zi >= zlo && zi <= zhi, sc, mu, sh);
+    q_commit<XF == 1>(pre, buf, qm, zi >= zlo && zi <= zhi, sc, mu, sh);
     q_fetch(pre, xp + zc(zi + 2), qm);
+    const int zo = zi - 1;   // output plane zo has all three input planes after this step
+    f4 e = {0.f, 0.f, 0.f, 0.f};
+    if (EPI == 1 || EPI == 2) e = *reinterpret_cast<const f4*>(epp + (long long)min(max(zo, 0), D - 1) * HW + qofs);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -519,9 +544,21 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
     }
     pin(a1);
     pin(a2);
-    const int zo = zi - 1;   // output plane zo has all three input planes now
-    if (b.own && zo >= b.z0 && zo < b.z1)
-      *reinterpret_cast<f4*>(yp + (long long)zo * HW + qofs) = a0;
+    const bool fin = b.own && zo >= b.z0 && zo < b.z1;
+    f4 o = a0;
+    if (EPI == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pre = fmaf(sc, e[i] - mu, sh);
+        const float dp = o[i] * kk * lrelu_d(pre);
+        o[i] = dp;
+        s1 += fin ? dp : 0.f;
+        s2 += fin ? dp * ((e[i] - mu) * rstd) : 0.f;
+      }
+    } else if (EPI == 2) {
+      o += e;
+    }
+    if (fin) *reinterpret_cast<f4*>(yp + (long long)zo * HW + qofs) = o;
     a0 = a1;
     a1 = a2;
     a2 = f4{0.f, 0.f, 0.f, 0.f};
@@ -530,6 +567,109 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
   for (int t = 0; t < TZC + 2; t += 2) {
     step(t, p0);
     step(t + 1, p1);
+  }
+  if (EPI == 1) {   // fixed-order block reduction of the IN-backward sums
+    __syncthreads();
+    double* redd = reinterpret_cast<double*>(lds);
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const double r1 = wave_sum_d((double)s1), r2 = wave_sum_d((double)s2);
+    if (ln == 0) { redd[wv * 2] = r1; redd[wv * 2 + 1] = r2; }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      double r = 0.0;
+      for (int k = 0; k < nw; ++k) r += redd[k * 2 + threadIdx.x];
+      in_part[(((long long)b.c * N + b.n) * (nz * ny) + b.ck) * 2 + threadIdx.x] = r;
+    }
+  }
+}
+
+// Depthwise weight gradient alone: dw_part[c][n*nchunk + chunk][27] = sum over the tile's voxels
+// of dZ(v) * A(v + tap), A = x (XF = 0) or lrelu(scale*(x-mean)+shift) (XF = 1).  The A planes go
+// through LDS (x-neighbours by DPP); each thread's own dZ quad comes straight from global memory,
+// three planes kept in registers.  Split from the data gradient (which is the forward kernel with
+// flipped taps) so that each pass keeps few registers and a short VALU chain per byte.
+template <int XF, int TZC>
+__global__ __launch_bounds__(256) void dw3q_dw_kernel(
+    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
+    const float* __restrict__ rec, float* __restrict__ dw_part, int N, int C, int D, int H, int W,
+    int RB, int RPW, int ny, int TZ, int nz) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int WQ = W >> 2, PP = (RB + 2) * W, HW = H * W;
+  const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
+  const long long cofs = (long long)b.c * D * HW;
+  const float* dzp = dz + (long long)b.n * dzns + cofs;
+  const float* xp = x + (long long)b.n * xns + cofs;
+  float sc = 1.f, sh = 0.f, mu = 0.f;
+  if (XF) {
+    const float* r = rec + (long long)b.nc * kRec;
+    mu = r[0]; sc = r[2]; sh = r[3];
+  }
+  for (int i = threadIdx.x; i < 2 * PP; i += blockDim.x) lds[i] = 0.f;
+  __syncthreads();
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  f4 g0 = zero4, g1 = zero4, g2 = zero4;   // own dZ of planes za-1, za, za+1
+  f2 gw[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t) gw[t] = f2{0.f, 0.f};
+  const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
+  const QMap qm = q_map(b.y0, b.rows, H, W, WQ);
+  auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };
+  const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
+  auto dzq = [&](int z) {   // own dZ quad of plane z (clamped address, always issued)
+    return *reinterpret_cast<const f4*>(dzp + (long long)min(max(z, 0), D - 1) * HW + qofs);
+  };
+  QPre p0, p1;
+  q_fetch(p0, xp + zc(b.z0 - 1), qm);
+  q_fetch(p1, xp + zc(b.z0), qm);
+  f4 q0 = dzq(b.z0), q1 = dzq(b.z0 + 1);
+  auto step = [&](int t, QPre& pre, f4& q) {
+    const int za = b.z0 - 1 + t;   // A plane of this step
+    float* buf = lds + (t & 1) * PP;
+    q_commit<XF == 1>(pre, buf, qm, za >= zlo && za <= zhi, sc, mu, sh);
+    q_fetch(pre, xp + zc(za + 2), qm);
+    g0 = g1;
+    g1 = g2;
+    const int zd = za + 1;
+    g2 = (b.own && zd >= b.z0 && zd < b.z1) ? q : zero4;
+    q = dzq(zd + 2);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      float u[6];
+      q_nbr(buf, b.oy + r, W, b.ox, b.el, b.er, u);
+#pragma unroll
+      for (int dxi = 0; dxi < 3; ++dxi) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {   // x-pairs (2h, 2h+1): one v_pk_fma_f32 per tap and kd
+          const f2 uu = {u[2 * h + dxi], u[2 * h + 1 + dxi]};
+          gw[r * 3 + dxi] = pfma(f2{g2[2 * h], g2[2 * h + 1]}, uu, gw[r * 3 + dxi]);            // kd=0
+          gw[9 + r * 3 + dxi] = pfma(f2{g1[2 * h], g1[2 * h + 1]}, uu, gw[9 + r * 3 + dxi]);    // kd=1
+          gw[18 + r * 3 + dxi] = pfma(f2{g0[2 * h], g0[2 * h + 1]}, uu, gw[18 + r * 3 + dxi]);  // kd=2
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 27; ++k) pin(gw[k]);
+  };
+#pragma unroll
+  for (int t = 0; t < TZC + 2; t += 2) {
+    step(t, p0, q0);
+    step(t + 1, p1, q1);
+  }
+  __syncthreads();
+  float* red = lds;   // [nwaves][32]
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int t = 0; t < 27; ++t) {
+    const float r = wave_sum(gw[t].x + gw[t].y);
+    if (ln == 0) red[wv * 32 + t] = r;
+  }
+  __syncthreads();
+  const int nchunk = nz * ny;
+  if (threadIdx.x < 27) {
+    float r = 0.f;
+    for (int k = 0; k < nw; ++k) r += red[k * 32 + threadIdx.x];
+    dw_part[((long long)b.c * N * nchunk + (long long)b.n * nchunk + b.ck) * 27 + threadIdx.x] = r;
   }
 }
 
@@ -744,12 +884,14 @@ int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float
   const bool xf = rec != nullptr || src != nullptr;
   if (use_quads(H, W) && x_nstride % 4 == 0 && y_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
-    const size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
+    size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
+    if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);   // reduction scratch
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
-#define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<M_, T_>), grid, block, lds, stream, x, \
-      x_nstride, w, rec, s, has, y, y_nstride, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
-    if (xf) { if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
-    else { if (g.TZ == 8) DWQF(0, 8); else if (g.TZ == 4) DWQF(0, 4); else DWQF(0, 2); }
+#define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<M_, 0, T_>), grid, block, lds, stream, x, \
+      x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W, g.RB, g.RPW, \
+      g.ny, g.TZ, g.nz)
+    if (xf) { if (g.TZ == 16) DWQF(1, 16); else if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
+    else { if (g.TZ == 16) DWQF(0, 16); else if (g.TZ == 8) DWQF(0, 8); else if (g.TZ == 4) DWQF(0, 4); else DWQF(0, 2); }
 #undef DWQF
     L3U_CHECK_LAUNCH();
   }
@@ -772,13 +914,40 @@ int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long
   L3U_REQUIRE(rec == nullptr || accumulate == 0);
   if (use_quads(H, W) && x_nstride % 4 == 0 && dz_nstride % 4 == 0 && dx_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
+    dim3 grid(N * C * g.nz * g.ny), block(g.threads);
+    if (dw_split(H, W)) {
+      // data gradient = the forward stencil with flipped taps (+ epilogue), then the weight
+      // gradient on its own; both use the same tile geometry, so the chunking of dw_part /
+      // in_part is identical to the fused kernel's
+      const l3u_norm_src z{};
+      size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
+      if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);
+#define DWQX(E_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<0, E_, T_>), grid, block, lds, stream, dz, \
+      dz_nstride, w, rec, z, 0, dx, dx_nstride, (E_ == 1 ? x : dx), (E_ == 1 ? x_nstride : dx_nstride), \
+      in_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
+#define DWQX_T(E_) do { if (g.TZ == 16) DWQX(E_, 16); else if (g.TZ == 8) DWQX(E_, 8); else if (g.TZ == 4) DWQX(E_, 4); else DWQX(E_, 2); } while (0)
+      if (rec) DWQX_T(1);
+      else if (accumulate) DWQX_T(2);
+      else DWQX_T(3);
+#undef DWQX_T
+#undef DWQX
+      size_t lds2 = 2 * (size_t)(g.RB + 2) * W * sizeof(float);
+      if (lds2 < 128 * sizeof(float)) lds2 = 128 * sizeof(float);
+#define DWQW(X_, T_) hipLaunchKernelGGL((dw3q_dw_kernel<X_, T_>), grid, block, lds2, stream, dz, \
+      dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
+#define DWQW_T(X_) do { if (g.TZ == 16) DWQW(X_, 16); else if (g.TZ == 8) DWQW(X_, 8); else if (g.TZ == 4) DWQW(X_, 4); else DWQW(X_, 2); } while (0)
+      if (rec) DWQW_T(1);
+      else DWQW_T(0);
+#undef DWQW_T
+#undef DWQW
+      L3U_CHECK_LAUNCH();
+    }
     size_t lds = 4 * (size_t)(g.RB + 2) * W * sizeof(float);
     if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch
-    dim3 grid(N * C * g.nz * g.ny), block(g.threads);
 #define DWQB(M_, T_) hipLaunchKernelGGL((dw3q_bwd_kernel<M_, T_>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
       g.RPW, g.ny, g.TZ, g.nz)
-#define DWQB_T(M_) do { if (g.TZ == 8) DWQB(M_, 8); else if (g.TZ == 4) DWQB(M_, 4); else DWQB(M_, 2); } while (0)
+#define DWQB_T(M_) do { if (g.TZ == 16) DWQB(M_, 16); else if (g.TZ == 8) DWQB(M_, 8); else if (g.TZ == 4) DWQB(M_, 4); else DWQB(M_, 2); } while (0)
     if (rec) DWQB_T(1);
     else if (accumulate) DWQB_T(2);
     else DWQB_T(0);

@@ -468,20 +468,21 @@ class UNetEngine:
         self._call("l3u_pw_bwd_weight", dy1.data_ptr(), cout * S, z1.data_ptr(), cin * S, A.ptr(pp1),
                    N, cout, cin, S, st)
         self._seg(pp1, npw, cout * cin, 1, cout * cin, pre + "conv1.pointwise.weight")
-        # (5) shortcut conv backward writes d(input) first
-        if shortcut:
-            self._call("l3u_pw_fwd", drv.p, drv.ns, self._w(flat, pre + "shortcut.0.weight"), 1, None,
-                       dxv.p, dxv.ns, 0, None, N, cout, cin, S, st)
-            ppr = A.alloc(npw * cout * cin)
-            self._call("l3u_pw_bwd_weight", drv.p, drv.ns, x.p, x.ns, A.ptr(ppr), N, cout, cin, S, st)
-            self._seg(ppr, npw, cout * cin, 1, cout * cin, pre + "shortcut.0.weight")
-        # (6) conv1.depthwise backward accumulates into d(input)
+        # (5) conv1.depthwise backward: writes d(input) (Conv1x1 shortcut) or accumulates into the
+        # identity-shortcut gradient already there
         nch1 = nat.query("l3u_dw3_nchunk", N, cin, d, h, w)
         pd1 = A.alloc(cin * N * nch1 * 27)
         self._call("l3u_dw3_bwd", dz1.data_ptr(), cin * S, x.p, x.ns,
-                   self._w(flat, pre + "conv1.depthwise.weight"), None, dxv.p, dxv.ns, 1, A.ptr(pd1),
-                   None, N, cin, d, h, w, st)
+                   self._w(flat, pre + "conv1.depthwise.weight"), None, dxv.p, dxv.ns,
+                   0 if shortcut else 1, A.ptr(pd1), None, N, cin, d, h, w, st)
         self._seg_dw(pd1, N * nch1, cin, pre + "conv1.depthwise.weight")
+        # (6) shortcut conv backward accumulates into d(input)
+        if shortcut:
+            self._call("l3u_pw_fwd", drv.p, drv.ns, self._w(flat, pre + "shortcut.0.weight"), 1, None,
+                       dxv.p, dxv.ns, 1, None, N, cout, cin, S, st)
+            ppr = A.alloc(npw * cout * cin)
+            self._call("l3u_pw_bwd_weight", drv.p, drv.ns, x.p, x.ns, A.ptr(ppr), N, cout, cin, S, st)
+            self._seg(ppr, npw, cout * cin, 1, cout * cin, pre + "shortcut.0.weight")
         if self.debug is not None and not self._dry:
             self.debug[pre + "#"] = {"dy2": dy2, "dr": drv, "dz2": dz2, "dy1": dy1, "dz1": dz1,
                                      "dx": dxv}
