@@ -77,9 +77,9 @@ int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long
  * replaces nn.Conv3d(Ci, Co, 1, bias=False)  (DepthwiseSeparableConv3d.pointwise, unet3d.py:18;
  *          shortcut conv unet3d.py:70-73; out_conv unet3d.py:201) and the GEMM of
  *          nn.ConvTranspose3d(Ci, Ci//2, 2, 2) (unet3d.py:119).
- * stat_part != NULL: emits InstanceNorm partials [N][Nout][l3u_pw_stat_nsb][3] = (count, mean, M2)
+ * stat_part != NULL: emits InstanceNorm partials [N][Nout][l3u_pw_stat_nsb(K, Nout, S)][3] = (count, mean, M2)
  * of the output for the nn.InstanceNorm3d that follows (unet3d.py:51,62,72).                  */
-int l3u_pw_stat_nsb(int Nout, int S);
+int l3u_pw_stat_nsb(int K, int Nout, int S);
 int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout,
                const float* bias, float* y, long long y_nstride, int accumulate,
                float* stat_part, int N, int K, int Nout, int S, hipStream_t stream);
@@ -138,6 +138,11 @@ int l3u_maxpool2_bwd(const float* dy, long long dy_nstride, const unsigned char*
  * s2d: the inverse permutation (backward)                                                     */
 int l3u_convt_d2s(const float* yp, const float* bias, float* out, long long out_nstride, int N,
                   int Co, int D, int H, int W, hipStream_t stream);
+/* the whole forward in one launch: the [Co*8 x Ci] GEMM on MFMA with the scatter (and bias) in
+ * its epilogue (x: [N][Ci][D*H*W], w: torch ConvTranspose3d weight [Ci][Co][2][2][2])        */
+int l3u_convt_fwd(const float* x, long long x_nstride, const float* w, const float* bias,
+                  float* out, long long out_nstride, int N, int Ci, int Co, int D, int H, int W,
+                  hipStream_t stream);
 int l3u_convt_s2d(const float* dy, long long dy_nstride, float* dyp, int N, int Co, int D, int H,
                   int W, hipStream_t stream);
 /* per-channel sums part[C][N][nblocks] (fp64; bias gradients)                                */
@@ -146,13 +151,18 @@ int l3u_chan_sum(const float* x, long long x_nstride, double* part, int N, int C
                  hipStream_t stream);
 
 /* ---- out_conv (1x1x1, C->1, bias) + Sigmoid (unet3d.py:201-202, forward :220-221) ----------
- * bwd: dz = dp*p*(1-p); dh[c] = w[c]*dz; part[N*nblocks][C+1] (fp64) = {sum dz*h[c].., sum dz}*/
+ * fwd: p = sigmoid(b + w.h); t != NULL also emits the FocalTversky first-stage partials
+ *      ftl_part[N*nblocks][3] = {sum p*t, sum p, sum t} (reduce them with l3u_ftl_reduce)
+ * bwd: dz = g*p*(1-p) with g = dp, or (dp == NULL) the FocalTversky gradient of the global sums
+ *      (closed form, * gscale[0] if given); dh[c] = w[c]*dz;
+ *      part[N*nblocks][C+1] (fp64) = {sum dz*h[c].., sum dz}                                  */
 int l3u_outconv_nblocks(int S);
 int l3u_outconv_fwd(const float* h, long long h_nstride, const float* w, const float* b, float* p,
-                    int N, int C, int S, hipStream_t stream);
-int l3u_outconv_bwd(const float* dp, const float* p, const float* h, long long h_nstride,
-                    const float* w, float* dh, long long dh_nstride, double* part, int N, int C,
-                    int S, hipStream_t stream);
+                    const float* t, float* ftl_part, int N, int C, int S, hipStream_t stream);
+int l3u_outconv_bwd(const float* dp, const float* p, const float* t, const double* sums,
+                    double alpha, double beta, double gamma, double smooth, const float* gscale,
+                    const float* h, long long h_nstride, const float* w, float* dh,
+                    long long dh_nstride, double* part, int N, int C, int S, hipStream_t stream);
 
 /* ---- FocalTverskyLoss (light_unet/models/losses.py:11-54) ----------------------------------
  * sums = {sum p*t, sum p, sum t} over ALL voxels of the batch (pred.view(-1), losses.py:40-46),
@@ -162,6 +172,8 @@ int l3u_outconv_bwd(const float* dp, const float* p, const float* h, long long h
 int l3u_ftl_nblocks(long long numel);
 int l3u_ftl_sums(const float* p, const float* t, long long numel, float* part, double* sums,
                  hipStream_t stream);
+/* second stage only (partials from l3u_outconv_fwd): sums[3] = fixed-order sum of part[nparts][3] */
+int l3u_ftl_reduce(const float* part, int nparts, double* sums, hipStream_t stream);
 int l3u_ftl_loss(const double* sums, double alpha, double beta, double gamma, double smooth,
                  float* loss, hipStream_t stream);
 int l3u_ftl_bwd(const float* p, const float* t, long long numel, const double* sums, double alpha,

@@ -116,42 +116,133 @@ __global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__
 }
 
 // ---------------------------------------------------------------- out_conv + sigmoid
+// p = sigmoid(b + sum_c w[c] h[c]); 4 voxels per thread (float4 when VEC).  t != NULL: also the
+// FocalTversky partials of this block, ftl_part[n*nb + blk] = {sum p*t, sum p, sum t} (the loss's
+// first reduction stage fused into the producer of p: losses.py:40-42).
+template <bool VEC>
 __global__ __launch_bounds__(256) void outconv_fwd_kernel(
     const float* __restrict__ h, long long hns, const float* __restrict__ w,
-    const float* __restrict__ b, float* __restrict__ p, int C, int S) {
+    const float* __restrict__ b, float* __restrict__ p, const float* __restrict__ t,
+    float* __restrict__ ftl_part, int C, int S) {
+  __shared__ float red[4];
   const int n = blockIdx.y;
   const float* hp = h + (long long)n * hns;
   float* pp = p + (long long)n * S;
   const float bv = b[0];
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256) {
-    float z = bv;
-    for (int c = 0; c < C; ++c) z = fmaf(w[c], hp[(long long)c * S + i], z);
-    pp[i] = 1.f / (1.f + expf(-z));
+  const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  f4 z = {bv, bv, bv, bv};
+  if (VEC) {
+    if (i0 < S) {
+      for (int c = 0; c < C; ++c) z += w[c] * *reinterpret_cast<const f4*>(hp + (long long)c * S + i0);
+    }
+  } else {
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (i0 + q < S) z[q] = fmaf(w[c], hp[(long long)c * S + i0 + q], z[q]);
+  }
+  f4 pv;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) pv[q] = 1.f / (1.f + expf(-z[q]));
+  if (VEC) {
+    if (i0 < S) *reinterpret_cast<f4*>(pp + i0) = pv;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (i0 + q < S) pp[i0 + q] = pv[q];
+  }
+  if (t == nullptr) return;
+  float spt = 0.f, sp = 0.f, st = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (i0 + q < S) {
+      const float tv = t[(long long)n * S + i0 + q];
+      spt = fmaf(pv[q], tv, spt);
+      sp += pv[q];
+      st += tv;
+    }
+  }
+  spt = block_sum256(spt, red);
+  sp = block_sum256(sp, red);
+  st = block_sum256(st, red);
+  if (threadIdx.x == 0) {
+    float* o = ftl_part + ((long long)n * gridDim.x + blockIdx.x) * 3;
+    o[0] = spt;
+    o[1] = sp;
+    o[2] = st;
   }
 }
 
-// dz = dp * p * (1 - p); dh[c] = w[c] * dz; part[blk][0..C-1] = sum dz*h[c], part[blk][C] = sum dz
+struct FtlCoef { double loss, A, B; };
+
+L3U_DEV FtlCoef ftl_coef(const double* sums, double alpha, double beta, double gamma, double smooth) {
+  const double tp = sums[0], fp = sums[1] - sums[0], fn = sums[2] - sums[0];
+  const double dn = tp + alpha * fn + beta * fp + smooth;
+  const double ti = (tp + smooth) / dn;
+  const double one_m = 1.0 - ti;
+  FtlCoef r;
+  r.loss = pow(one_m, gamma);
+  const double pre = -gamma * pow(one_m, gamma - 1.0) / (dn * dn);
+  r.A = pre * (dn - (tp + smooth) * (1.0 - alpha));   // t = 1
+  r.B = pre * (-(tp + smooth) * beta);                 // t = 0
+  return r;
+}
+
+// dz = dL/dp * p(1-p); dh[c] = w[c] * dz; part[n*nb + blk][0..C-1] = sum dz*h[c], [C] = sum dz.
+// dL/dp comes from dp, or (dp == NULL) from the FocalTversky closed form A t + B (1 - t) of the
+// global sums (losses.py:30-54), fused so the loss gradient is never written out.
+template <bool VEC>
 __global__ __launch_bounds__(256) void outconv_bwd_kernel(
-    const float* __restrict__ dp, const float* __restrict__ p, const float* __restrict__ h,
-    long long hns, const float* __restrict__ w, float* __restrict__ dh, long long dhns,
+    const float* __restrict__ dp, const float* __restrict__ p, const float* __restrict__ t,
+    const double* __restrict__ sums, double alpha, double beta, double gamma, double smooth,
+    const float* __restrict__ gscale, const float* __restrict__ h, long long hns,
+    const float* __restrict__ w, float* __restrict__ dh, long long dhns,
     double* __restrict__ part, int C, int S) {
   extern __shared__ double redd[];   // [4][C+1]
+  __shared__ float coef[2];
   const int n = blockIdx.y, nb = gridDim.x;
+  if (dp == nullptr) {
+    if (threadIdx.x == 0) {
+      const FtlCoef r = ftl_coef(sums, alpha, beta, gamma, smooth);
+      const double s = gscale ? (double)gscale[0] : 1.0;
+      coef[0] = (float)(r.A * s);
+      coef[1] = (float)(r.B * s);
+    }
+    __syncthreads();
+  }
   const float* hp = h + (long long)n * hns;
   float* dhp = dh + (long long)n * dhns;
+  const long long o = (long long)n * S;
+  const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  f4 dz = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (i0 + q < S) {
+      const float pv = p[o + i0 + q];
+      const float g = dp ? dp[o + i0 + q] : fmaf(coef[0] - coef[1], t[o + i0 + q], coef[1]);
+      dz[q] = g * pv * (1.f - pv);
+    }
+  }
   float acc[33];
 #pragma unroll
   for (int c = 0; c < 33; ++c) acc[c] = 0.f;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += nb * 256) {
-    const float pv = p[(long long)n * S + i];
-    const float dz = dp[(long long)n * S + i] * pv * (1.f - pv);
-    acc[32] += dz;
+  acc[32] = (dz[0] + dz[1]) + (dz[2] + dz[3]);
 #pragma unroll
-    for (int c = 0; c < 32; ++c) {
-      if (c < C) {
-        const float hv = hp[(long long)c * S + i];
-        acc[c] = fmaf(dz, hv, acc[c]);
-        dhp[(long long)c * S + i] = w[c] * dz;
+  for (int c = 0; c < 32; ++c) {
+    if (c < C) {
+      if (VEC) {
+        if (i0 < S) {
+          const f4 hv = *reinterpret_cast<const f4*>(hp + (long long)c * S + i0);
+          acc[c] = fmaf(dz[0], hv[0], fmaf(dz[1], hv[1], fmaf(dz[2], hv[2], dz[3] * hv[3])));
+          *reinterpret_cast<f4*>(dhp + (long long)c * S + i0) = w[c] * dz;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (i0 + q < S) {
+            acc[c] = fmaf(dz[q], hp[(long long)c * S + i0 + q], acc[c]);
+            dhp[(long long)c * S + i0 + q] = w[c] * dz[q];
+          }
       }
     }
   }
@@ -165,9 +256,9 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
   }
   __syncthreads();
   if (threadIdx.x <= C) {
-    const int t = threadIdx.x;
-    const double r = (redd[t] + redd[(C + 1) + t]) + (redd[2 * (C + 1) + t] + redd[3 * (C + 1) + t]);
-    part[((long long)n * nb + blockIdx.x) * (C + 1) + t] = r;
+    const int tt = threadIdx.x;
+    const double r = (redd[tt] + redd[(C + 1) + tt]) + (redd[2 * (C + 1) + tt] + redd[3 * (C + 1) + tt]);
+    part[((long long)n * nb + blockIdx.x) * (C + 1) + tt] = r;
   }
 }
 
@@ -208,21 +299,6 @@ __global__ void ftl_sums_kernel(const float* __restrict__ part, int nb, double* 
     for (int i = 0; i < 64; ++i) s += red[l][i];
     sums[l] = s;
   }
-}
-
-struct FtlCoef { double loss, A, B; };
-
-L3U_DEV FtlCoef ftl_coef(const double* sums, double alpha, double beta, double gamma, double smooth) {
-  const double tp = sums[0], fp = sums[1] - sums[0], fn = sums[2] - sums[0];
-  const double dn = tp + alpha * fn + beta * fp + smooth;
-  const double ti = (tp + smooth) / dn;
-  const double one_m = 1.0 - ti;
-  FtlCoef r;
-  r.loss = pow(one_m, gamma);
-  const double pre = -gamma * pow(one_m, gamma - 1.0) / (dn * dn);
-  r.A = pre * (dn - (tp + smooth) * (1.0 - alpha));   // t = 1
-  r.B = pre * (-(tp + smooth) * beta);                 // t = 0
-  return r;
 }
 
 __global__ void ftl_loss_kernel(const double* __restrict__ sums, double alpha, double beta,
@@ -380,23 +456,36 @@ int l3u_chan_sum(const float* x, long long x_nstride, double* part, int N, int C
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_outconv_nblocks(int S) { return grid_for(S, 1024, 128); }
+int l3u_outconv_nblocks(int S) { return (S + 1023) / 1024; }
 
 int l3u_outconv_fwd(const float* h, long long h_nstride, const float* w, const float* b, float* p,
-                    int N, int C, int S, hipStream_t stream) {
-  L3U_REQUIRE(N > 0 && C > 0 && C <= 32 && S > 0);
-  hipLaunchKernelGGL(outconv_fwd_kernel, dim3(grid_for(S, 1024, 128), N), dim3(256), 0, stream,
-                     h, h_nstride, w, b, p, C, S);
+                    const float* t, float* ftl_part, int N, int C, int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && S > 0);
+  L3U_REQUIRE(t == nullptr || ftl_part != nullptr);
+  const bool vec = S % 4 == 0 && h_nstride % 4 == 0;
+  dim3 grid((S + 1023) / 1024, N);
+  if (vec) hipLaunchKernelGGL(outconv_fwd_kernel<true>, grid, dim3(256), 0, stream, h, h_nstride, w, b, p, t, ftl_part, C, S);
+  else hipLaunchKernelGGL(outconv_fwd_kernel<false>, grid, dim3(256), 0, stream, h, h_nstride, w, b, p, t, ftl_part, C, S);
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_outconv_bwd(const float* dp, const float* p, const float* h, long long h_nstride,
-                    const float* w, float* dh, long long dh_nstride, double* part, int N, int C,
-                    int S, hipStream_t stream) {
+int l3u_outconv_bwd(const float* dp, const float* p, const float* t, const double* sums, double alpha,
+                    double beta, double gamma, double smooth, const float* gscale, const float* h,
+                    long long h_nstride, const float* w, float* dh, long long dh_nstride,
+                    double* part, int N, int C, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && C <= 32 && S > 0);
-  hipLaunchKernelGGL(outconv_bwd_kernel, dim3(grid_for(S, 1024, 128), N), dim3(256),
-                     4 * (C + 1) * sizeof(double), stream, dp, p, h, h_nstride, w, dh, dh_nstride,
-                     part, C, S);
+  L3U_REQUIRE(dp != nullptr || (t != nullptr && sums != nullptr));
+  const bool vec = S % 4 == 0 && h_nstride % 4 == 0 && dh_nstride % 4 == 0;
+  dim3 grid((S + 1023) / 1024, N);
+  const size_t lds = 4 * (C + 1) * sizeof(double);
+  if (vec) hipLaunchKernelGGL(outconv_bwd_kernel<true>, grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, C, S);
+  else hipLaunchKernelGGL(outconv_bwd_kernel<false>, grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, C, S);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_ftl_reduce(const float* part, int nparts, double* sums, hipStream_t stream) {
+  L3U_REQUIRE(nparts > 0);
+  hipLaunchKernelGGL(ftl_sums_kernel, dim3(1), dim3(64), 0, stream, part, nparts, sums);
   L3U_CHECK_LAUNCH();
 }
 

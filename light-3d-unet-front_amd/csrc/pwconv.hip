@@ -22,11 +22,47 @@ namespace {
 
 L3U_DEV f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
-template <int NC, int NSW, bool VEC>
+// ConvTranspose3d(k=2, s=2) epilogue: GEMM row j = co*8 + (4a + 2b + c) of input voxel s lands at
+// out[co][2z+a][2y+b][2x+c] (+ bias[co]).  The lane's accumulator quad holds 4 consecutive input
+// voxels of one row j; its c-partner row j^1 sits in lane l^1 (same co, a, b, voxels), so one DPP
+// swap of two values gives each lane 4 CONTIGUOUS outputs [2x0 .. 2x0+3] (c = 0) or
+// [2x0+4 .. 2x0+7] (c = 1): one float4 store instead of 4 stride-2 scalar stores.  Requires W % 4
+// == 0 (VEC); otherwise per-voxel scalar stores.  Every lane of the wave must call it.
+template <bool VEC>
+L3U_DEV void d2s_store(float* outn, int j, int Nout, const float* __restrict__ bias, int s, f4 v,
+                       int S, int D, int H, int W) {
+  const bool ok = j < Nout;
+  const int co = j >> 3, a = (j >> 2) & 1, bq = (j >> 1) & 1, c = j & 1;
+  const float bv = (bias && ok) ? bias[co] : 0.f;
+  v += bv;
+  const long long So = 8ll * S;
+  float* oc = outn + (long long)co * So;
+  if (VEC) {
+    const float s0 = c ? v[0] : v[2], s1 = c ? v[1] : v[3];
+    const float r0 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s0), 0xB1, 0xf, 0xf, false));
+    const float r1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s1), 0xB1, 0xf, 0xf, false));
+    const f4 o = c ? f4{r0, v[2], r1, v[3]} : f4{v[0], r0, v[1], r1};
+    if (ok && s < S) {
+      const int x = s % W, t = s / W, y = t % H, z = t / H;
+      float* dst = oc + ((long long)(2 * z + a) * (2 * H) + (2 * y + bq)) * (2 * W) + 2 * x + (c ? 4 : 0);
+      *reinterpret_cast<f4*>(dst) = o;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (ok && s + q < S) {
+        const int x = (s + q) % W, t = (s + q) / W, y = t % H, z = t / H;
+        oc[((long long)(2 * z + a) * (2 * H) + (2 * y + bq)) * (2 * W) + 2 * x + c] = v[q];
+      }
+    }
+  }
+}
+
+template <int NC, int NSW, bool VEC, bool D2S>
 __global__ __launch_bounds__(256) void pw_fwd_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
     const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
-    float* __restrict__ stat_part, int K, int Nout, int S, int nsb) {
+    float* __restrict__ stat_part, int K, int Nout, int S, int nsb, int Dq, int Hq, int Wq) {
   constexpr int CO_BLK = 16 * NC;
   constexpr int TSB = 256 * NSW;
   constexpr int WS = (CO_BLK % 32 == 16) ? CO_BLK : CO_BLK + 16;
@@ -91,6 +127,18 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
 
   // epilogue: bias, accumulate, store, InstanceNorm partials
   float* yn = y + (long long)n * yns;
+  if (D2S) {
+#pragma unroll
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+      for (int j = 0; j < NSW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          d2s_store<VEC>(yn, co0 + 16 * m + lr, Nout, bias, sbase + j * 64 + 16 * lk + 4 * r,
+                         f4{acc[j][m][0][r], acc[j][m][1][r], acc[j][m][2][r], acc[j][m][3][r]},
+                         S, Dq, Hq, Wq);
+    return;
+  }
   float lsum[NC];
 #pragma unroll
   for (int m = 0; m < NC; ++m) lsum[m] = 0.f;
@@ -188,11 +236,11 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
 // share ONE 64-voxel tile and split the reduction dimension K (k-steps interleaved by wave), then
 // combine through LDS in a fixed order; weights are read straight from L2 (they are tiny and
 // every workgroup re-reads them).  This turns an 8-workgroup grid into hundreds.
-template <int NC, bool VEC>
+template <int NC, bool VEC, bool D2S>
 __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
     const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
-    float* __restrict__ stat_part, int K, int Nout, int S, int nsb) {
+    float* __restrict__ stat_part, int K, int Nout, int S, int nsb, int Dq, int Hq, int Wq) {
   constexpr int CO_BLK = 16 * NC;
   constexpr int T = NC * 16;   // accumulator floats per lane
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [3 waves][64 lanes][T]
@@ -254,6 +302,15 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
   }
   // epilogue (one wave): lane holds Y[co0+16m+lr][sb*64 + 16lk + 4r + q]
   float* yn = y + (long long)n * yns;
+  if (D2S) {
+#pragma unroll
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        d2s_store<VEC>(yn, co0 + 16 * m + lr, Nout, bias, sb * 64 + 16 * lk + 4 * r,
+                       f4{acc[m][0][r], acc[m][1][r], acc[m][2][r], acc[m][3][r]}, S, Dq, Hq, Wq);
+    return;
+  }
   const int cnt = min(64, S - sb * 64);
 #pragma unroll
   for (int m = 0; m < NC; ++m) {
@@ -419,36 +476,41 @@ int pw_sch(int S) { return S >= 4096 ? L3U_PW_SCH_MAX : (S >= 1024 ? 512 : 256);
 // still launch enough workgroups (>= 4 per CU at one sample)
 int pw_nsw(int NC) { const int n = 4 / NC; return n < L3U_PW_NSW_MAX ? n : L3U_PW_NSW_MAX; }
 
-bool pw_use_ks(int S) { return S < 32768; }
+#ifndef L3U_PW_KS_MIN_K
+#define L3U_PW_KS_MIN_K 0
+#endif
+// K split across the 4 waves (pw_fwd_ks_kernel) for small volumes with a deep enough reduction
+bool pw_use_ks(int S, int K) { return S < 32768 && K >= L3U_PW_KS_MIN_K; }
 
 }  // namespace
 
 extern "C" {
 
-int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout,
-               const float* bias, float* y, long long y_nstride, int accumulate,
-               float* stat_part, int N, int K, int Nout, int S, hipStream_t stream) {
+}  // extern "C"
+
+namespace {
+
+int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout, const float* bias,
+              float* y, long long y_nstride, int accumulate, float* stat_part, int N, int K,
+              int Nout, int S, bool d2s, int Dq, int Hq, int Wq, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && K > 0 && Nout > 0 && S > 0);
-  const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (y_nstride % 4 == 0);
-  if (pw_use_ks(S)) {
+  const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (y_nstride % 4 == 0) &&
+                   (!d2s || Wq % 4 == 0);
+  if (pw_use_ks(S, K)) {
     // co tile: as wide as possible while keeping >= 256 workgroups
     const int nsb = (S + 63) / 64;
     int NC = Nout <= 16 ? 1 : (Nout <= 32 ? 2 : 4);
     while (NC > 1 && (long long)nsb * ((Nout + 16 * NC - 1) / (16 * NC)) * N < 256) NC >>= 1;
     const size_t lds = 3 * 64 * (size_t)NC * 16 * sizeof(float);
     dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), N), block(256);
-#define PWK(NC_)                                                                                  \
-  do {                                                                                            \
-    if (vec) hipLaunchKernelGGL((pw_fwd_ks_kernel<NC_, true>), grid, block, lds, stream, x,      \
-                                x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, \
-                                K, Nout, S, nsb);                                                  \
-    else hipLaunchKernelGGL((pw_fwd_ks_kernel<NC_, false>), grid, block, lds, stream, x,         \
-                            x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K,  \
-                            Nout, S, nsb);                                                         \
-  } while (0)
-    if (NC == 1) PWK(1);
-    else if (NC == 2) PWK(2);
-    else PWK(4);
+#define PWK(NC_, V_, D_) hipLaunchKernelGGL((pw_fwd_ks_kernel<NC_, V_, D_>), grid, block, lds, stream, \
+      x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq)
+#define PWK_V(NC_) do { if (d2s) { if (vec) PWK(NC_, true, true); else PWK(NC_, false, true); } \
+                        else { if (vec) PWK(NC_, true, false); else PWK(NC_, false, false); } } while (0)
+    if (NC == 1) PWK_V(1);
+    else if (NC == 2) PWK_V(2);
+    else PWK_V(4);
+#undef PWK_V
 #undef PWK
     L3U_CHECK_LAUNCH();
   }
@@ -461,24 +523,40 @@ int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout
   if (lds < 4 * CO_BLK * sizeof(float)) lds = 4 * CO_BLK * sizeof(float);
   L3U_REQUIRE(lds <= 160 * 1024);
   dim3 grid(nsb, (Nout + CO_BLK - 1) / CO_BLK, N), block(256);
-#define PWF(NC_, NSW_)                                                                          \
-  do {                                                                                          \
-    if (vec) hipLaunchKernelGGL((pw_fwd_kernel<NC_, NSW_, true>), grid, block, lds, stream, x,  \
-                                x_nstride, w, w_layout, bias, y, y_nstride, accumulate,          \
-                                stat_part, K, Nout, S, nsb);                                     \
-    else hipLaunchKernelGGL((pw_fwd_kernel<NC_, NSW_, false>), grid, block, lds, stream, x,     \
-                            x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part,   \
-                            K, Nout, S, nsb);                                                    \
-  } while (0)
-  if (NC == 1) { if (NSW == 4) PWF(1, 4); else if (NSW == 2) PWF(1, 2); else PWF(1, 1); }
-  else if (NC == 2) { if (NSW == 2) PWF(2, 2); else PWF(2, 1); }
-  else PWF(4, 1);
+#define PWF(NC_, NSW_, V_, D_) hipLaunchKernelGGL((pw_fwd_kernel<NC_, NSW_, V_, D_>), grid, block, lds, \
+      stream, x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, \
+      Dq, Hq, Wq)
+#define PWF_V(NC_, NSW_) do { if (d2s) { if (vec) PWF(NC_, NSW_, true, true); else PWF(NC_, NSW_, false, true); } \
+                              else { if (vec) PWF(NC_, NSW_, true, false); else PWF(NC_, NSW_, false, false); } } while (0)
+  if (NC == 1) { if (NSW == 4) PWF_V(1, 4); else if (NSW == 2) PWF_V(1, 2); else PWF_V(1, 1); }
+  else if (NC == 2) { if (NSW == 2) PWF_V(2, 2); else PWF_V(2, 1); }
+  else PWF_V(4, 1);
+#undef PWF_V
 #undef PWF
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_pw_stat_nsb(int Nout, int S) {
-  if (pw_use_ks(S)) return (S + 63) / 64;
+}  // namespace
+
+extern "C" {
+
+int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout,
+               const float* bias, float* y, long long y_nstride, int accumulate,
+               float* stat_part, int N, int K, int Nout, int S, hipStream_t stream) {
+  return pw_launch(x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, N, K,
+                   Nout, S, false, 0, 0, 0, stream);
+}
+
+int l3u_convt_fwd(const float* x, long long x_nstride, const float* w, const float* bias,
+                  float* out, long long out_nstride, int N, int Ci, int Co, int D, int H, int W,
+                  hipStream_t stream) {
+  L3U_REQUIRE(D > 0 && H > 0 && W > 0);
+  return pw_launch(x, x_nstride, w, 1, bias, out, out_nstride, 0, nullptr, N, Ci, Co * 8,
+                   D * H * W, true, D, H, W, stream);
+}
+
+int l3u_pw_stat_nsb(int K, int Nout, int S) {
+  if (pw_use_ks(S, K)) return (S + 63) / 64;
   const int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
   const int TSB = 256 * pw_nsw(CO_BLK / 16);
   return (S + TSB - 1) / TSB;

@@ -25,7 +25,7 @@ _SIGS = {
     "l3u_dw3_nchunk": [I, I, I, I, I],
     "l3u_dw3_fwd": [P, L, P, P, P, P, L, I, I, I, I, I, P],
     "l3u_dw3_bwd": [P, L, P, L, P, P, P, L, I, P, P, I, I, I, I, I, P],
-    "l3u_pw_stat_nsb": [I, I],
+    "l3u_pw_stat_nsb": [I, I, I],
     "l3u_pw_fwd": [P, L, P, I, P, P, L, I, P, I, I, I, I, P],
     "l3u_pw_bwd_weight_nparts": [I, I],
     "l3u_pw_bwd_weight": [P, L, P, L, P, I, I, I, I, P],
@@ -38,14 +38,16 @@ _SIGS = {
     "l3u_maxpool2_fwd": [P, L, P, L, P, I, I, I, I, I, P],
     "l3u_maxpool2_bwd": [P, L, P, P, L, P, L, I, I, I, I, I, P],
     "l3u_convt_d2s": [P, P, P, L, I, I, I, I, I, P],
+    "l3u_convt_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, P],
     "l3u_convt_s2d": [P, L, P, I, I, I, I, I, P],
     "l3u_chan_sum_nblocks": [L],
     "l3u_chan_sum": [P, L, P, I, I, L, P],
     "l3u_outconv_nblocks": [I],
-    "l3u_outconv_fwd": [P, L, P, P, P, I, I, I, P],
-    "l3u_outconv_bwd": [P, P, P, L, P, P, L, P, I, I, I, P],
+    "l3u_outconv_fwd": [P, L, P, P, P, P, P, I, I, I, P],
+    "l3u_outconv_bwd": [P, P, P, P, D, D, D, D, P, P, L, P, P, L, P, I, I, I, P],
     "l3u_ftl_nblocks": [L],
     "l3u_ftl_sums": [P, P, L, P, P, P],
+    "l3u_ftl_reduce": [P, I, P, P],
     "l3u_ftl_loss": [P, D, D, D, D, P, P],
     "l3u_ftl_bwd": [P, P, L, P, D, D, D, D, P, I, P, P],
     "l3u_adamw": [P, P, P, P, L, P, F, F, F, F, P, F, P],

@@ -159,8 +159,11 @@ class UNetEngine:
             raise NotImplementedError(f"H*W <= 4096 required by the stencil kernel, got {H * W}")
 
     # ------------------------------------------------------------------ forward
-    def forward(self, flat, x, training=False, dropout_p=0.0, counter=None, save=True):
-        """x: [N,1,D,H,W] fp32 on device -> probabilities [N,1,D,H,W] (+ saved state)."""
+    def forward(self, flat, x, training=False, dropout_p=0.0, counter=None, save=True, target=None,
+                ftl_part=None):
+        """x: [N,1,D,H,W] fp32 on device -> probabilities [N,1,D,H,W] (+ saved state).  With a
+        target (same shape) the out_conv launch also writes the FocalTversky partials into
+        ftl_part [N * l3u_outconv_nblocks(S)][3]."""
         self.check_shape(x)
         x = x.contiguous()
         N, _, D, H, W = x.shape
@@ -170,15 +173,16 @@ class UNetEngine:
             self._dry = True
             self.fwd_arena.reset(None)
             try:
-                self._forward_impl(flat, x, training, dropout_p, counter, save, dev)
+                self._forward_impl(flat, x, training, dropout_p, counter, save, dev, target, ftl_part)
             finally:
                 self._dry = False
             self._arenas[key] = torch.empty(max(self.fwd_arena.top, 64), dtype=torch.float32,
                                             device=dev)
         self.fwd_arena.reset(self._arenas[key])
-        return self._forward_impl(flat, x, training, dropout_p, counter, save, dev)
+        return self._forward_impl(flat, x, training, dropout_p, counter, save, dev, target, ftl_part)
 
-    def _forward_impl(self, flat, x, training, dropout_p, counter, save, dev):
+    def _forward_impl(self, flat, x, training, dropout_p, counter, save, dev, target=None,
+                      ftl_part=None):
         N, _, D, H, W = x.shape
         c0, c1, c2, c3 = self.enc
         dims = [(D >> k, H >> k, W >> k) for k in range(4)]
@@ -222,11 +226,9 @@ class UNetEngine:
                                                 ("up3.", cat3, c0, 0))):
             d, h, w = dims[lvl + 1]
             ci = prev.C
-            yp = e(N, co * 8, S[lvl + 1])
-            self._call("l3u_pw_fwd", prev.p, prev.ns, self._w(flat, up + "up.weight"), 1, None,
-                       yp.data_ptr(), co * 8 * S[lvl + 1], 0, None, N, ci, co * 8, S[lvl + 1], st)
-            self._call("l3u_convt_d2s", yp.data_ptr(), self._w(flat, up + "up.bias"), cat.data_ptr(),
-                       2 * co * S[lvl], N, co, d, h, w, st)
+            self._call("l3u_convt_fwd", prev.p, prev.ns, self._w(flat, up + "up.weight"),
+                       self._w(flat, up + "up.bias"), cat.data_ptr(), 2 * co * S[lvl], N, ci, co,
+                       d, h, w, st)
             out = e(N, co, S[lvl])
             cat_v = V(cat, 0, 2 * co * S[lvl], 2 * co)
             blk[up + "res_block."] = self._block_fwd(flat, up + "res_block.", 5 + k, cat_v,
@@ -236,8 +238,11 @@ class UNetEngine:
             prev = V(out, 0, co * S[lvl], co)
         sv["ups"] = ups
         p = e(N, 1, D, H, W)
+        # with a target, the FocalTversky first-stage partials come out of the same launch
         self._call("l3u_outconv_fwd", prev.p, prev.ns, self._w(flat, "out_conv.weight"),
-                   self._w(flat, "out_conv.bias"), p.data_ptr(), N, c0, S[0], st)
+                   self._w(flat, "out_conv.bias"), p.data_ptr(),
+                   target.data_ptr() if target is not None else None,
+                   ftl_part.data_ptr() if target is not None else None, N, c0, S[0], st)
         sv["h"] = prev
         sv["p"] = p
         sv["blk"] = blk
@@ -257,7 +262,8 @@ class UNetEngine:
         cin = x.C
         cout = out.C
         e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
-        nsb = nat.query("l3u_pw_stat_nsb", cout, S)
+        nsb = nat.query("l3u_pw_stat_nsb", cin, cout, S)      # pw1 / shortcut (K = cin)
+        nsb2 = nat.query("l3u_pw_stat_nsb", cout, cout, S)    # pw2 (K = cout)
         recs = e(3, N * cout, 8)
         rec_r, rec1, rec2 = (recs[0].data_ptr(), recs[1].data_ptr(), recs[2].data_ptr())
         sv = {"x": x, "out": out, "recs": recs}
@@ -288,10 +294,10 @@ class UNetEngine:
         self._call("l3u_dw3_fwd", y1.data_ptr(), cout * S, self._w(flat, pre + "conv2.depthwise.weight"),
                    None, nat.norm_src_ptr(src1), z2.data_ptr(), cout * S, N, cout, d, h, w, st)
         y2 = e(N, cout, S)
-        s2 = self.fwd_arena.alloc(N * cout * nsb * 3)
+        s2 = self.fwd_arena.alloc(N * cout * nsb2 * 3)
         self._call("l3u_pw_fwd", z2.data_ptr(), cout * S, self._w(flat, pre + "conv2.pointwise.weight"),
                    0, None, y2.data_ptr(), cout * S, 0, self.fwd_arena.ptr(s2), N, cout, cout, S, st)
-        src2 = self._src(flat, pre + "norm2.", s2, nsb, rec2, 0.0, cptr, 0)
+        src2 = self._src(flat, pre + "norm2.", s2, nsb2, rec2, 0.0, cptr, 0)
         self._call("l3u_norm_act_fwd", y2.data_ptr(), cout * S, None, nat.norm_src_ptr(src2), rv.p,
                    rv.ns, None, nat.norm_src_ptr(src_r), 1 if shortcut else 0, out.p, out.ns, N,
                    cout, S, st)
@@ -299,9 +305,10 @@ class UNetEngine:
         return sv
 
     # ------------------------------------------------------------------ backward
-    def backward(self, flat, gflat, sv, dp, need_dx=False):
-        """Given dL/dp write all parameter gradients into gflat
-        (overwrite) and return dL/dx if need_dx."""
+    def backward(self, flat, gflat, sv, dp, need_dx=False, ftl=None):
+        """Given dL/dp write all parameter gradients into gflat (overwrite) and return dL/dx if
+        need_dx.  dp = None: the loss is FocalTversky and ftl = (target, global sums [3] fp64,
+        (alpha, beta, gamma, smooth)); its gradient is formed inside the out_conv backward."""
         N = sv["N"]
         D, H, W = sv["dims"][0]
         key = ("b", N, D, H, W, bool(need_dx))
@@ -310,22 +317,22 @@ class UNetEngine:
             self.bwd_arena.reset(None)
             self._items_rec = []
             try:
-                self._backward_impl(flat, gflat, sv, dp, need_dx)
+                self._backward_impl(flat, gflat, sv, dp, need_dx, ftl)
             finally:
                 self._dry = False
-            dev = dp.device
+            dev = sv["p"].device
             self._arenas[key] = torch.empty(max(self.bwd_arena.top, 64), dtype=torch.float32,
                                             device=dev)
             self._items[key] = torch.tensor(self._items_rec, dtype=torch.int64, device=dev)
         self.bwd_arena.reset(self._arenas[key])
         self._items_rec = []
-        dx = self._backward_impl(flat, gflat, sv, dp, need_dx)
+        dx = self._backward_impl(flat, gflat, sv, dp, need_dx, ftl)
         items = self._items[key]
         nat.call("l3u_reduce_segments", self.bwd_arena.ptr(0), items.data_ptr(), items.shape[0],
                  gflat.data_ptr(), nat.stream())
         return dx
 
-    def _backward_impl(self, flat, gflat, sv, dp, need_dx):
+    def _backward_impl(self, flat, gflat, sv, dp, need_dx, ftl=None):
         N = sv["N"]
         dims, S = sv["dims"], sv["S"]
         c0, c1, c2, c3 = self.enc
@@ -338,7 +345,12 @@ class UNetEngine:
         dh = e(N, c0, S[0])
         nb = nat.query("l3u_outconv_nblocks", S[0])
         po = A.alloc(2 * N * nb * (c0 + 1))          # fp64 partials
-        self._call("l3u_outconv_bwd", dp.data_ptr(), sv["p"].data_ptr(), h.p, h.ns,
+        if dp is not None:
+            g = (dp.data_ptr(), None, None, 0.0, 0.0, 0.0, 0.0, None)
+        else:   # FocalTversky gradient formed inside the kernel from the global sums
+            t, sums, (alpha, beta, gamma, smooth) = ftl
+            g = (None, t.data_ptr(), sums.data_ptr(), alpha, beta, gamma, smooth, None)
+        self._call("l3u_outconv_bwd", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
                    self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po), N, c0,
                    S[0], st)
         self._seg(po // 2, N * nb, c0 + 1, 1, c0, "out_conv.weight", f64=1)

@@ -45,25 +45,25 @@ class TrainStep:
 
     # ----------------------------------------------------------------- pieces
     def _fwd(self, x, t):
+        # the out_conv launch also produces the FocalTversky partials (losses.py:40-42)
+        N, S = x.shape[0], x[0].numel()
+        nparts = N * nat.query("l3u_outconv_nblocks", S)
+        part = torch.empty(nparts * 3, dtype=torch.float32, device=x.device)
         p, sv = self.engine.forward(self.flat, x, training=self.model.training,
                                     dropout_p=self.model.dropout_p,
-                                    counter=self.model._rng_counter, save=True)
-        n = p.numel()
-        nb = nat.query("l3u_ftl_nblocks", n)
-        part = torch.empty(nb * 3, dtype=torch.float32, device=p.device)
+                                    counter=self.model._rng_counter, save=True, target=t,
+                                    ftl_part=part)
         sums = torch.empty(3, dtype=torch.float64, device=p.device)
-        nat.call("l3u_ftl_sums", p.data_ptr(), t.data_ptr(), n, part.data_ptr(), sums.data_ptr(),
-                 nat.stream())
+        nat.call("l3u_ftl_reduce", part.data_ptr(), nparts, sums.data_ptr(), nat.stream())
         return p, sv, sums
 
     def _bwd(self, p, sv, t, sums):
         st = nat.stream()
         nat.call("l3u_ftl_loss", sums.data_ptr(), self.alpha, self.beta, self.gamma, self.smooth,
                  self.loss.data_ptr(), st)
-        dp = torch.empty_like(p)
-        nat.call("l3u_ftl_bwd", p.data_ptr(), t.data_ptr(), p.numel(), sums.data_ptr(), self.alpha,
-                 self.beta, self.gamma, self.smooth, None, 0, dp.data_ptr(), st)
-        self.engine.backward(self.flat, self.gflat, sv, dp, need_dx=False)
+        # dL/dp is formed inside the out_conv backward from t and the (global) sums
+        self.engine.backward(self.flat, self.gflat, sv, None, need_dx=False,
+                             ftl=(t, sums, (self.alpha, self.beta, self.gamma, self.smooth)))
 
     def _grad_exchange(self):
         exchange_grads(self.gflat, self.ftl_mode, self.group)

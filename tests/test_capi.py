@@ -62,7 +62,7 @@ def test_host_queries_without_gpu():
     assert _native.query("l3u_dw3_nchunk", 4, 32, 48, 48, 48) == 30   # 3 z-slabs x 10 y-strips
     assert _native.query("l3u_dw3_nchunk", 4, 32, 24, 24, 24) == 18   # 6 z-slabs x 3 y-strips
     assert _native.query("l3u_dw3_nchunk", 4, 128, 6, 6, 6) == 1
-    assert _native.query("l3u_pw_stat_nsb", 16, 48 ** 3) == 432   # 256-voxel tiles
+    assert _native.query("l3u_pw_stat_nsb", 16, 16, 48 ** 3) == 432   # 256-voxel tiles
 
 
 def test_no_cpu_fallback_in_product_package():

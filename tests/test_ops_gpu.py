@@ -191,7 +191,7 @@ def test_pw_fwd(cuda, case, layout):
     w_store = wm if layout == 0 else wm.t().contiguous()
     xd, wdv, bd = x.float().to(cuda), w_store.float().contiguous().to(cuda), bias.float().to(cuda)
     y = torch.full((N, J, S), float("nan"), device=cuda)
-    nsb = nat().query("l3u_pw_stat_nsb", J, S)
+    nsb = nat().query("l3u_pw_stat_nsb", K, J, S)
     part = torch.full((N * J * nsb * 3,), float("nan"), device=cuda)
     nat().call("l3u_pw_fwd", xd.data_ptr(), K * S, wdv.data_ptr(), layout, bd.data_ptr(),
                y.data_ptr(), J * S, 0, part.data_ptr(), N, K, J, S, st())
@@ -464,13 +464,14 @@ def test_outconv(cuda, case):
     hd, wd, bd = h.float().to(cuda), w.float().to(cuda), b.float().to(cuda)
     pd = torch.empty(N, 1, S, device=cuda)
     nat().call("l3u_outconv_fwd", hd.data_ptr(), C * S, wd.data_ptr(), bd.data_ptr(), pd.data_ptr(),
-               N, C, S, st())
+               None, None, N, C, S, st())
     nb = nat().query("l3u_outconv_nblocks", S)
     part = torch.empty(N * nb * (C + 1), dtype=torch.float64, device=cuda)
     dh = torch.empty(N, C, S, device=cuda)
     dpd = dp.float().to(cuda)
-    nat().call("l3u_outconv_bwd", dpd.data_ptr(), pd.data_ptr(), hd.data_ptr(), C * S, wd.data_ptr(),
-               dh.data_ptr(), C * S, part.data_ptr(), N, C, S, st())
+    nat().call("l3u_outconv_bwd", dpd.data_ptr(), pd.data_ptr(), None, None, 0.0, 0.0, 0.0, 0.0,
+               None, hd.data_ptr(), C * S, wd.data_ptr(), dh.data_ptr(), C * S, part.data_ptr(), N,
+               C, S, st())
     torch.cuda.synchronize()
     close(pd, p, 1e-6, "outconv p")
     close(dh, hr.grad, 1e-5, "outconv dh")
@@ -541,3 +542,69 @@ def test_reduce_segments(cuda):
     d = dst.cpu()
     assert d[0] == 0 + 10 + 20 + 30 and d[1] == 1 + 11 + 21 + 31 and d[2] == 2 + 12 + 22 + 32
     assert d[5] == 500 + 501 and d[6] == 600 + 601 and d[3] == -1 and d[7] == 6
+
+
+CONVT_FUSED = [(2, 128, 64, 6, 6, 6), (2, 64, 32, 12, 12, 12), (1, 32, 16, 24, 24, 24),
+               (2, 16, 8, 3, 4, 8), (1, 8, 4, 5, 7, 9), (3, 24, 16, 4, 8, 12)]
+
+
+@pytest.mark.parametrize("case", CONVT_FUSED)
+def test_convt_fwd_fused(cuda, case):
+    """l3u_convt_fwd: the GEMM with the scatter + bias in its epilogue, into the lower half of a
+    concat buffer (upper half untouched), vs torch conv_transpose3d in fp64."""
+    N, Ci, Co, D, H, W = case
+    Si = D * H * W
+    So = 8 * Si
+    gen = torch.Generator().manual_seed(11)
+    x = torch.randn(N, Ci, D, H, W, generator=gen, dtype=torch.float64)
+    w = torch.randn(Ci, Co, 2, 2, 2, generator=gen, dtype=torch.float64)
+    b = torch.randn(Co, generator=gen, dtype=torch.float64)
+    y = F.conv_transpose3d(x, w, b, stride=2)
+    xd, wd, bd = x.float().to(cuda), w.float().to(cuda), b.float().to(cuda)
+    cat = torch.full((N, 2 * Co, So), 7.0, device=cuda)
+    nat().call("l3u_convt_fwd", xd.data_ptr(), Ci * Si, wd.data_ptr(), bd.data_ptr(), cat.data_ptr(),
+               2 * Co * So, N, Ci, Co, D, H, W, st())
+    torch.cuda.synchronize()
+    close(cat[:, :Co].reshape(y.shape), y, 1e-5, f"convT fused {case}")
+    assert torch.all(cat[:, Co:] == 7.0)
+
+
+@pytest.mark.parametrize("case", [(2, 16, 4096), (3, 16, 1000), (1, 8, 37)])
+def test_outconv_ftl_fused(cuda, case):
+    """out_conv forward emitting the FocalTversky partials, and its backward forming dL/dp from
+    the global sums in-kernel, vs the oracle (losses.py:30-54 autograd) in fp64."""
+    from oracle.unet_oracle import focal_tversky
+    N, C, S = case
+    gen = torch.Generator().manual_seed(12)
+    h = torch.randn(N, C, S, generator=gen, dtype=torch.float64)
+    w = torch.randn(1, C, generator=gen, dtype=torch.float64) * 0.3
+    b = torch.randn(1, generator=gen, dtype=torch.float64)
+    t = (torch.rand(N, 1, S, generator=gen) > 0.8).double()
+    hr, wr, br = (v.clone().requires_grad_(True) for v in (h, w, b))
+    p = torch.sigmoid(torch.einsum("oc,ncs->nos", wr, hr) + br[None, :, None])
+    loss = focal_tversky(p, t)
+    loss.backward()
+    hd, wd, bd, td = h.float().to(cuda), w.float().to(cuda), b.float().to(cuda), t.float().to(cuda)
+    nb = nat().query("l3u_outconv_nblocks", S)
+    fpart = torch.full((N * nb * 3,), float("nan"), device=cuda)
+    pd = torch.empty(N, 1, S, device=cuda)
+    nat().call("l3u_outconv_fwd", hd.data_ptr(), C * S, wd.data_ptr(), bd.data_ptr(), pd.data_ptr(),
+               td.data_ptr(), fpart.data_ptr(), N, C, S, st())
+    sums = torch.empty(3, dtype=torch.float64, device=cuda)
+    nat().call("l3u_ftl_reduce", fpart.data_ptr(), N * nb, sums.data_ptr(), st())
+    lossd = torch.empty((), device=cuda)
+    nat().call("l3u_ftl_loss", sums.data_ptr(), 0.7, 0.3, 0.75, 1e-6, lossd.data_ptr(), st())
+    part = torch.empty(N * nb * (C + 1), dtype=torch.float64, device=cuda)
+    dh = torch.empty(N, C, S, device=cuda)
+    nat().call("l3u_outconv_bwd", None, pd.data_ptr(), td.data_ptr(), sums.data_ptr(), 0.7, 0.3, 0.75,
+               1e-6, None, hd.data_ptr(), C * S, wd.data_ptr(), dh.data_ptr(), C * S, part.data_ptr(),
+               N, C, S, st())
+    torch.cuda.synchronize()
+    pr = p.detach()
+    ref_sums = torch.stack([(pr * t).sum(), pr.sum(), t.sum()])
+    close(sums.cpu(), ref_sums, 1e-5, "ftl sums")
+    assert abs(float(lossd) - float(loss.detach())) <= 1e-5 * abs(float(loss.detach())) + 1e-7
+    close(dh, hr.grad, 1e-4, "dh via fused FTL gradient")
+    ps = part.view(N * nb, C + 1).double().sum(0).cpu()
+    close(ps[:C], wr.grad[0], 1e-4, "dw")
+    close(ps[C:], br.grad, 1e-4, "db")
