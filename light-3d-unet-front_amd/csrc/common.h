@@ -176,6 +176,27 @@ L3U_DEV void block_record(const l3u_norm_src& s, int n, int c, int C, bool store
   __syncthreads();
 }
 
+// Two records at once (waves 0 and 1 merge in parallel), one barrier; sh8: 16 floats of LDS.
+L3U_DEV void block_record2(const l3u_norm_src& a, const l3u_norm_src& b, bool has_b, int n, int c,
+                           int C, bool store, float* sh8) {
+  const int wv = threadIdx.x >> 6;
+  if (wv == 0 || (wv == 1 && has_b)) {
+    const l3u_norm_src& s = wv == 0 ? a : b;
+    float r[kRec];
+    finalize_record(s, n, c, C, r);
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int i = 0; i < kRec; ++i) sh8[wv * 8 + i] = r[i];
+      if (store && s.rec_out) {
+        float* o = s.rec_out + ((long long)n * C + c) * kRec;
+#pragma unroll
+        for (int i = 0; i < kRec; ++i) o[i] = r[i];
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // XCD-aware block remap (guide §5.5 T1, bijective form): blocks that share halo planes / weight
 // tiles are consecutive in the logical order, and consecutive logical ids land on one XCD.
 L3U_DEV int xcd_remap(int bid, int nblocks) {

@@ -364,39 +364,51 @@ __global__ void counter_add_kernel(int* c, int v) { c[0] += v; }
 __global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __restrict__ src,
                                                               const long long* __restrict__ items,
                                                               float* __restrict__ dst) {
+  __shared__ double red[256];
   const long long* it = items + (long long)blockIdx.x * 8;
   const int t = threadIdx.x;
   const int len = (int)it[4];
-  if (t >= len) return;
-  const long long base = it[0] + t * it[3];
+  // TP threads per output: thread (k, o) sums terms i = k, k+TP, k+2TP, ... of output o
+  // (consecutive threads on consecutive outputs: coalesced), then the TP partial sums are added
+  // in k order.  TP depends only on len, so the summation order is fixed: deterministic.
+  const int TP = 256 / len;
+  const int o = t % len, k = t / len;
   const long long cnt = it[1], is = it[2];
   double s = 0.0;
-  // loads are issued 16 at a time (memory-level parallelism); the adds stay in index order
-  if (it[7]) {
-    const double* sd = reinterpret_cast<const double*>(src) + base;
-    long long i = 0;
-    for (; i + 16 <= cnt; i += 16) {
-      double v[16];
+  if (k < TP) {
+    const long long base = it[0] + o * it[3];
+    const long long stp = is * TP;
+    long long i = k;
+    if (it[7]) {
+      const double* sd = reinterpret_cast<const double*>(src) + base;
+      for (; i + 15 * TP < cnt; i += 16 * TP) {
+        double v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = sd[(i + u) * is];
+        for (int u = 0; u < 16; ++u) v[u] = sd[i * is + u * stp];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) s += v[u];
+        for (int u = 0; u < 16; ++u) s += v[u];
+      }
+      for (; i < cnt; i += TP) s += sd[i * is];
+    } else {
+      const float* sf = src + base;
+      for (; i + 15 * TP < cnt; i += 16 * TP) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = sf[i * is + u * stp];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += v[u];
+      }
+      for (; i < cnt; i += TP) s += sf[i * is];
     }
-    for (; i < cnt; ++i) s += sd[i * is];
-  } else {
-    const float* sf = src + base;
-    long long i = 0;
-    for (; i + 16 <= cnt; i += 16) {
-      float v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = sf[(i + u) * is];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) s += v[u];
-    }
-    for (; i < cnt; ++i) s += sf[i * is];
   }
-  float* d = dst + it[5] + t;
-  *d = it[6] ? (float)((double)*d + s) : (float)s;
+  red[t] = s;
+  __syncthreads();
+  if (t < len) {
+    double r = 0.0;
+    for (int kk = 0; kk < TP; ++kk) r += red[kk * len + t];
+    float* d = dst + it[5] + t;
+    *d = it[6] ? (float)((double)*d + r) : (float)r;
+  }
 }
 
 int grid_for(long long n, int per_block, int cap) {

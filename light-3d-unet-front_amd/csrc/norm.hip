@@ -38,8 +38,7 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f;
   if (HAS_SRC) {
-    block_record(src2, n, c, C, blockIdx.x == 0, sh);
-    if (shortcut) block_record(srcr, n, c, C, blockIdx.x == 0, sh + 8);
+    block_record2(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh);
     m2 = sh[0]; a2 = sh[2]; b2 = sh[3];
     if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; }
   } else {
@@ -199,10 +198,17 @@ __global__ __launch_bounds__(256) void in_bwd_apply_kernel(
   }
 }
 
+#ifndef L3U_ELEM_PER_BLOCK
+#define L3U_ELEM_PER_BLOCK 4096
+#endif
+#ifndef L3U_ELEM_MAX_BLOCKS
+#define L3U_ELEM_MAX_BLOCKS 16
+#endif
+// workgroups per (n, c) plane of the elementwise IN kernels: few enough that the per-workgroup
+// record merge (in-kernel finalize) stays small next to the streaming work
 int elem_blocks(int S) {
-  const int per = 1024;   // elements per workgroup pass
-  int b = (S + per - 1) / per;
-  return b > 64 ? 64 : (b < 1 ? 1 : b);
+  int b = (S + L3U_ELEM_PER_BLOCK - 1) / L3U_ELEM_PER_BLOCK;
+  return b > L3U_ELEM_MAX_BLOCKS ? L3U_ELEM_MAX_BLOCKS : (b < 1 ? 1 : b);
 }
 
 }  // namespace

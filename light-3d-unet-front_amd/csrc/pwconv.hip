@@ -243,7 +243,7 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
     float* __restrict__ stat_part, int K, int Nout, int S, int nsb, int Dq, int Hq, int Wq) {
   constexpr int CO_BLK = 16 * NC;
   constexpr int T = NC * 16;   // accumulator floats per lane
-  extern __shared__ __attribute__((aligned(16))) float lds[];   // [3 waves][64 lanes][T]
+  extern __shared__ __attribute__((aligned(16))) float lds[];   // [4 waves][T][64 lanes]
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const int sb = blockIdx.x, co0 = blockIdx.y * CO_BLK, n = blockIdx.z;
   const float* xn = x + (long long)n * xns;
@@ -278,9 +278,11 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
     }
   }
   // cross-wave combine through LDS, value-major ([wave][value][lane]: consecutive lanes hit
-  // consecutive banks, conflict-free), added in fixed wave order
-  if (wave > 0) {
-    float* dst = lds + (wave - 1) * T * 64 + l;
+  // consecutive banks, conflict-free).  Every wave parks its partials; wave w then owns output
+  // tile m = w (16 channels x 64 voxels) and adds the four waves' partials of that tile in wave
+  // order (fixed: deterministic), so the epilogue stores are spread over min(NC, 4) waves.
+  {
+    float* dst = lds + wave * T * 64 + l;
 #pragma unroll
     for (int m = 0; m < NC; ++m)
 #pragma unroll
@@ -289,84 +291,79 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
         for (int r = 0; r < 4; ++r) dst[((m * 4 + q) * 4 + r) * 64] = acc[m][q][r];
   }
   __syncthreads();
-  if (wave != 0) return;
+  const int m = wave;
+  if (m >= NC) return;
+  f4 t4[4];
 #pragma unroll
-  for (int wv = 0; wv < 3; ++wv) {
-    const float* src = lds + wv * T * 64 + l;
+  for (int q = 0; q < 4; ++q) {
 #pragma unroll
-    for (int m = 0; m < NC; ++m)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[m][q][r] += src[((m * 4 + q) * 4 + r) * 64];
+    for (int r = 0; r < 4; ++r) {
+      const float* src = lds + ((m * 4 + q) * 4 + r) * 64 + l;
+      t4[q][r] = ((src[0] + src[T * 64]) + src[2 * T * 64]) + src[3 * T * 64];
+    }
   }
-  // epilogue (one wave): lane holds Y[co0+16m+lr][sb*64 + 16lk + 4r + q]
+  // epilogue: lane holds Y[co0+16m+lr][sb*64 + 16lk + 4r + q]
   float* yn = y + (long long)n * yns;
   if (D2S) {
 #pragma unroll
-    for (int m = 0; m < NC; ++m)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        d2s_store<VEC>(yn, co0 + 16 * m + lr, Nout, bias, sb * 64 + 16 * lk + 4 * r,
-                       f4{acc[m][0][r], acc[m][1][r], acc[m][2][r], acc[m][3][r]}, S, Dq, Hq, Wq);
+    for (int r = 0; r < 4; ++r)
+      d2s_store<VEC>(yn, co0 + 16 * m + lr, Nout, bias, sb * 64 + 16 * lk + 4 * r,
+                     f4{t4[0][r], t4[1][r], t4[2][r], t4[3][r]}, S, Dq, Hq, Wq);
     return;
   }
   const int cnt = min(64, S - sb * 64);
+  const int co = co0 + 16 * m + lr;
+  const bool cok = co < Nout;
+  const float bv = (bias && cok) ? bias[co] : 0.f;
+  float lsum = 0.f;
 #pragma unroll
-  for (int m = 0; m < NC; ++m) {
-    const int co = co0 + 16 * m + lr;
-    const bool cok = co < Nout;
-    const float bv = (bias && cok) ? bias[co] : 0.f;
-    float lsum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int sv = sb * 64 + 16 * lk + 4 * r;
-      f4 v = f4{acc[m][0][r], acc[m][1][r], acc[m][2][r], acc[m][3][r]} + bv;
-      float* dst = yn + (long long)co * S + sv;
-      if (cok) {
-        if (VEC) {
-          if (sv < S) {
-            if (accumulate) v += *reinterpret_cast<const f4*>(dst);
-            *reinterpret_cast<f4*>(dst) = v;
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (sv + q < S) {
-              if (accumulate) v[q] += dst[q];
-              dst[q] = v[q];
-            }
+  for (int r = 0; r < 4; ++r) {
+    const int sv = sb * 64 + 16 * lk + 4 * r;
+    f4 v = f4{t4[0][r], t4[1][r], t4[2][r], t4[3][r]} + bv;
+    float* dst = yn + (long long)co * S + sv;
+    if (cok) {
+      if (VEC) {
+        if (sv < S) {
+          if (accumulate) v += *reinterpret_cast<const f4*>(dst);
+          *reinterpret_cast<f4*>(dst) = v;
         }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        acc[m][q][r] = v[q];
-        if (sv + q < S) lsum += v[q];
-      }
-    }
-    if (stat_part != nullptr) {
-      lsum += __shfl_xor(lsum, 16, 64);
-      lsum += __shfl_xor(lsum, 32, 64);
-      const float mean = lsum / (float)cnt;
-      float m2 = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int sv = sb * 64 + 16 * lk + 4 * r;
+      } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (sv + q < S) {
-            const float d = acc[m][q][r] - mean;
-            m2 = fmaf(d, d, m2);
+            if (accumulate) v[q] += dst[q];
+            dst[q] = v[q];
           }
       }
-      m2 += __shfl_xor(m2, 16, 64);
-      m2 += __shfl_xor(m2, 32, 64);
-      if (lk == 0 && cok) {
-        float* o = stat_part + (((long long)n * Nout + co) * nsb + sb) * 3;
-        o[0] = (float)cnt;
-        o[1] = mean;
-        o[2] = m2;
-      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      t4[q][r] = v[q];
+      if (sv + q < S) lsum += v[q];
+    }
+  }
+  if (stat_part != nullptr) {
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    const float mean = lsum / (float)cnt;
+    float m2 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int sv = sb * 64 + 16 * lk + 4 * r;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (sv + q < S) {
+          const float d = t4[q][r] - mean;
+          m2 = fmaf(d, d, m2);
+        }
+    }
+    m2 += __shfl_xor(m2, 16, 64);
+    m2 += __shfl_xor(m2, 32, 64);
+    if (lk == 0 && cok) {
+      float* o = stat_part + (((long long)n * Nout + co) * nsb + sb) * 3;
+      o[0] = (float)cnt;
+      o[1] = mean;
+      o[2] = m2;
     }
   }
 }
@@ -501,7 +498,7 @@ int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout,
     const int nsb = (S + 63) / 64;
     int NC = Nout <= 16 ? 1 : (Nout <= 32 ? 2 : 4);
     while (NC > 1 && (long long)nsb * ((Nout + 16 * NC - 1) / (16 * NC)) * N < 256) NC >>= 1;
-    const size_t lds = 3 * 64 * (size_t)NC * 16 * sizeof(float);
+    const size_t lds = 4 * 64 * (size_t)NC * 16 * sizeof(float);
     dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), N), block(256);
 #define PWK(NC_, V_, D_) hipLaunchKernelGGL((pw_fwd_ks_kernel<NC_, V_, D_>), grid, block, lds, stream, \
       x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq)

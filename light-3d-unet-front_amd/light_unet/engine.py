@@ -140,8 +140,8 @@ class UNetEngine:
         f64=1: the partials are fp64 and src_off/strides count doubles from the arena base."""
         base = self.offsets[dst_name][0] + dst_elem
         t0 = 0
-        while t0 < length:
-            ln = min(256, length - t0)
+        while t0 < length:   # <= 32 outputs per item: >= 8 threads share each output's terms
+            ln = min(32, length - t0)
             self._items_rec.append((src_off + t0 * tstride, count, istride, tstride, ln,
                                     base + t0, accumulate, f64))
             t0 += ln
