@@ -66,33 +66,38 @@ def dw_bytes(N, C, S):
 
 
 class KernelTimer:
-    """Captures the arguments of one C-ABI call of the step (the dominant kernel at its real
-    shape and buffers), then re-issues exactly that call back-to-back between two HIP events on
-    the launch stream: the average is the kernel's own duration, free of event/launch gaps."""
+    """Captures the arguments of the C-ABI calls that make up the dominant operation (at their
+    real shapes and buffers) during one eager step, then re-issues exactly those calls
+    back-to-back between two HIP events on one stream: the average is the kernels' own
+    duration, free of event/launch gaps."""
 
-    def __init__(self, name, match):
-        self.name, self.match, self.args = name, match, None
+    def __init__(self, names, match):
+        self.names, self.match, self.args = names, match, {}
 
     def wrap(self, nat):
         orig = nat.call
 
         def call(name, *args):
-            if name == self.name and self.match(args) and self.args is None:
-                self.args = args
+            if name in self.names and self.match(args) and name not in self.args:
+                self.args[name] = args
             orig(name, *args)
         nat.call = call
         return orig
 
     def mean_ms(self, nat_call, reps=50):
-        if self.args is None:
+        if set(self.args) != set(self.names):
             return None
         s = torch.cuda.current_stream()
+
+        def issue():
+            for name in self.names:
+                nat_call(name, *self.args[name][:-1], s.cuda_stream)
         for _ in range(3):
-            nat_call(self.name, *self.args)
+            issue()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         for _ in range(reps):
-            nat_call(self.name, *self.args)
+            issue()
         e1.record(s)
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
@@ -188,7 +193,8 @@ def main():
     # roofline leg (eager, instrumented): HIP events around the dominant kernel's launches
     N, S = args.batch, args.size ** 3
     cdom = 2 * enc[0]      # up3.res_block conv1.depthwise: [N, 2*c0, D^3] backward
-    timer = KernelTimer("l3u_dw3_bwd", lambda a: a[-5] == cdom and a[-4] == args.size)
+    # l3u_dw3_bwd args end with (..., N, C, D, H, W, stream)
+    timer = KernelTimer(("l3u_dw3_bwd",), lambda a: a[-5] == cdom and a[-4] == args.size)
     orig = timer.wrap(nat)
     for i in range(3):
         step(xs[i % 8], ts[i % 8])

@@ -68,6 +68,15 @@ int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long
                 const float* w, const float* rec, float* dx, long long dx_nstride, int accumulate,
                 float* dw_part, double* in_part, int N, int C, int D, int H, int W,
                 hipStream_t stream);
+/* the two halves of l3u_dw3_bwd as separate calls (same arguments and partial layouts), so the
+ * weight gradient can run on another stream off the data-gradient critical path             */
+int l3u_dw3_bwd_data(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
+                     const float* w, const float* rec, float* dx, long long dx_nstride,
+                     int accumulate, double* in_part, int N, int C, int D, int H, int W,
+                     hipStream_t stream);
+int l3u_dw3_bwd_weight(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
+                       const float* w, const float* rec, float* dw_part, int N, int C, int D,
+                       int H, int W, hipStream_t stream);
 
 /* ---- channel-contraction GEMM on MFMA (v_mfma_f32_16x16x4_f32) ------------------------------
  * Y[n][j][s] = sum_k Wm[j][k] X[n][k][s] (+ bias[j]) (+ Y if accumulate)

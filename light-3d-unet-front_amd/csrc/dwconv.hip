@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void dw3_bwd_kernel(
       }
     }
     const int zf = zd - 1;   // dA plane zf is complete
-    if (zf >= z0 && zf < z1) {
+    if (dx != nullptr && zf >= z0 && zf < z1) {
 #pragma unroll
       for (int k = 0; k < P; ++k) {
         if (!own[k]) continue;
@@ -273,11 +273,11 @@ __global__ __launch_bounds__(256) void dw3_bwd_kernel(
     if (ln == 0) { redd[wv * 2] = r1; redd[wv * 2 + 1] = r2; }
   }
   __syncthreads();
-  if (tid < 27) {
+  if (tid < 27 && dw_part != nullptr) {
     const float r = (red[tid] + red[27 + tid]) + (red[54 + tid] + red[81 + tid]);
     dw_part[((long long)c * N * nchunk + (long long)n * nchunk + chunk) * 27 + tid] = r;
   }
-  if (MODE == 1 && tid >= 32 && tid < 34) {
+  if (MODE == 1 && dx != nullptr && tid >= 32 && tid < 34) {
     const int j = tid - 32;
     const double r = (redd[j] + redd[2 + j]) + (redd[4 + j] + redd[6 + j]);
     // in_part layout [c][n][chunk][2]
@@ -905,41 +905,52 @@ int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
-                const float* w, const float* rec, float* dx, long long dx_nstride, int accumulate,
-                float* dw_part, double* in_part, int N, int C, int D, int H, int W,
-                hipStream_t stream) {
+}  // extern "C"
+
+namespace {
+
+// parts: 1 = data gradient (dx, IN-backward sums), 2 = weight gradient (dw_part), 3 = both
+int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
+                   const float* w, const float* rec, float* dx, long long dx_nstride,
+                   int accumulate, float* dw_part, double* in_part, int N, int C, int D, int H,
+                   int W, int parts, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && D > 0 && H > 0 && W > 0);
-  L3U_REQUIRE(rec == nullptr || in_part != nullptr);
+  L3U_REQUIRE(!(parts & 1) || dx != nullptr);
+  L3U_REQUIRE(!(parts & 2) || dw_part != nullptr);
+  L3U_REQUIRE(!(parts & 1) || rec == nullptr || in_part != nullptr);
   L3U_REQUIRE(rec == nullptr || accumulate == 0);
   if (use_quads(H, W) && x_nstride % 4 == 0 && dz_nstride % 4 == 0 && dx_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
-    if (dw_split(H, W)) {
+    if (dw_split(H, W) || parts != 3) {
       // data gradient = the forward stencil with flipped taps (+ epilogue), then the weight
       // gradient on its own; both use the same tile geometry, so the chunking of dw_part /
       // in_part is identical to the fused kernel's
-      const l3u_norm_src z{};
-      size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
-      if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);
+      if (parts & 1) {
+        const l3u_norm_src z{};
+        size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
+        if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);
 #define DWQX(E_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<0, E_, T_>), grid, block, lds, stream, dz, \
       dz_nstride, w, rec, z, 0, dx, dx_nstride, (E_ == 1 ? x : dx), (E_ == 1 ? x_nstride : dx_nstride), \
       in_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
 #define DWQX_T(E_) do { if (g.TZ == 16) DWQX(E_, 16); else if (g.TZ == 8) DWQX(E_, 8); else if (g.TZ == 4) DWQX(E_, 4); else DWQX(E_, 2); } while (0)
-      if (rec) DWQX_T(1);
-      else if (accumulate) DWQX_T(2);
-      else DWQX_T(3);
+        if (rec) DWQX_T(1);
+        else if (accumulate) DWQX_T(2);
+        else DWQX_T(3);
 #undef DWQX_T
 #undef DWQX
-      size_t lds2 = 2 * (size_t)(g.RB + 2) * W * sizeof(float);
-      if (lds2 < 128 * sizeof(float)) lds2 = 128 * sizeof(float);
+      }
+      if (parts & 2) {
+        size_t lds2 = 2 * (size_t)(g.RB + 2) * W * sizeof(float);
+        if (lds2 < 128 * sizeof(float)) lds2 = 128 * sizeof(float);
 #define DWQW(X_, T_) hipLaunchKernelGGL((dw3q_dw_kernel<X_, T_>), grid, block, lds2, stream, dz, \
       dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
 #define DWQW_T(X_) do { if (g.TZ == 16) DWQW(X_, 16); else if (g.TZ == 8) DWQW(X_, 8); else if (g.TZ == 4) DWQW(X_, 4); else DWQW(X_, 2); } while (0)
-      if (rec) DWQW_T(1);
-      else DWQW_T(0);
+        if (rec) DWQW_T(1);
+        else DWQW_T(0);
 #undef DWQW_T
 #undef DWQW
+      }
       L3U_CHECK_LAUNCH();
     }
     size_t lds = 4 * (size_t)(g.RB + 2) * W * sizeof(float);
@@ -955,15 +966,45 @@ int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long
 #undef DWQB
     L3U_CHECK_LAUNCH();
   }
+  // small / odd planes: one fused kernel; a partial call only skips the other part's stores
   L3U_REQUIRE(H * W <= 4096);
   const int TZ = pick_tz(D), nchunk = (D + TZ - 1) / TZ;
   const int P = (H * W + 255) / 256;
   size_t lds = 4 * (size_t)(H + 2) * (W + 2) * sizeof(float);
   if (lds < 128 * sizeof(float)) lds = 128 * sizeof(float);   // reduction scratch
   dim3 grid(N * C * nchunk), block(256);
-  if (rec) DW_DISPATCH_P(dw3_bwd_kernel, 1, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part, in_part, N, C, D, H, W, TZ, nchunk);
-  else DW_DISPATCH_P(dw3_bwd_kernel, 0, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part, in_part, N, C, D, H, W, TZ, nchunk);
+  float* dxs = (parts & 1) ? dx : nullptr;
+  float* dws = (parts & 2) ? dw_part : nullptr;
+  if (rec) DW_DISPATCH_P(dw3_bwd_kernel, 1, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dxs, dx_nstride, accumulate, dws, in_part, N, C, D, H, W, TZ, nchunk);
+  else DW_DISPATCH_P(dw3_bwd_kernel, 0, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dxs, dx_nstride, accumulate, dws, in_part, N, C, D, H, W, TZ, nchunk);
   L3U_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+extern "C" {
+
+int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
+                const float* w, const float* rec, float* dx, long long dx_nstride, int accumulate,
+                float* dw_part, double* in_part, int N, int C, int D, int H, int W,
+                hipStream_t stream) {
+  return dw3_bwd_launch(dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part,
+                        in_part, N, C, D, H, W, 3, stream);
+}
+
+int l3u_dw3_bwd_data(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
+                     const float* w, const float* rec, float* dx, long long dx_nstride,
+                     int accumulate, double* in_part, int N, int C, int D, int H, int W,
+                     hipStream_t stream) {
+  return dw3_bwd_launch(dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, nullptr,
+                        in_part, N, C, D, H, W, 1, stream);
+}
+
+int l3u_dw3_bwd_weight(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
+                       const float* w, const float* rec, float* dw_part, int N, int C, int D,
+                       int H, int W, hipStream_t stream) {
+  return dw3_bwd_launch(dz, dz_nstride, x, x_nstride, w, rec, nullptr, dz_nstride, 0, dw_part,
+                        nullptr, N, C, D, H, W, 2, stream);
 }
 
 }  // extern "C"

@@ -25,6 +25,8 @@ _SIGS = {
     "l3u_dw3_nchunk": [I, I, I, I, I],
     "l3u_dw3_fwd": [P, L, P, P, P, P, L, I, I, I, I, I, P],
     "l3u_dw3_bwd": [P, L, P, L, P, P, P, L, I, P, P, I, I, I, I, I, P],
+    "l3u_dw3_bwd_data": [P, L, P, L, P, P, P, L, I, P, I, I, I, I, I, P],
+    "l3u_dw3_bwd_weight": [P, L, P, L, P, P, P, I, I, I, I, I, P],
     "l3u_pw_stat_nsb": [I, I, I],
     "l3u_pw_fwd": [P, L, P, I, P, P, L, I, P, I, I, I, I, P],
     "l3u_pw_bwd_weight_nparts": [I, I],

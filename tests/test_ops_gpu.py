@@ -608,3 +608,44 @@ def test_outconv_ftl_fused(cuda, case):
     ps = part.view(N * nb, C + 1).double().sum(0).cpu()
     close(ps[:C], wr.grad[0], 1e-4, "dw")
     close(ps[C:], br.grad, 1e-4, "db")
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 48, 48, 48), (4, 32, 24, 24, 24), (2, 8, 6, 6, 6),
+                                   (1, 5, 7, 12, 8)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_dw3_bwd_split_calls(cuda, shape, mode):
+    """l3u_dw3_bwd_data + l3u_dw3_bwd_weight (the engine issues them on two streams) give
+    bitwise the results of the combined l3u_dw3_bwd (mode 2 = accumulate into dx)."""
+    N, C, D, H, W = shape
+    S = D * H * W
+    gen = torch.Generator().manual_seed(31)
+    x = torch.randn(N, C, S, generator=gen).to(cuda)
+    dz = torch.randn(N, C, S, generator=gen).to(cuda)
+    w = torch.randn(C, 27, generator=gen).to(cuda)
+    rec = make_rec(N, C, gen).float().to(cuda) if mode == 1 else None
+    init = torch.randn(N, C, S, generator=gen).to(cuda)
+    nch = nat().query("l3u_dw3_nchunk", N, C, D, H, W)
+    acc = 1 if mode == 2 else 0
+
+    def run(split):
+        dx = init.clone()
+        dwp = torch.full((C * N * nch * 27,), float("nan"), device=cuda)
+        inp = torch.full((C * N * nch * 2,), float("nan"), dtype=torch.float64, device=cuda)
+        r = rec.data_ptr() if rec is not None else None
+        ip = inp.data_ptr() if rec is not None else None
+        if split:
+            nat().call("l3u_dw3_bwd_data", dz.data_ptr(), C * S, x.data_ptr(), C * S, w.data_ptr(), r,
+                       dx.data_ptr(), C * S, acc, ip, N, C, D, H, W, st())
+            nat().call("l3u_dw3_bwd_weight", dz.data_ptr(), C * S, x.data_ptr(), C * S, w.data_ptr(),
+                       r, dwp.data_ptr(), N, C, D, H, W, st())
+        else:
+            nat().call("l3u_dw3_bwd", dz.data_ptr(), C * S, x.data_ptr(), C * S, w.data_ptr(), r,
+                       dx.data_ptr(), C * S, acc, dwp.data_ptr(), ip, N, C, D, H, W, st())
+        torch.cuda.synchronize()
+        return dx, dwp, inp
+
+    a, b = run(False), run(True)
+    assert torch.equal(a[0], b[0])
+    assert torch.equal(a[1], b[1])
+    if rec is not None:
+        assert torch.equal(a[2], b[2])
