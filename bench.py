@@ -9,9 +9,11 @@ timed step).  N > 1: one process per GPU (torch.distributed.run), exact global-b
 (3-float all-reduce) + one flat-gradient RCCL all-reduce per step; per-GPU batch fixed (weak
 scaling); time = max over ranks.
 
-Also reported: eval forward ms/patch (bs 1 and 4), the roofline of the dominant kernel measured
-live with HIP events around its launches, and the CPU baseline (the torch-CPU oracle restatement
-of the same network on this host's cores, rank 0 only, bounded sample).
+Also reported: eval forward ms/patch (bs 1 and 4), the config-4 whole-volume sliding-window
+inference of a 256^3 synthetic PET volume (seconds, ms/window; light_unet.utils), the roofline of
+the dominant kernel measured with HIP events around back-to-back replays of its C-ABI call, and
+the CPU baseline (the torch-CPU oracle restatement of the same network on this host's cores,
+rank 0 only, bounded sample).
 """
 import argparse
 import json
@@ -45,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--ftl-mode", default="exact", choices=["exact", "local"])
+    ap.add_argument("--no-sliding", action="store_true", help="skip the config-4 inference timing")
     return ap.parse_args()
 
 
@@ -163,6 +166,41 @@ def fwd_ms_per_patch(model, bs, size, device, iters=20):
     return 1000 * dt / iters / bs
 
 
+def synthetic_pet(size=256, seed=42):
+    """background U[0,0.05), central ellipsoid body U[0.1,0.4], 20 hot
+    spheres (radius 2-6 voxels) U[0.6,1.0]."""
+    rng = np.random.default_rng(seed)
+    vol = rng.uniform(0.0, 0.05, (size, size, size)).astype(np.float32)
+    zz, yy, xx = np.ogrid[:size, :size, :size]
+    c = size / 2
+    body = ((zz - c) / (0.45 * size)) ** 2 + ((yy - c) / (0.35 * size)) ** 2 + ((xx - c) / (0.3 * size)) ** 2 <= 1
+    vol[body] = rng.uniform(0.1, 0.4, int(body.sum())).astype(np.float32)
+    for _ in range(20):
+        r = rng.integers(2, 7)
+        ctr = rng.integers(int(0.3 * size), int(0.7 * size), 3)
+        sph = (zz - ctr[0]) ** 2 + (yy - ctr[1]) ** 2 + (xx - ctr[2]) ** 2 <= r * r
+        vol[sph] = rng.uniform(0.6, 1.0, int(sph.sum())).astype(np.float32)
+    return vol
+
+
+def sliding_bench(model, device, size=256):
+    """Config 4: whole-volume sliding-window inference (48^3 windows, overlap 0.5) of a 256^3
+    synthetic PET volume, host numpy in -> host prob map out (the reference's contract)."""
+    from light_unet.utils import sliding_window_inference_3d, window_positions
+    vol = synthetic_pet(size)
+    nwin = len(window_positions(size, 48, 24)) ** 3
+    sliding_window_inference_3d(vol[:96, :96, :96], model, device=device)   # warm up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    prob = sliding_window_inference_3d(vol, model, device=device, window_batch=32)
+    dt = time.perf_counter() - t0
+    if not np.isfinite(prob).all():
+        raise SystemExit("non-finite sliding-window output")
+    return {"volume": [size] * 3, "windows": nwin, "seconds": round(dt, 4),
+            "ms_per_window": round(1000 * dt / nwin, 4), "window_batch": 32,
+            "note": "includes the host->device upload and the prob-map copy back"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -235,6 +273,7 @@ def main():
     if not np.isfinite(final_loss):
         raise SystemExit(f"non-finite loss {final_loss}")
 
+    sliding = sliding_bench(model, device) if (rank == 0 and not args.no_sliding) else None
     fwd1 = fwd_ms_per_patch(model, 1, args.size, device) if rank == 0 else None
     fwd4 = fwd_ms_per_patch(model, args.batch, args.size, device) if rank == 0 else None
     out = None
@@ -265,6 +304,7 @@ def main():
                        "graph": not args.no_graph},
             "fwd_ms_per_patch": {"bs1": round(fwd1, 4), f"bs{args.batch}": round(fwd4, 4)},
             "final_loss": round(final_loss, 6),
+            "sliding_window_256": sliding,
             "roofline": {
                 "kernel": f"l3u_dw3_bwd [{N},{cdom},{args.size}^3] (up3.res_block.conv1.depthwise "
                           "backward: flipped-tap data-gradient stencil + weight-gradient pass, "

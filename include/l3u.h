@@ -202,6 +202,18 @@ int l3u_adamw(float* p, const float* g, float* m, float* v, long long numel, con
 int l3u_reduce_segments(const float* src, const long long* items, int nitems, float* dst,
                         hipStream_t stream);
 
+/* ---- whole-volume sliding-window inference (light_unet/utils.py:11-173) --------------------
+ * gather: out[b] = volume[z:z+pd, y:y+ph, x:x+pw] of window b (pos[b] = {z, y, x}), zero past
+ *         the volume edge (utils.py:96-113)
+ * blend:  prob[v] = sum_w pred_w[v] * imp[v - pos_w] / sum_w imp[v - pos_w] over the windows
+ *         covering v, in the reference's window order (z, y, x) with separate fp32 multiply and
+ *         add; windows are the grid zpos x ypos x xpos, preds[(iz*ny + iy)*nx + ix][pd*ph*pw] */
+int l3u_window_gather(const float* img, int D, int H, int W, const int* pos, int B, int pd, int ph,
+                      int pw, float* out, hipStream_t stream);
+int l3u_window_blend(const float* preds, const int* zpos, int nz, const int* ypos, int ny,
+                     const int* xpos, int nx, const float* imp, int D, int H, int W, int pd, int ph,
+                     int pw, float* prob, hipStream_t stream);
+
 /* device counter += value (Dropout3d RNG stream position, advanced once per training forward) */
 int l3u_counter_add(int* counter, int value, hipStream_t stream);
 

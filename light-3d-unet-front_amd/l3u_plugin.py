@@ -15,6 +15,7 @@ After install():
     light_unet.models.losses.FocalTverskyLoss       -> l3u_amd.models.losses.FocalTverskyLoss
     light_unet.models.losses.get_loss_function      -> l3u_amd.models.losses.get_loss_function
     light_unet.models.Lightweight3DUNet / get_loss_function (package re-exports, models/__init__.py:6-8)
+    light_unet.utils.sliding_window_inference_3d    -> l3u_amd.utils.sliding_window_inference_3d
 Everything else in the reference package is left untouched.
 """
 import importlib
@@ -26,6 +27,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 ALIAS = "l3u_amd"
 
 REPLACED = {
+    "light_unet.utils": ("sliding_window_inference_3d",),
     "light_unet.models.unet3d": ("Lightweight3DUNet",),
     "light_unet.models.losses": ("FocalTverskyLoss", "get_loss_function"),
     "light_unet.models": ("Lightweight3DUNet", "FocalTverskyLoss", "get_loss_function"),
@@ -44,6 +46,7 @@ def load():
     spec.loader.exec_module(mod)
     importlib.import_module(ALIAS + ".models.unet3d")
     importlib.import_module(ALIAS + ".models.losses")
+    importlib.import_module(ALIAS + ".utils")
     return mod
 
 
@@ -56,9 +59,10 @@ def install():
         "Lightweight3DUNet": sys.modules[ALIAS + ".models.unet3d"].Lightweight3DUNet,
         "FocalTverskyLoss": sys.modules[ALIAS + ".models.losses"].FocalTverskyLoss,
         "get_loss_function": sys.modules[ALIAS + ".models.losses"].get_loss_function,
+        "sliding_window_inference_3d": sys.modules[ALIAS + ".utils"].sliding_window_inference_3d,
     }
     mods = {}
-    for modname in ("light_unet.models.unet3d", "light_unet.models.losses"):
+    for modname in ("light_unet.utils", "light_unet.models.unet3d", "light_unet.models.losses"):
         mods[modname] = importlib.import_module(modname)
     pkg = sys.modules.get("light_unet.models")
     if pkg is not None:

@@ -3,8 +3,8 @@
 Mirrors the reference import paths used by its Trainer / Inferencer:
     from light_unet.models.unet3d import Lightweight3DUNet       (trainer.py:16, inferencer.py:13)
     from light_unet.models.losses import get_loss_function        (trainer.py:17)
-(the on-device sliding_window_inference_3d of trainer.py:19 / utils.py:11 is the next row,
-SURVEY §8f rank 1).  To bind this build into the reference package, see l3u_plugin.py.
+    from light_unet.utils import sliding_window_inference_3d      (trainer.py:19)
+To bind this build into the reference package, see l3u_plugin.py.
 Compute runs in lib/libl3u_hip.so (include/l3u.h); see DESIGN.md.
 """
 __version__ = "0.1.0"

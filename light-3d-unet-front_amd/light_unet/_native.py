@@ -50,6 +50,8 @@ _SIGS = {
     "l3u_ftl_nblocks": [L],
     "l3u_ftl_sums": [P, P, L, P, P, P],
     "l3u_ftl_reduce": [P, I, P, P],
+    "l3u_window_gather": [P, I, I, I, P, I, I, I, I, P, P],
+    "l3u_window_blend": [P, P, I, P, I, P, I, P, I, I, I, I, I, I, P, P],
     "l3u_ftl_loss": [P, D, D, D, D, P, P],
     "l3u_ftl_bwd": [P, P, L, P, D, D, D, D, P, I, P, P],
     "l3u_adamw": [P, P, P, P, L, P, F, F, F, F, P, F, P],

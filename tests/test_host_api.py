@@ -89,3 +89,24 @@ def test_engine_rejects_bad_shapes():
         UNetEngine.check_shape(torch.zeros(1, 2, 48, 48, 48))
     with pytest.raises(NotImplementedError):
         UNetEngine.check_shape(torch.zeros(1, 1, 8, 72, 72))
+
+
+def test_sliding_window_host_pieces(golden):
+    """importance map and window positions of the device sliding window == the reference's
+    (fixture from utils.py:142-173 run by the reference); CPU device fails loudly."""
+    import numpy as np
+    import torch
+    from light_unet import _native
+    from light_unet.utils import _get_gaussian_importance_map, sliding_window_inference_3d, window_positions
+    z = golden("sliding.npz")
+    np.testing.assert_array_equal(_get_gaussian_importance_map((48, 48, 48)), z["importance_48"])
+    assert window_positions(256, 48, 24) == list(range(0, 209, 24)) + [208]
+    assert window_positions(144, 48, 24) == [0, 24, 48, 72, 96]
+    assert window_positions(40, 48, 24) == [0]
+    assert window_positions(49, 48, 24) == [0, 1]
+    from light_unet.models.unet3d import Lightweight3DUNet
+    with pytest.raises(ValueError):
+        sliding_window_inference_3d(np.zeros((2, 3, 4, 5), np.float32), Lightweight3DUNet())
+    with pytest.raises(_native.NativeError):
+        sliding_window_inference_3d(np.zeros((48, 48, 48), np.float32), Lightweight3DUNet(),
+                                    device=torch.device("cpu"))

@@ -14,6 +14,7 @@ def _standin(tmp_path):
     (base / "models").mkdir(parents=True)
     (base / "core").mkdir()
     (base / "__init__.py").write_text("")
+    (base / "utils.py").write_text("def sliding_window_inference_3d(image, model):\n    return 'reference'\n")
     (base / "models" / "__init__.py").write_text(
         "from .unet3d import Lightweight3DUNet\nfrom .losses import FocalTverskyLoss, get_loss_function\n")
     (base / "models" / "unet3d.py").write_text("class Lightweight3DUNet:\n    origin = 'reference'\n")
@@ -24,7 +25,8 @@ def _standin(tmp_path):
     (base / "core" / "__init__.py").write_text("")
     (base / "core" / "trainer.py").write_text(
         "from light_unet.models.unet3d import Lightweight3DUNet\n"
-        "from light_unet.models.losses import get_loss_function\n")
+        "from light_unet.models.losses import get_loss_function\n"
+        "from light_unet.utils import sliding_window_inference_3d\n")
 
 
 def test_install_binds_model_and_loss(tmp_path):
@@ -40,6 +42,7 @@ def test_install_binds_model_and_loss(tmp_path):
         assert trainer.Lightweight3DUNet.__module__ == "l3u_amd.models.unet3d", trainer.Lightweight3DUNet
         assert trainer.get_loss_function.__module__ == "l3u_amd.models.losses"
         assert m.FocalTverskyLoss.__module__ == "l3u_amd.models.losses"
+        assert trainer.sliding_window_inference_3d.__module__ == "l3u_amd.utils"
         assert sys.modules["light_unet"].__file__.startswith({str(tmp_path)!r})
         net = trainer.Lightweight3DUNet()
         assert net.count_parameters()["total"] == 217228
