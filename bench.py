@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--ftl-mode", default="exact", choices=["exact", "local"])
     ap.add_argument("--no-sliding", action="store_true", help="skip the config-4 inference timing")
+    # multi-rank rehearsal on a one-GPU box: every rank on cuda:0, collectives over gloo
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--one-device", action="store_true")
     return ap.parse_args()
 
 
@@ -209,10 +212,14 @@ def main():
     if args.gpus > 1 and world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} needs torchrun with {args.gpus} processes "
                          f"(WORLD_SIZE={world})")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    dev_index = 0 if args.one_device else local
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":   # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
     enc = tuple(int(c) for c in args.enc.split(","))
 
     from light_unet import _native as nat
