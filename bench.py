@@ -71,6 +71,20 @@ def dw_bytes(N, C, S):
     return 4 * (3 * N * C * S) + 4 * 27 * C
 
 
+def pmc_traffic(N, C, size):
+    """Memory-side bytes per call of the dominant kernel from the committed rocprofv3 PMC passes
+    (tools/pmc.sh -> profiles/*_pmc_dw3_bwd.json), when they were taken at this exact shape."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_dw3_bwd.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        rec = json.load(f)
+    if f"[{N},{C},{size}^3]" not in rec.get("call", ""):
+        return None, None
+    return rec["traffic_bytes"], os.path.relpath(files[-1], ROOT) + " (FETCH_SIZE x2 + WRITE_SIZE)"
+
+
 class KernelTimer:
     """Captures the arguments of the C-ABI calls that make up the dominant operation (at their
     real shapes and buffers) during one eager step, then re-issues exactly those calls
@@ -289,6 +303,7 @@ def main():
         value = patches / elapsed
         dbytes = dw_bytes(N, cdom, S)
         achieved = dbytes / (dom_ms * 1e-3) / 1e9 if dom_ms else None
+        traffic, traffic_src = pmc_traffic(N, cdom, args.size)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -321,7 +336,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes": dbytes,
                 "avg_launch_ms": round(dom_ms, 5) if dom_ms else None,
             },
