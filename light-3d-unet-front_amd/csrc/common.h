@@ -42,6 +42,13 @@ L3U_DEV float swap_sum32(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+L3U_DEV float row_sum16(float v) {   // sum over the 16 lanes of a DPP row, in every lane
+  v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);   // row_half_mirror
+  v += dpp_f<0x140>(v);   // row_mirror
+  return v;
+}
 L3U_DEV float wave_sum(float v) {
   v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
   v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]

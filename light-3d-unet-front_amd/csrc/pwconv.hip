@@ -5,12 +5,14 @@
 // Replaces nn.Conv3d(Ci, Co, 1) of DepthwiseSeparableConv3d.pointwise (unet3d.py:18), the shortcut
 // conv (unet3d.py:70-73), and the GEMM part of nn.ConvTranspose3d(Ci, Ci/2, 2, 2) (unet3d.py:119).
 //
-// Register-direct operand mapping (no LDS round trip for the streamed operand): a lane loads one
-// float4 X[k0 + (l>>4)][s + 4(l&15) .. +3] (each k-row of the wave is 256 contiguous bytes) and
-// feeds component q to MFMA q, so MFMA q owns voxels {s + 4i + q}.  The accumulator row
-// i = 4(l>>4) + r of the four MFMAs then holds 4 CONSECUTIVE voxels per lane -> float4 stores.
-// The small weight operand is staged once per workgroup in LDS as Wt[k][j] (row stride padded to
-// 16 mod 32 floats: conflict-free ds_read_b32 for the 2x16-lane groups).
+// Register-direct operand mapping (no LDS round trip for the streamed operand): the weights are
+// the MFMA A operand (row i = output channel), X the B operand: a lane loads one float4
+// X[k0 + (l>>4)][s + 4(l&15) .. +3] (each k-row of the wave is 256 contiguous bytes) and feeds
+// component q to MFMA q, so MFMA q owns voxels {s + 4j + q}.  The accumulator of lane l then holds
+// channels 4(l>>4) + r and the 4 CONSECUTIVE voxels 4(l&15) .. +3: a store instruction writes
+// 64 consecutive voxels (256 B) per channel row.  Small K keeps the whole reduction in registers
+// (weights read from L1/L2); larger K stages the weights per workgroup in LDS as Wt[k][j] (row
+// stride padded to 16 mod 32 floats: conflict-free ds_read_b32 for the 2x16-lane groups).
 // The pw_fwd epilogue can also emit per-(n, j) InstanceNorm partials (count, mean, M2) of its
 // output tile (Chan merge later), so InstanceNorm statistics never re-read the activation.
 #include "common.h"
@@ -23,42 +25,42 @@ namespace {
 L3U_DEV f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
 // ConvTranspose3d(k=2, s=2) epilogue: GEMM row j = co*8 + (4a + 2b + c) of input voxel s lands at
-// out[co][2z+a][2y+b][2x+c] (+ bias[co]).  The lane's accumulator quad holds 4 consecutive input
-// voxels of one row j; its c-partner row j^1 sits in lane l^1 (same co, a, b, voxels), so one DPP
-// swap of two values gives each lane 4 CONTIGUOUS outputs [2x0 .. 2x0+3] (c = 0) or
-// [2x0+4 .. 2x0+7] (c = 1): one float4 store instead of 4 stride-2 scalar stores.  Requires W % 4
-// == 0 (VEC); otherwise per-voxel scalar stores.  Every lane of the wave must call it.
+// out[co][2z+a][2y+b][2x+c] (+ bias[co]).  A lane holds rows j0 (c = 0) and j0 + 1 (c = 1) of the
+// same 4 consecutive input voxels, i.e. 8 CONTIGUOUS outputs [2x0 .. 2x0+7]: two float4 stores.
+// Requires W % 4 == 0 (VEC); otherwise per-voxel scalar stores.
 template <bool VEC>
-L3U_DEV void d2s_store(float* outn, int j, int Nout, const float* __restrict__ bias, int s, f4 v,
-                       int S, int D, int H, int W) {
-  const bool ok = j < Nout;
-  const int co = j >> 3, a = (j >> 2) & 1, bq = (j >> 1) & 1, c = j & 1;
+L3U_DEV void d2s_store2(float* outn, int j0, int Nout, const float* __restrict__ bias, int s, f4 v0,
+                        f4 v1, int S, int D, int H, int W) {
+  const bool ok = j0 < Nout;
+  const int co = j0 >> 3, a = (j0 >> 2) & 1, bq = (j0 >> 1) & 1;
   const float bv = (bias && ok) ? bias[co] : 0.f;
-  v += bv;
-  const long long So = 8ll * S;
-  float* oc = outn + (long long)co * So;
+  v0 += bv;
+  v1 += bv;
+  float* oc = outn + (long long)co * (8ll * S);
   if (VEC) {
-    const float s0 = c ? v[0] : v[2], s1 = c ? v[1] : v[3];
-    const float r0 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s0), 0xB1, 0xf, 0xf, false));
-    const float r1 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s1), 0xB1, 0xf, 0xf, false));
-    const f4 o = c ? f4{r0, v[2], r1, v[3]} : f4{v[0], r0, v[1], r1};
     if (ok && s < S) {
       const int x = s % W, t = s / W, y = t % H, z = t / H;
-      float* dst = oc + ((long long)(2 * z + a) * (2 * H) + (2 * y + bq)) * (2 * W) + 2 * x + (c ? 4 : 0);
-      *reinterpret_cast<f4*>(dst) = o;
+      float* dst = oc + ((long long)(2 * z + a) * (2 * H) + (2 * y + bq)) * (2 * W) + 2 * x;
+      *reinterpret_cast<f4*>(dst) = f4{v0[0], v1[0], v0[1], v1[1]};
+      *reinterpret_cast<f4*>(dst + 4) = f4{v0[2], v1[2], v0[3], v1[3]};
     }
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (ok && s + q < S) {
         const int x = (s + q) % W, t = (s + q) / W, y = t % H, z = t / H;
-        oc[((long long)(2 * z + a) * (2 * H) + (2 * y + bq)) * (2 * W) + 2 * x + c] = v[q];
+        float* dst = oc + ((long long)(2 * z + a) * (2 * H) + (2 * y + bq)) * (2 * W) + 2 * x;
+        dst[0] = v0[q];
+        dst[1] = v1[q];
       }
     }
   }
 }
 
-template <int NC, int NSW, bool VEC, bool D2S>
+// KS > 0: the whole reduction (K <= 4*KS) in registers, X and weight loads (weights straight
+// from L1/L2, no LDS staging barrier) all issued before the first MFMA; KS = 0: generic K loop
+// with the weights staged through LDS in chunks of 128 reduction rows.
+template <int NC, int NSW, bool VEC, bool D2S, int KS>
 __global__ __launch_bounds__(256) void pw_fwd_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
     const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
@@ -83,6 +85,42 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[j][m][q] = f4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (KS > 0) {
+    f4 a[KS][NSW];
+    float b[KS][NC];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int kk = 4 * ks + lk;
+#pragma unroll
+      for (int j = 0; j < NSW; ++j) {
+        const int s = sbase + j * 64 + 4 * lr;
+        a[ks][j] = f4{0.f, 0.f, 0.f, 0.f};
+        if (kk < K) {
+          const float* src = xn + (long long)kk * S + s;
+          if (VEC) {
+            if (s < S) a[ks][j] = *reinterpret_cast<const f4*>(src);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (s + q < S) a[ks][j][q] = src[q];
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < NC; ++m) {
+        const int co = co0 + 16 * m + lr;
+        b[ks][m] = (kk < K && co < Nout) ? (wl == 0 ? w[(long long)co * K + kk] : w[(long long)kk * Nout + co]) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < NSW; ++j)
+#pragma unroll
+        for (int m = 0; m < NC; ++m)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[j][m][q] = mfma4(b[ks][m], a[ks][j][q], acc[j][m][q]);
+  } else {
   // the weight operand is staged through LDS in chunks of KCH reduction rows
   for (int kc0 = 0; kc0 < Kp; kc0 += KCH) {
   const int kc1 = min(Kp, kc0 + KCH);
@@ -121,11 +159,13 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
 #pragma unroll
       for (int m = 0; m < NC; ++m)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[j][m][q] = mfma4(a[j][q], b[m], acc[j][m][q]);
+        for (int q = 0; q < 4; ++q) acc[j][m][q] = mfma4(b[m], a[j][q], acc[j][m][q]);
+  }
   }
   }
 
-  // epilogue: bias, accumulate, store, InstanceNorm partials
+  // epilogue: lane (lr, lk) holds Y[co0 + 16m + 4lk + r][sbase + 64j + 4lr + q]: per (m, r) the
+  // 16 lanes of a row store 64 consecutive voxels of one channel (256 B, coalesced)
   float* yn = y + (long long)n * yns;
   if (D2S) {
 #pragma unroll
@@ -133,25 +173,26 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
 #pragma unroll
       for (int j = 0; j < NSW; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          d2s_store<VEC>(yn, co0 + 16 * m + lr, Nout, bias, sbase + j * 64 + 16 * lk + 4 * r,
-                         f4{acc[j][m][0][r], acc[j][m][1][r], acc[j][m][2][r], acc[j][m][3][r]},
-                         S, Dq, Hq, Wq);
+        for (int rp = 0; rp < 4; rp += 2)
+          d2s_store2<VEC>(yn, co0 + 16 * m + 4 * lk + rp, Nout, bias, sbase + j * 64 + 4 * lr,
+                          f4{acc[j][m][0][rp], acc[j][m][1][rp], acc[j][m][2][rp], acc[j][m][3][rp]},
+                          f4{acc[j][m][0][rp + 1], acc[j][m][1][rp + 1], acc[j][m][2][rp + 1],
+                             acc[j][m][3][rp + 1]},
+                          S, Dq, Hq, Wq);
     return;
   }
-  float lsum[NC];
+  float lsum[NC][4];
 #pragma unroll
-  for (int m = 0; m < NC; ++m) lsum[m] = 0.f;
+  for (int m = 0; m < NC; ++m)
 #pragma unroll
-  for (int m = 0; m < NC; ++m) {
-    const int co = co0 + 16 * m + lr;
-    const bool cok = co < Nout;
-    const float bv = (bias && cok) ? bias[co] : 0.f;
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + 16 * m + 4 * lk + r;
+      const bool cok = co < Nout;
+      const float bv = (bias && cok) ? bias[co] : 0.f;
+      lsum[m][r] = 0.f;
 #pragma unroll
-    for (int j = 0; j < NSW; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int s = sbase + j * 64 + 16 * lk + 4 * r;
+      for (int j = 0; j < NSW; ++j) {
+        const int s = sbase + j * 64 + 4 * lr;
         f4 v = f4{acc[j][m][0][r], acc[j][m][1][r], acc[j][m][2][r], acc[j][m][3][r]} + bv;
         float* dst = yn + (long long)co * S + s;
         if (cok) {
@@ -172,63 +213,67 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           acc[j][m][q][r] = v[q];                       // keep the stored value for the stats
-          if (s + q < S) lsum[m] += v[q];
+          if (s + q < S) lsum[m][r] += v[q];
         }
       }
-  }
+    }
   if (stat_part == nullptr) return;
-  // per-channel block statistics (two-pass within the tile: mean, then M2 about that mean)
+  // per-channel block statistics (two-pass within the tile: mean, then M2 about that mean):
+  // row sums over the 16 voxel lanes by DPP, then the 4 waves through LDS in fixed order
   float* red = lds;                                     // [4][CO_BLK] (weights no longer needed)
   const int s_lo = sb * TSB;
   const int cnt = min(TSB, S - s_lo);
   __syncthreads();
 #pragma unroll
-  for (int m = 0; m < NC; ++m) {
-    float v = lsum[m];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (lk == 0) red[wave * CO_BLK + 16 * m + lr] = v;
-  }
+  for (int m = 0; m < NC; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = row_sum16(lsum[m][r]);
+      if (lr == 0) red[wave * CO_BLK + 16 * m + 4 * lk + r] = v;
+    }
   __syncthreads();
-  float mean[NC];
+  float mean[NC][4];
 #pragma unroll
-  for (int m = 0; m < NC; ++m) {
-    const int jj = 16 * m + lr;
-    mean[m] = ((red[jj] + red[CO_BLK + jj]) + (red[2 * CO_BLK + jj] + red[3 * CO_BLK + jj])) / (float)cnt;
-  }
+  for (int m = 0; m < NC; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int jj = 16 * m + 4 * lk + r;
+      mean[m][r] = ((red[jj] + red[CO_BLK + jj]) + (red[2 * CO_BLK + jj] + red[3 * CO_BLK + jj])) / (float)cnt;
+    }
   __syncthreads();
 #pragma unroll
-  for (int m = 0; m < NC; ++m) {
-    float v = 0.f;
+  for (int m = 0; m < NC; ++m)
 #pragma unroll
-    for (int j = 0; j < NSW; ++j)
+    for (int r = 0; r < 4; ++r) {
+      float v = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int s = sbase + j * 64 + 16 * lk + 4 * r;
+      for (int j = 0; j < NSW; ++j) {
+        const int s = sbase + j * 64 + 4 * lr;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (s + q < S) {
-            const float d = acc[j][m][q][r] - mean[m];
+            const float d = acc[j][m][q][r] - mean[m][r];
             v = fmaf(d, d, v);
           }
       }
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (lk == 0) red[wave * CO_BLK + 16 * m + lr] = v;
-  }
-  __syncthreads();
-  if (wave == 0 && lk == 0) {
-#pragma unroll
-    for (int m = 0; m < NC; ++m) {
-      const int jj = 16 * m + lr, co = co0 + jj;
-      if (co < Nout) {
-        const float m2 = (red[jj] + red[CO_BLK + jj]) + (red[2 * CO_BLK + jj] + red[3 * CO_BLK + jj]);
-        float* o = stat_part + (((long long)n * Nout + co) * nsb + sb) * 3;
-        o[0] = (float)cnt;
-        o[1] = mean[m];
-        o[2] = m2;
-      }
+      v = row_sum16(v);
+      if (lr == 0) red[wave * CO_BLK + 16 * m + 4 * lk + r] = v;
     }
+  __syncthreads();
+  if (wave == 0 && lr == 0) {
+#pragma unroll
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int jj = 16 * m + 4 * lk + r, co = co0 + jj;
+        if (co < Nout) {
+          const float m2 = (red[jj] + red[CO_BLK + jj]) + (red[2 * CO_BLK + jj] + red[3 * CO_BLK + jj]);
+          float* o = stat_part + (((long long)n * Nout + co) * nsb + sb) * 3;
+          o[0] = (float)cnt;
+          o[1] = mean[m][r];
+          o[2] = m2;
+        }
+      }
   }
 }
 
@@ -274,7 +319,7 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
       float b = 0.f;
       if (kk < K && co < Nout) b = wl == 0 ? w[(long long)co * K + kk] : w[(long long)kk * Nout + co];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[m][q] = mfma4(a[q], b, acc[m][q]);
+      for (int q = 0; q < 4; ++q) acc[m][q] = mfma4(b, a[q], acc[m][q]);
     }
   }
   // cross-wave combine through LDS, value-major ([wave][value][lane]: consecutive lanes hit
@@ -302,23 +347,23 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
       t4[q][r] = ((src[0] + src[T * 64]) + src[2 * T * 64]) + src[3 * T * 64];
     }
   }
-  // epilogue: lane holds Y[co0+16m+lr][sb*64 + 16lk + 4r + q]
+  // epilogue: lane (lr, lk) holds Y[co0 + 16m + 4lk + r][sb*64 + 4lr + q]
   float* yn = y + (long long)n * yns;
+  const int sv = sb * 64 + 4 * lr;
   if (D2S) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      d2s_store<VEC>(yn, co0 + 16 * m + lr, Nout, bias, sb * 64 + 16 * lk + 4 * r,
-                     f4{t4[0][r], t4[1][r], t4[2][r], t4[3][r]}, S, Dq, Hq, Wq);
+    for (int rp = 0; rp < 4; rp += 2)
+      d2s_store2<VEC>(yn, co0 + 16 * m + 4 * lk + rp, Nout, bias, sv,
+                      f4{t4[0][rp], t4[1][rp], t4[2][rp], t4[3][rp]},
+                      f4{t4[0][rp + 1], t4[1][rp + 1], t4[2][rp + 1], t4[3][rp + 1]}, S, Dq, Hq, Wq);
     return;
   }
   const int cnt = min(64, S - sb * 64);
-  const int co = co0 + 16 * m + lr;
-  const bool cok = co < Nout;
-  const float bv = (bias && cok) ? bias[co] : 0.f;
-  float lsum = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int sv = sb * 64 + 16 * lk + 4 * r;
+    const int co = co0 + 16 * m + 4 * lk + r;
+    const bool cok = co < Nout;
+    const float bv = (bias && cok) ? bias[co] : 0.f;
     f4 v = f4{t4[0][r], t4[1][r], t4[2][r], t4[3][r]} + bv;
     float* dst = yn + (long long)co * S + sv;
     if (cok) {
@@ -336,34 +381,26 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
           }
       }
     }
+    if (stat_part != nullptr) {
+      float ls = 0.f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      t4[q][r] = v[q];
-      if (sv + q < S) lsum += v[q];
-    }
-  }
-  if (stat_part != nullptr) {
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-    const float mean = lsum / (float)cnt;
-    float m2 = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int sv = sb * 64 + 16 * lk + 4 * r;
+      for (int q = 0; q < 4; ++q)
+        if (sv + q < S) ls += v[q];
+      const float mean = row_sum16(ls) / (float)cnt;
+      float m2 = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         if (sv + q < S) {
-          const float d = t4[q][r] - mean;
+          const float d = v[q] - mean;
           m2 = fmaf(d, d, m2);
         }
-    }
-    m2 += __shfl_xor(m2, 16, 64);
-    m2 += __shfl_xor(m2, 32, 64);
-    if (lk == 0 && cok) {
-      float* o = stat_part + (((long long)n * Nout + co) * nsb + sb) * 3;
-      o[0] = (float)cnt;
-      o[1] = mean;
-      o[2] = m2;
+      m2 = row_sum16(m2);
+      if (lr == 0 && cok) {
+        float* o = stat_part + (((long long)n * Nout + co) * nsb + sb) * 3;
+        o[0] = (float)cnt;
+        o[1] = mean;
+        o[2] = m2;
+      }
     }
   }
 }
@@ -520,15 +557,20 @@ int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout,
   if (lds < 4 * CO_BLK * sizeof(float)) lds = 4 * CO_BLK * sizeof(float);
   L3U_REQUIRE(lds <= 160 * 1024);
   dim3 grid(nsb, (Nout + CO_BLK - 1) / CO_BLK, N), block(256);
-#define PWF(NC_, NSW_, V_, D_) hipLaunchKernelGGL((pw_fwd_kernel<NC_, NSW_, V_, D_>), grid, block, lds, \
+  L3U_REQUIRE(NSW == 1);
+  const int KSn = K <= 16 ? 4 : (K <= 32 ? 8 : (K <= 64 ? 16 : 0));
+#define PWF(NC_, V_, D_, KS_) hipLaunchKernelGGL((pw_fwd_kernel<NC_, 1, V_, D_, KS_>), grid, block, lds, \
       stream, x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, \
       Dq, Hq, Wq)
-#define PWF_V(NC_, NSW_) do { if (d2s) { if (vec) PWF(NC_, NSW_, true, true); else PWF(NC_, NSW_, false, true); } \
-                              else { if (vec) PWF(NC_, NSW_, true, false); else PWF(NC_, NSW_, false, false); } } while (0)
-  if (NC == 1) { if (NSW == 4) PWF_V(1, 4); else if (NSW == 2) PWF_V(1, 2); else PWF_V(1, 1); }
-  else if (NC == 2) { if (NSW == 2) PWF_V(2, 2); else PWF_V(2, 1); }
-  else PWF_V(4, 1);
+#define PWF_K(NC_, V_, D_) do { if (KSn == 4) PWF(NC_, V_, D_, 4); else if (KSn == 8) PWF(NC_, V_, D_, 8); \
+                                else if (KSn == 16) PWF(NC_, V_, D_, 16); else PWF(NC_, V_, D_, 0); } while (0)
+#define PWF_V(NC_) do { if (d2s) { if (vec) PWF_K(NC_, true, true); else PWF_K(NC_, false, true); } \
+                        else { if (vec) PWF_K(NC_, true, false); else PWF_K(NC_, false, false); } } while (0)
+  if (NC == 1) PWF_V(1);
+  else if (NC == 2) PWF_V(2);
+  else PWF_V(4);
 #undef PWF_V
+#undef PWF_K
 #undef PWF
   L3U_CHECK_LAUNCH();
 }
