@@ -850,6 +850,153 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ?
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Whole-volume variants for small planes/volumes (the 12^3 and 6^3 levels): one workgroup per
+// (n, c) holds the whole zero-padded volume [(D+2)(H+2)(W+2)] in LDS and each thread computes
+// voxels v = tid, tid + 256, ... with all 27 taps read straight from LDS.  One load phase and
+// one barrier instead of a chain of plane steps: these volumes are latency-, not
+// bandwidth-bound.  nchunk = 1 (one partial per (n, c)).
+// ------------------------------------------------------------------------------------------------
+#ifndef L3U_VOL_MAX
+#define L3U_VOL_MAX 600   // measured: the 6^3 level gains, at 12^3 the plane kernels are faster
+#endif
+bool use_volume(int D, int H, int W) { return (long long)(D + 2) * (H + 2) * (W + 2) <= L3U_VOL_MAX; }
+
+// load volume `src` (transformed if XF) into the padded LDS image; the halo is zero
+template <bool XF>
+L3U_DEV void v_load(float* L, const float* __restrict__ src, int D, int H, int W, float sc, float mu,
+                    float sh) {
+  const int PW = W + 2, PH = H + 2, PV = (D + 2) * PH * PW;
+  for (int i = threadIdx.x; i < PV; i += blockDim.x) {
+    const int x = i % PW - 1, t = i / PW, y = t % PH - 1, z = t / PH - 1;
+    float v = 0.f;
+    if (x >= 0 && x < W && y >= 0 && y < H && z >= 0 && z < D) {
+      v = src[((long long)z * H + y) * W + x];
+      if (XF) v = lrelu(fmaf(sc, v - mu, sh));
+    }
+    L[i] = v;
+  }
+}
+
+// y = conv(x) (EPI 0, taps as given) or the data gradient (EPI 1: dpre epilogue + IN sums,
+// 2: y += conv^T, 3: y = conv^T; flipped taps), one (n, c) per workgroup
+template <int XF, int EPI>
+__global__ __launch_bounds__(256) void dwv_fwd_kernel(
+    const float* __restrict__ x, long long xns, const float* __restrict__ w,
+    const float* __restrict__ rec, l3u_norm_src src, int has_src, float* __restrict__ y,
+    long long yns, const float* __restrict__ ep, long long epns, double* __restrict__ in_part,
+    int N, int C, int D, int H, int W) {
+  constexpr bool FLIP = EPI != 0;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int nc = blockIdx.x, c = nc % C, n = nc / C;
+  const long long HW = (long long)H * W, S = D * HW, cofs = (long long)c * S;
+  float wk[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t) wk[t] = w[c * 27 + (FLIP ? 26 - t : t)];
+  float sc = 1.f, sh = 0.f, mu = 0.f, rstd = 1.f, kk = 1.f;
+  if (XF || EPI == 1) {
+    if (has_src) {
+      float* s8 = lds;
+      block_record(src, n, c, C, true, s8);
+      mu = s8[0]; rstd = s8[1]; sc = s8[2]; sh = s8[3]; kk = s8[4];
+      __syncthreads();
+    } else {
+      const float* r = rec + (long long)nc * kRec;
+      mu = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];
+    }
+  }
+  v_load<XF == 1>(lds, x + (long long)n * xns + cofs, D, H, W, sc, mu, sh);
+  __syncthreads();
+  const int PW = W + 2, PHW = (H + 2) * PW;
+  float* yp = y + (long long)n * yns + cofs;
+  const float* epp = (EPI == 1 || EPI == 2) ? ep + (long long)n * epns + cofs : nullptr;
+  float s1 = 0.f, s2 = 0.f;
+  for (int v = threadIdx.x; v < S; v += blockDim.x) {
+    const int xx = v % W, t = v / W, yy = t % H, zz = t / H;
+    const float* b = lds + zz * PHW + yy * PW + xx;   // corner of the 3x3x3 neighbourhood
+    float o = 0.f;
+#pragma unroll
+    for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) o = fmaf(wk[dz * 9 + dy * 3 + dx], b[dz * PHW + dy * PW + dx], o);
+    if (EPI == 1) {
+      const float e = epp[v];
+      const float pre = fmaf(sc, e - mu, sh);
+      o = o * kk * lrelu_d(pre);
+      s1 += o;
+      s2 += o * ((e - mu) * rstd);
+    } else if (EPI == 2) {
+      o += epp[v];
+    }
+    yp[v] = o;
+  }
+  if (EPI == 1) {
+    __syncthreads();
+    double* redd = reinterpret_cast<double*>(lds);
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const double r1 = wave_sum_d((double)s1), r2 = wave_sum_d((double)s2);
+    if (ln == 0) { redd[wv * 2] = r1; redd[wv * 2 + 1] = r2; }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      double r = 0.0;
+      for (int k = 0; k < nw; ++k) r += redd[k * 2 + threadIdx.x];
+      in_part[((long long)c * N + n) * 2 + threadIdx.x] = r;
+    }
+  }
+}
+
+// dw_part[c][n][27] = sum_v dZ(v) * A(v + tap), A = x (XF 0) or lrelu(IN(x)) (XF 1)
+template <int XF>
+__global__ __launch_bounds__(256) void dwv_dw_kernel(
+    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
+    const float* __restrict__ rec, float* __restrict__ dw_part, int N, int C, int D, int H, int W) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int nc = blockIdx.x, c = nc % C, n = nc / C;
+  const long long HW = (long long)H * W, S = D * HW, cofs = (long long)c * S;
+  float sc = 1.f, sh = 0.f, mu = 0.f;
+  if (XF) {
+    const float* r = rec + (long long)nc * kRec;
+    mu = r[0]; sc = r[2]; sh = r[3];
+  }
+  v_load<XF == 1>(lds, x + (long long)n * xns + cofs, D, H, W, sc, mu, sh);
+  __syncthreads();
+  const int PW = W + 2, PHW = (H + 2) * PW;
+  const float* dzp = dz + (long long)n * dzns + cofs;
+  float gw[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t) gw[t] = 0.f;
+  for (int v = threadIdx.x; v < S; v += blockDim.x) {
+    const int xx = v % W, t = v / W, yy = t % H, zz = t / H;
+    const float* b = lds + zz * PHW + yy * PW + xx;
+    const float g = dzp[v];
+#pragma unroll
+    for (int dz2 = 0; dz2 < 3; ++dz2)
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int tp = dz2 * 9 + dy * 3 + dx;
+          gw[tp] = fmaf(g, b[dz2 * PHW + dy * PW + dx], gw[tp]);
+        }
+  }
+  __syncthreads();
+  float* red = lds;   // [4 waves][32]
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int t = 0; t < 27; ++t) {
+    const float r = wave_sum(gw[t]);
+    if (ln == 0) red[wv * 32 + t] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    float r = 0.f;
+    for (int k = 0; k < nw; ++k) r += red[k * 32 + threadIdx.x];
+    dw_part[((long long)c * N + n) * 27 + threadIdx.x] = r;
+  }
+}
+
 }  // namespace
 
 #define DW_DISPATCH_P(KERNEL, MODE, ...)                                               \
@@ -867,6 +1014,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ?
 extern "C" {
 
 int l3u_dw3_nchunk(int N, int C, int D, int H, int W) {
+  if (use_volume(D, H, W)) return 1;
   if (use_quads(H, W)) {
     const QGeom g = qgeom(N, C, D, H, W);
     return g.nz * g.ny;
@@ -882,6 +1030,13 @@ int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float
   const l3u_norm_src s = src ? *src : z;
   const int has = src ? 1 : 0;
   const bool xf = rec != nullptr || src != nullptr;
+  if (use_volume(D, H, W)) {
+    size_t lds = (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
+    if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);
+    if (xf) hipLaunchKernelGGL((dwv_fwd_kernel<1, 0>), dim3(N * C), dim3(256), lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W);
+    else hipLaunchKernelGGL((dwv_fwd_kernel<0, 0>), dim3(N * C), dim3(256), lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W);
+    L3U_CHECK_LAUNCH();
+  }
   if (use_quads(H, W) && x_nstride % 4 == 0 && y_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
     size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
@@ -919,6 +1074,25 @@ int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long l
   L3U_REQUIRE(!(parts & 2) || dw_part != nullptr);
   L3U_REQUIRE(!(parts & 1) || rec == nullptr || in_part != nullptr);
   L3U_REQUIRE(rec == nullptr || accumulate == 0);
+  if (use_volume(D, H, W)) {
+    size_t lds = (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
+    if (lds < 128 * sizeof(float)) lds = 128 * sizeof(float);
+    if (parts & 1) {
+      const l3u_norm_src z{};
+#define DWVX(E_) hipLaunchKernelGGL((dwv_fwd_kernel<0, E_>), dim3(N * C), dim3(256), lds, stream, dz, \
+      dz_nstride, w, rec, z, 0, dx, dx_nstride, (E_ == 1 ? x : dx), (E_ == 1 ? x_nstride : dx_nstride), \
+      in_part, N, C, D, H, W)
+      if (rec) DWVX(1);
+      else if (accumulate) DWVX(2);
+      else DWVX(3);
+#undef DWVX
+    }
+    if (parts & 2) {
+      if (rec) hipLaunchKernelGGL((dwv_dw_kernel<1>), dim3(N * C), dim3(256), lds, stream, dz, dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W);
+      else hipLaunchKernelGGL((dwv_dw_kernel<0>), dim3(N * C), dim3(256), lds, stream, dz, dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W);
+    }
+    L3U_CHECK_LAUNCH();
+  }
   if (use_quads(H, W) && x_nstride % 4 == 0 && dz_nstride % 4 == 0 && dx_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
