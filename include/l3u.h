@@ -152,6 +152,14 @@ int l3u_convt_d2s(const float* yp, const float* bias, float* out, long long out_
 int l3u_convt_fwd(const float* x, long long x_nstride, const float* w, const float* bias,
                   float* out, long long out_nstride, int N, int Ci, int Co, int D, int H, int W,
                   hipStream_t stream);
+/* the whole backward reading dY in place from the up-sampled gradient (no space-to-depth copy):
+ * dx = the data-gradient GEMM with its X operand gathered from dy; wpart[l3u_pw_bwd_weight_nparts
+ * (N, D*H*W)][Ci][Co*8] weight partials; bpart[Co][N][l3u_chan_sum_nblocks(8*D*H*W)] (fp64) bias
+ * partials (dy: [N][Co][2D][2H][2W] with batch stride dy_nstride, e.g. the lower half of the
+ * decoder's concat gradient)                                                                   */
+int l3u_convt_bwd(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
+                  const float* w, float* dx, long long dx_nstride, float* wpart, double* bpart,
+                  int N, int Ci, int Co, int D, int H, int W, hipStream_t stream);
 int l3u_convt_s2d(const float* dy, long long dy_nstride, float* dyp, int N, int Co, int D, int H,
                   int W, hipStream_t stream);
 /* per-channel sums part[C][N][nblocks] (fp64; bias gradients)                                */

@@ -24,6 +24,48 @@ namespace {
 
 L3U_DEV f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
+// The streamed operand X[k][s .. s+3] (4 voxels, zero past S / past row K).  GATHER: X is the
+// ConvTranspose3d(k2, s2) gradient read in place from the up-sampled tensor (its backward without
+// a space-to-depth copy): row k = co*8 + (4a + 2b + c) at input voxel (z, y, x) is
+// src[co][2z+a][2y+b][2x+c], channel stride 8S, dims (Dq, Hq, Wq) = the input (low-res) volume.
+// With W % 4 == 0 the 4 voxels share an output row: two float4 loads of 8 consecutive floats and
+// an even/odd pick.
+template <bool VEC, bool GATHER>
+L3U_DEV f4 load_x4(const float* __restrict__ xn, int kk, int K, int s, int lim, int S, int Hq,
+                   int Wq) {   // voxels >= lim (<= S) read as zero
+  f4 a = {0.f, 0.f, 0.f, 0.f};
+  if (kk >= K) return a;
+  if (GATHER) {
+    const int a_ = (kk >> 2) & 1, b_ = (kk >> 1) & 1, c_ = kk & 1;
+    const float* base = xn + (long long)(kk >> 3) * (8ll * S);
+    if (VEC) {
+      if (s < lim) {
+        const int x = s % Wq, t = s / Wq, y = t % Hq, z = t / Hq;
+        const float* p = base + ((long long)(2 * z + a_) * (2 * Hq) + (2 * y + b_)) * (2 * Wq) + 2 * x;
+        const f4 lo = *reinterpret_cast<const f4*>(p), hi = *reinterpret_cast<const f4*>(p + 4);
+        a = c_ ? f4{lo[1], lo[3], hi[1], hi[3]} : f4{lo[0], lo[2], hi[0], hi[2]};
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (s + q < lim) {
+          const int x = (s + q) % Wq, t = (s + q) / Wq, y = t % Hq, z = t / Hq;
+          a[q] = base[((long long)(2 * z + a_) * (2 * Hq) + (2 * y + b_)) * (2 * Wq) + 2 * x + c_];
+        }
+    }
+    return a;
+  }
+  const float* src = xn + (long long)kk * S + s;
+  if (VEC) {
+    if (s < lim) a = *reinterpret_cast<const f4*>(src);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (s + q < lim) a[q] = src[q];
+  }
+  return a;
+}
+
 // ConvTranspose3d(k=2, s=2) epilogue: GEMM row j = co*8 + (4a + 2b + c) of input voxel s lands at
 // out[co][2z+a][2y+b][2x+c] (+ bias[co]).  A lane holds rows j0 (c = 0) and j0 + 1 (c = 1) of the
 // same 4 consecutive input voxels, i.e. 8 CONTIGUOUS outputs [2x0 .. 2x0+7]: two float4 stores.
@@ -60,7 +102,7 @@ L3U_DEV void d2s_store2(float* outn, int j0, int Nout, const float* __restrict__
 // KS > 0: the whole reduction (K <= 4*KS) in registers, X and weight loads (weights straight
 // from L1/L2, no LDS staging barrier) all issued before the first MFMA; KS = 0: generic K loop
 // with the weights staged through LDS in chunks of 128 reduction rows.
-template <int NC, int NSW, bool VEC, bool D2S, int KS>
+template <int NC, int NSW, bool VEC, int XM, int KS>   // XM: 0 plain, 1 scatter epilogue, 2 gathered X
 __global__ __launch_bounds__(256) void pw_fwd_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
     const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
@@ -93,18 +135,7 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
       const int kk = 4 * ks + lk;
 #pragma unroll
       for (int j = 0; j < NSW; ++j) {
-        const int s = sbase + j * 64 + 4 * lr;
-        a[ks][j] = f4{0.f, 0.f, 0.f, 0.f};
-        if (kk < K) {
-          const float* src = xn + (long long)kk * S + s;
-          if (VEC) {
-            if (s < S) a[ks][j] = *reinterpret_cast<const f4*>(src);
-          } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (s + q < S) a[ks][j][q] = src[q];
-          }
-        }
+        a[ks][j] = load_x4<VEC, XM == 2>(xn, kk, K, sbase + j * 64 + 4 * lr, S, S, Hq, Wq);
       }
 #pragma unroll
       for (int m = 0; m < NC; ++m) {
@@ -138,18 +169,7 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
     f4 a[NSW];
 #pragma unroll
     for (int j = 0; j < NSW; ++j) {
-      const int s = sbase + j * 64 + 4 * lr;
-      a[j] = f4{0.f, 0.f, 0.f, 0.f};
-      if (kk < K) {
-        const float* src = xn + (long long)kk * S + s;
-        if (VEC) {
-          if (s < S) a[j] = *reinterpret_cast<const f4*>(src);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (s + q < S) a[j][q] = src[q];
-        }
-      }
+      a[j] = load_x4<VEC, XM == 2>(xn, kk, K, sbase + j * 64 + 4 * lr, S, S, Hq, Wq);
     }
     float b[NC];
 #pragma unroll
@@ -167,7 +187,7 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
   // epilogue: lane (lr, lk) holds Y[co0 + 16m + 4lk + r][sbase + 64j + 4lr + q]: per (m, r) the
   // 16 lanes of a row store 64 consecutive voxels of one channel (256 B, coalesced)
   float* yn = y + (long long)n * yns;
-  if (D2S) {
+  if (XM == 1) {
 #pragma unroll
     for (int m = 0; m < NC; ++m)
 #pragma unroll
@@ -281,7 +301,7 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
 // share ONE 64-voxel tile and split the reduction dimension K (k-steps interleaved by wave), then
 // combine through LDS in a fixed order; weights are read straight from L2 (they are tiny and
 // every workgroup re-reads them).  This turns an 8-workgroup grid into hundreds.
-template <int NC, bool VEC, bool D2S>
+template <int NC, bool VEC, int XM>
 __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
     const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
@@ -302,17 +322,7 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
 #pragma unroll 4
   for (int ks = wave; ks < ksteps; ks += 4) {
     const int kk = 4 * ks + lk;
-    f4 a = {0.f, 0.f, 0.f, 0.f};
-    if (kk < K) {
-      const float* src = xn + (long long)kk * S + s;
-      if (VEC) {
-        if (s < S) a = *reinterpret_cast<const f4*>(src);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (s + q < S) a[q] = src[q];
-      }
-    }
+    const f4 a = load_x4<VEC, XM == 2>(xn, kk, K, s, S, S, Hq, Wq);
 #pragma unroll
     for (int m = 0; m < NC; ++m) {
       const int co = co0 + 16 * m + lr;
@@ -350,7 +360,7 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
   // epilogue: lane (lr, lk) holds Y[co0 + 16m + 4lk + r][sb*64 + 4lr + q]
   float* yn = y + (long long)n * yns;
   const int sv = sb * 64 + 4 * lr;
-  if (D2S) {
+  if (XM == 1) {
 #pragma unroll
     for (int rp = 0; rp < 4; rp += 2)
       d2s_store2<VEC>(yn, co0 + 16 * m + 4 * lk + rp, Nout, bias, sv,
@@ -408,10 +418,10 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
 // dW[j][k] partial over one voxel chunk of one sample.  A = dY (rows j), B = X^T (cols k),
 // the MFMA k-dimension is the voxel: lane l loads float4 dY[j0+16mo+(l&15)][s+4(l>>4)..+3] and
 // X[k0+16mi+(l&15)][s+4(l>>4)..+3]; component q feeds MFMA q.
-template <int NJ, int NK, bool VEC>
+template <int NJ, int NK, bool VEC, bool GATHER>
 __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
     const float* __restrict__ dy, long long dyns, const float* __restrict__ x, long long xns,
-    float* __restrict__ part, int J, int K, int S, int SCH, int nsc) {
+    float* __restrict__ part, int J, int K, int S, int SCH, int nsc, int Hq, int Wq) {
   constexpr int TJ = 16 * NJ, TK = 16 * NK;
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [64][T]
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
@@ -448,20 +458,8 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
       }
     }
 #pragma unroll
-    for (int b = 0; b < NK; ++b) {
-      const int kk = k0 + 16 * b + lr;
-      bv[b] = f4{0.f, 0.f, 0.f, 0.f};
-      if (kk < K) {
-        const float* src = xn + (long long)kk * S + sl;
-        if (VEC) {
-          if (sl < s_hi) bv[b] = *reinterpret_cast<const f4*>(src);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (sl + q < s_hi) bv[b][q] = src[q];
-        }
-      }
-    }
+    for (int b = 0; b < NK; ++b)
+      bv[b] = load_x4<VEC, GATHER>(xn, k0 + 16 * b + lr, K, sl, s_hi, S, Hq, Wq);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -526,10 +524,12 @@ namespace {
 
 int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout, const float* bias,
               float* y, long long y_nstride, int accumulate, float* stat_part, int N, int K,
-              int Nout, int S, bool d2s, int Dq, int Hq, int Wq, hipStream_t stream) {
+              int Nout, int S, int xm, int Dq, int Hq, int Wq, hipStream_t stream) {
+  // xm: 0 plain GEMM, 1 ConvTranspose3d scatter epilogue, 2 X gathered from the up-sampled
+  // ConvTranspose3d gradient; (Dq, Hq, Wq) = the low-resolution volume for xm != 0
   L3U_REQUIRE(N > 0 && K > 0 && Nout > 0 && S > 0);
   const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (y_nstride % 4 == 0) &&
-                   (!d2s || Wq % 4 == 0);
+                   (xm == 0 || Wq % 4 == 0);
   if (pw_use_ks(S, K)) {
     // co tile: as wide as possible while keeping >= 256 workgroups
     const int nsb = (S + 63) / 64;
@@ -537,14 +537,15 @@ int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout,
     while (NC > 1 && (long long)nsb * ((Nout + 16 * NC - 1) / (16 * NC)) * N < 256) NC >>= 1;
     const size_t lds = 4 * 64 * (size_t)NC * 16 * sizeof(float);
     dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), N), block(256);
-#define PWK(NC_, V_, D_) hipLaunchKernelGGL((pw_fwd_ks_kernel<NC_, V_, D_>), grid, block, lds, stream, \
+#define PWK(NC_, V_, X_) hipLaunchKernelGGL((pw_fwd_ks_kernel<NC_, V_, X_>), grid, block, lds, stream, \
       x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq)
-#define PWK_V(NC_) do { if (d2s) { if (vec) PWK(NC_, true, true); else PWK(NC_, false, true); } \
-                        else { if (vec) PWK(NC_, true, false); else PWK(NC_, false, false); } } while (0)
+#define PWK_X(NC_, V_) do { if (xm == 1) PWK(NC_, V_, 1); else if (xm == 2) PWK(NC_, V_, 2); else PWK(NC_, V_, 0); } while (0)
+#define PWK_V(NC_) do { if (vec) PWK_X(NC_, true); else PWK_X(NC_, false); } while (0)
     if (NC == 1) PWK_V(1);
     else if (NC == 2) PWK_V(2);
     else PWK_V(4);
 #undef PWK_V
+#undef PWK_X
 #undef PWK
     L3U_CHECK_LAUNCH();
   }
@@ -559,19 +560,57 @@ int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout,
   dim3 grid(nsb, (Nout + CO_BLK - 1) / CO_BLK, N), block(256);
   L3U_REQUIRE(NSW == 1);
   const int KSn = K <= 16 ? 4 : (K <= 32 ? 8 : (K <= 64 ? 16 : 0));
-#define PWF(NC_, V_, D_, KS_) hipLaunchKernelGGL((pw_fwd_kernel<NC_, 1, V_, D_, KS_>), grid, block, lds, \
+#define PWF(NC_, V_, X_, KS_) hipLaunchKernelGGL((pw_fwd_kernel<NC_, 1, V_, X_, KS_>), grid, block, lds, \
       stream, x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, \
       Dq, Hq, Wq)
-#define PWF_K(NC_, V_, D_) do { if (KSn == 4) PWF(NC_, V_, D_, 4); else if (KSn == 8) PWF(NC_, V_, D_, 8); \
-                                else if (KSn == 16) PWF(NC_, V_, D_, 16); else PWF(NC_, V_, D_, 0); } while (0)
-#define PWF_V(NC_) do { if (d2s) { if (vec) PWF_K(NC_, true, true); else PWF_K(NC_, false, true); } \
-                        else { if (vec) PWF_K(NC_, true, false); else PWF_K(NC_, false, false); } } while (0)
+#define PWF_K(NC_, V_, X_) do { if (KSn == 4) PWF(NC_, V_, X_, 4); else if (KSn == 8) PWF(NC_, V_, X_, 8); \
+                                else if (KSn == 16) PWF(NC_, V_, X_, 16); else PWF(NC_, V_, X_, 0); } while (0)
+#define PWF_X(NC_, V_) do { if (xm == 1) PWF_K(NC_, V_, 1); else if (xm == 2) PWF_K(NC_, V_, 2); else PWF_K(NC_, V_, 0); } while (0)
+#define PWF_V(NC_) do { if (vec) PWF_X(NC_, true); else PWF_X(NC_, false); } while (0)
   if (NC == 1) PWF_V(1);
   else if (NC == 2) PWF_V(2);
   else PWF_V(4);
 #undef PWF_V
+#undef PWF_X
 #undef PWF_K
 #undef PWF
+  L3U_CHECK_LAUNCH();
+}
+
+int pw_bwd_weight_launch(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
+                         float* part, int N, int J, int K, int S, bool gather, int Hq, int Wq,
+                         hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && J > 0 && K > 0 && S > 0);
+  const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (dy_nstride % 4 == 0) &&
+                   (!gather || Wq % 4 == 0);
+  const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
+  int NJ = J <= 16 ? 1 : (J <= 32 ? 2 : 4);
+  int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
+  // shrink the output tile until the grid has enough workgroups to fill the chip
+  for (;;) {
+    const long long nb = (long long)N * nsc * ((J + 16 * NJ - 1) / (16 * NJ)) *
+                         ((K + 16 * NK - 1) / (16 * NK));
+    if (nb >= 512 || (NJ == 1 && NK == 1)) break;
+    if (NJ >= NK) NJ >>= 1; else NK >>= 1;
+  }
+  const int ntj = (J + 16 * NJ - 1) / (16 * NJ), ntk = (K + 16 * NK - 1) / (16 * NK);
+  const size_t lds = 64 * (size_t)NJ * NK * 4 * sizeof(float);
+  dim3 grid(N * nsc, ntj * ntk), block(256);
+#define PWB0(A_, B_, V_, G_) hipLaunchKernelGGL((pw_bwd_weight_kernel<A_, B_, V_, G_>), grid, block, lds, \
+      stream, dy, dy_nstride, x, x_nstride, part, J, K, S, SCH, nsc, Hq, Wq)
+#define PWB(A_, B_) do { if (gather) { if (vec) PWB0(A_, B_, true, true); else PWB0(A_, B_, false, true); } \
+                         else { if (vec) PWB0(A_, B_, true, false); else PWB0(A_, B_, false, false); } } while (0)
+  if (NJ == 1 && NK == 1) PWB(1, 1);
+  else if (NJ == 1 && NK == 2) PWB(1, 2);
+  else if (NJ == 1 && NK == 4) PWB(1, 4);
+  else if (NJ == 2 && NK == 1) PWB(2, 1);
+  else if (NJ == 2 && NK == 2) PWB(2, 2);
+  else if (NJ == 2 && NK == 4) PWB(2, 4);
+  else if (NJ == 4 && NK == 1) PWB(4, 1);
+  else if (NJ == 4 && NK == 2) PWB(4, 2);
+  else PWB(4, 4);
+#undef PWB
+#undef PWB0
   L3U_CHECK_LAUNCH();
 }
 
@@ -583,7 +622,7 @@ int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout
                const float* bias, float* y, long long y_nstride, int accumulate,
                float* stat_part, int N, int K, int Nout, int S, hipStream_t stream) {
   return pw_launch(x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, N, K,
-                   Nout, S, false, 0, 0, 0, stream);
+                   Nout, S, 0, 0, 0, 0, stream);
 }
 
 int l3u_convt_fwd(const float* x, long long x_nstride, const float* w, const float* bias,
@@ -591,7 +630,7 @@ int l3u_convt_fwd(const float* x, long long x_nstride, const float* w, const flo
                   hipStream_t stream) {
   L3U_REQUIRE(D > 0 && H > 0 && W > 0);
   return pw_launch(x, x_nstride, w, 1, bias, out, out_nstride, 0, nullptr, N, Ci, Co * 8,
-                   D * H * W, true, D, H, W, stream);
+                   D * H * W, 1, D, H, W, stream);
 }
 
 int l3u_pw_stat_nsb(int K, int Nout, int S) {
@@ -608,39 +647,23 @@ int l3u_pw_bwd_weight_nparts(int N, int S) {
 
 int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
                       float* part, int N, int J, int K, int S, hipStream_t stream) {
-  L3U_REQUIRE(N > 0 && J > 0 && K > 0 && S > 0);
-  const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (dy_nstride % 4 == 0);
-  const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
-  int NJ = J <= 16 ? 1 : (J <= 32 ? 2 : 4);
-  int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
-  // shrink the output tile until the grid has enough workgroups to fill the chip
-  for (;;) {
-    const long long nb = (long long)N * nsc * ((J + 16 * NJ - 1) / (16 * NJ)) *
-                         ((K + 16 * NK - 1) / (16 * NK));
-    if (nb >= 512 || (NJ == 1 && NK == 1)) break;
-    if (NJ >= NK) NJ >>= 1; else NK >>= 1;
-  }
-  const int ntj = (J + 16 * NJ - 1) / (16 * NJ), ntk = (K + 16 * NK - 1) / (16 * NK);
-  const size_t lds = 64 * (size_t)NJ * NK * 4 * sizeof(float);
-  dim3 grid(N * nsc, ntj * ntk), block(256);
-#define PWB(A_, B_)                                                                               \
-  do {                                                                                            \
-    if (vec) hipLaunchKernelGGL((pw_bwd_weight_kernel<A_, B_, true>), grid, block, lds, stream,  \
-                                dy, dy_nstride, x, x_nstride, part, J, K, S, SCH, nsc);          \
-    else hipLaunchKernelGGL((pw_bwd_weight_kernel<A_, B_, false>), grid, block, lds, stream, dy, \
-                            dy_nstride, x, x_nstride, part, J, K, S, SCH, nsc);                  \
-  } while (0)
-  if (NJ == 1 && NK == 1) PWB(1, 1);
-  else if (NJ == 1 && NK == 2) PWB(1, 2);
-  else if (NJ == 1 && NK == 4) PWB(1, 4);
-  else if (NJ == 2 && NK == 1) PWB(2, 1);
-  else if (NJ == 2 && NK == 2) PWB(2, 2);
-  else if (NJ == 2 && NK == 4) PWB(2, 4);
-  else if (NJ == 4 && NK == 1) PWB(4, 1);
-  else if (NJ == 4 && NK == 2) PWB(4, 2);
-  else PWB(4, 4);
-#undef PWB
-  L3U_CHECK_LAUNCH();
+  return pw_bwd_weight_launch(dy, dy_nstride, x, x_nstride, part, N, J, K, S, false, 0, 0, stream);
+}
+
+int l3u_convt_bwd(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
+                  const float* w, float* dx, long long dx_nstride, float* wpart, double* bpart,
+                  int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && Ci > 0 && Co > 0 && D > 0 && H > 0 && W > 0);
+  const int S = D * H * W;
+  // dX[ci][s] = sum_{co,abc} w[ci][co*8+abc] dY[co][up(s, abc)]: the GEMM with X gathered
+  int rc = pw_launch(dy, dy_nstride, w, 0, nullptr, dx, dx_nstride, 0, nullptr, N, Co * 8, Ci, S,
+                     2, D, H, W, stream);
+  if (rc != 0) return rc;
+  // dW[ci][co*8+abc] = sum_s x[ci][s] dY[co][up(s, abc)]
+  rc = pw_bwd_weight_launch(x, x_nstride, dy, dy_nstride, wpart, N, Ci, Co * 8, S, true, H, W, stream);
+  if (rc != 0) return rc;
+  // db[co] = sum of dY over the up-sampled volume (per-channel partials)
+  return l3u_chan_sum(dy, dy_nstride, bpart, N, Co, 8ll * S, stream);
 }
 
 }  // extern "C"

@@ -41,6 +41,7 @@ _SIGS = {
     "l3u_maxpool2_bwd": [P, L, P, P, L, P, L, I, I, I, I, I, P],
     "l3u_convt_d2s": [P, P, P, L, I, I, I, I, I, P],
     "l3u_convt_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, P],
+    "l3u_convt_bwd": [P, L, P, L, P, P, L, P, P, I, I, I, I, I, I, P],
     "l3u_convt_s2d": [P, L, P, I, I, I, I, I, P],
     "l3u_chan_sum_nblocks": [L],
     "l3u_chan_sum": [P, L, P, I, I, L, P],

@@ -368,22 +368,16 @@ class UNetEngine:
             prev, _ = sv["ups"][uidx]
             ci = prev.C
             d, hh, w = dims[lvl + 1]
-            dyp = e(N, co * 8, S[lvl + 1])
-            self._call("l3u_convt_s2d", dcat.data_ptr(), 2 * co * S[lvl], dyp.data_ptr(), N, co, d,
-                       hh, w, st)
             dprev = e(N, ci, S[lvl + 1])
-            self._call("l3u_pw_fwd", dyp.data_ptr(), co * 8 * S[lvl + 1],
-                       self._w(flat, up + "up.weight"), 0, None, dprev.data_ptr(), ci * S[lvl + 1],
-                       0, None, N, co * 8, ci, S[lvl + 1], st)
             npw = nat.query("l3u_pw_bwd_weight_nparts", N, S[lvl + 1])
             pw = A.alloc(npw * ci * co * 8)
-            self._call("l3u_pw_bwd_weight", prev.p, prev.ns, dyp.data_ptr(), co * 8 * S[lvl + 1],
-                       A.ptr(pw), N, ci, co * 8, S[lvl + 1], st)
-            self._seg(pw, npw, ci * co * 8, 1, ci * co * 8, up + "up.weight")
             ncs = nat.query("l3u_chan_sum_nblocks", 8 * S[lvl + 1])
             pb = A.alloc(2 * co * N * ncs)            # fp64 partials
-            self._call("l3u_chan_sum", dyp.data_ptr(), co * 8 * S[lvl + 1], A.ptr(pb), N, co,
-                       8 * S[lvl + 1], st)
+            # dY read in place from the lower half of the concat gradient
+            self._call("l3u_convt_bwd", dcat.data_ptr(), 2 * co * S[lvl], prev.p, prev.ns,
+                       self._w(flat, up + "up.weight"), dprev.data_ptr(), ci * S[lvl + 1], A.ptr(pw),
+                       A.ptr(pb), N, ci, co, d, hh, w, st)
+            self._seg(pw, npw, ci * co * 8, 1, ci * co * 8, up + "up.weight")
             self._seg(pb // 2, N * ncs, 1, N * ncs, co, up + "up.bias", f64=1)
             dout = V(dprev, 0, ci * S[lvl + 1], ci)
         # ---- bottleneck
