@@ -97,6 +97,20 @@ int l3u_pw_bwd_weight_nparts(int N, int S);
 int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
                       float* part, int N, int J, int K, int S, hipStream_t stream);
 
+/* fused backward of the same 1x1 conv (Y = W X, W = w[j*K + k], torch weight [J][K]) in one
+ * pass over dY: dx[n][k][s] = sum_j W[j][k] dY[n][j][s] (accumulate != 0: dx += ...) and
+ * part[N*nsc][J][K] weight-gradient partials (same layout and count as l3u_pw_bwd_weight).
+ * y != NULL: dy holds dpre of the preceding InstanceNorm and dY is formed on the fly as
+ * l3u_in_bwd_apply would (rec / in_part[J][N][npart][2] as for that call); dY is not stored.
+ * Replaces the autograd backward of DepthwiseSeparableConv3d.pointwise (unet3d.py:18) and of the
+ * shortcut conv (unet3d.py:70-73), with the InstanceNorm backward of unet3d.py:51 folded in.
+ * Supported shapes: l3u_pw_bwd_supported(J, K, S) != 0 (J <= 32, K <= 64, S % 4 == 0).         */
+int l3u_pw_bwd_supported(int J, int K, int S);
+int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long y_nstride,
+               const float* rec, const double* in_part, int npart, const float* x,
+               long long x_nstride, const float* w, float* dx, long long dx_nstride, int accumulate,
+               float* part, int N, int J, int K, int S, hipStream_t stream);
+
 /* ---- InstanceNorm3d(affine=True, eps=1e-5) + LeakyReLU(0.01) + Dropout3d + residual --------
  * replaces nn.InstanceNorm3d / nn.LeakyReLU / nn.Dropout3d / "out + residual"
  *          (ResidualBlock.forward, unet3d.py:77-93)

@@ -411,6 +411,85 @@ __global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __res
   }
 }
 
+// Vector forms for even D, H and W % 4 == 0 (every pooled level of the network): one thread per
+// pair of x-adjacent outputs reads the 2x2 rows of its 2x2x4 input block as four float4 loads and
+// writes the pair (float2) and its two argmax bytes; the backward writes the same block as four
+// float4 stores.  Same scan order and comparison as the scalar kernels above.
+__global__ __launch_bounds__(256) void maxpool2_fwd_v_kernel(
+    const float* __restrict__ x, long long xns, float* __restrict__ y, long long yns,
+    unsigned char* __restrict__ idx, int C, int D, int H, int W) {
+  const int Ho = H / 2, W4 = W / 4;
+  const long long So = (long long)(D / 2) * Ho * (W / 2), Si = (long long)D * H * W;
+  const long long Sp = So / 2;
+  const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const float* xp = x + (long long)n * xns + (long long)c * Si;
+  float2* yp = reinterpret_cast<float2*>(y + (long long)n * yns + (long long)c * So);
+  unsigned short* ip = reinterpret_cast<unsigned short*>(idx + (long long)nc * So);
+  for (long long o = blockIdx.x * 256ll + threadIdx.x; o < Sp; o += (long long)gridDim.x * 256) {
+    const int q = (int)(o % W4), t = (int)(o / W4), oy = t % Ho, oz = t / Ho;
+    const float* b = xp + ((long long)(2 * oz) * H + 2 * oy) * W + 4 * q;
+    float4 r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      r[j] = *reinterpret_cast<const float4*>(b + ((long long)(j >> 1) * H + (j & 1)) * W);
+    float b0 = r[0].x, b1 = r[0].z;
+    int i0 = 0, i1 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float v0[2] = {r[j].x, r[j].y}, v1[2] = {r[j].z, r[j].w};
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        if (j == 0 && dx == 0) continue;
+        if (v0[dx] > b0 || v0[dx] != v0[dx]) { b0 = v0[dx]; i0 = 2 * j + dx; }
+        if (v1[dx] > b1 || v1[dx] != v1[dx]) { b1 = v1[dx]; i1 = 2 * j + dx; }
+      }
+    }
+    yp[o] = make_float2(b0, b1);
+    ip[o] = (unsigned short)(i0 | (i1 << 8));
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool2_bwd_v_kernel(
+    const float* __restrict__ dy, long long dyns, const unsigned char* __restrict__ idx,
+    const float* __restrict__ add, long long addns, float* __restrict__ dx, long long dxns,
+    int C, int D, int H, int W) {
+  const int Ho = H / 2, W4 = W / 4;
+  const long long So = (long long)(D / 2) * Ho * (W / 2), Si = (long long)D * H * W;
+  const long long Sp = So / 2;
+  const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const float2* dyp = reinterpret_cast<const float2*>(dy + (long long)n * dyns + (long long)c * So);
+  const unsigned short* ip = reinterpret_cast<const unsigned short*>(idx + (long long)nc * So);
+  const float* ap = add ? add + (long long)n * addns + (long long)c * Si : nullptr;
+  float* dxp = dx + (long long)n * dxns + (long long)c * Si;
+  for (long long o = blockIdx.x * 256ll + threadIdx.x; o < Sp; o += (long long)gridDim.x * 256) {
+    const int q = (int)(o % W4), t = (int)(o / W4), oy = t % Ho, oz = t / Ho;
+    const long long base = ((long long)(2 * oz) * H + 2 * oy) * W + 4 * q;
+    const float2 g = dyp[o];
+    const int id = ip[o], i0 = id & 0xff, i1 = id >> 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long off = base + ((long long)(j >> 1) * H + (j & 1)) * W;
+      float4 v = ap ? *reinterpret_cast<const float4*>(ap + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v.x += i0 == 2 * j ? g.x : 0.f;
+      v.y += i0 == 2 * j + 1 ? g.x : 0.f;
+      v.z += i1 == 2 * j ? g.y : 0.f;
+      v.w += i1 == 2 * j + 1 ? g.y : 0.f;
+      *reinterpret_cast<float4*>(dxp + off) = v;
+    }
+  }
+}
+
+// the vector kernels need even D and H, W % 4 == 0 and 16-byte aligned channel planes
+bool pool_vec_ok(int D, int H, int W, const void* a, long long ans, const void* b, long long bns,
+                 const void* c, long long cns) {
+  if ((D & 1) || (H & 1) || (W & 3)) return false;
+  const void* p[3] = {a, b, c};
+  const long long ns[3] = {ans, bns, cns};
+  for (int i = 0; i < 3; ++i)
+    if (p[i] && (((uintptr_t)p[i] & 15) || (ns[i] & 3))) return false;
+  return true;
+}
+
 int grid_for(long long n, int per_block, int cap) {
   long long b = (n + per_block - 1) / per_block;
   if (b > cap) b = cap;
@@ -425,8 +504,13 @@ int l3u_maxpool2_fwd(const float* x, long long x_nstride, float* y, long long y_
                      unsigned char* idx, int N, int C, int D, int H, int W, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && D >= 2 && H >= 2 && W >= 2);
   const long long So = (long long)(D / 2) * (H / 2) * (W / 2);
-  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(So, 256, 64), N * C), dim3(256), 0, stream,
-                     x, x_nstride, y, y_nstride, idx, C, D, H, W);
+  if (pool_vec_ok(D, H, W, x, x_nstride, nullptr, 0, nullptr, 0) && ((uintptr_t)y & 7) == 0 &&
+      (y_nstride & 1) == 0 && ((uintptr_t)idx & 1) == 0)
+    hipLaunchKernelGGL(maxpool2_fwd_v_kernel, dim3(grid_for(So / 2, 256, 64), N * C), dim3(256), 0,
+                       stream, x, x_nstride, y, y_nstride, idx, C, D, H, W);
+  else
+    hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(So, 256, 64), N * C), dim3(256), 0, stream,
+                       x, x_nstride, y, y_nstride, idx, C, D, H, W);
   L3U_CHECK_LAUNCH();
 }
 
@@ -435,8 +519,13 @@ int l3u_maxpool2_bwd(const float* dy, long long dy_nstride, const unsigned char*
                      int N, int C, int D, int H, int W, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && D >= 2 && H >= 2 && W >= 2);
   const long long Si = (long long)D * H * W;
-  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(Si, 256, 128), N * C), dim3(256), 0, stream,
-                     dy, dy_nstride, idx, add, add_nstride, dx, dx_nstride, C, D, H, W);
+  if (pool_vec_ok(D, H, W, add, add_nstride, dx, dx_nstride, nullptr, 0) &&
+      ((uintptr_t)dy & 7) == 0 && (dy_nstride & 1) == 0 && ((uintptr_t)idx & 1) == 0)
+    hipLaunchKernelGGL(maxpool2_bwd_v_kernel, dim3(grid_for(Si / 16, 256, 64), N * C), dim3(256), 0,
+                       stream, dy, dy_nstride, idx, add, add_nstride, dx, dx_nstride, C, D, H, W);
+  else
+    hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(Si, 256, 128), N * C), dim3(256), 0, stream,
+                       dy, dy_nstride, idx, add, add_nstride, dx, dx_nstride, C, D, H, W);
   L3U_CHECK_LAUNCH();
 }
 

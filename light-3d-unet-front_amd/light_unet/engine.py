@@ -444,12 +444,11 @@ class UNetEngine:
                    cout * S, drv.p, drv.ns, N, cout, S, st)
         # (2) conv2.pointwise backward
         dz2 = e(N, cout, S)
-        self._call("l3u_pw_fwd", dy2.data_ptr(), cout * S, self._w(flat, pre + "conv2.pointwise.weight"),
-                   1, None, dz2.data_ptr(), cout * S, 0, None, N, cout, cout, S, st)
         npw = nat.query("l3u_pw_bwd_weight_nparts", N, S)
         pp2 = A.alloc(npw * cout * cout)
-        self._call("l3u_pw_bwd_weight", dy2.data_ptr(), cout * S, z2.data_ptr(), cout * S, A.ptr(pp2),
-                   N, cout, cout, S, st)
+        self._pw_bwd(V(dy2, 0, cout * S, cout), None, V(z2, 0, cout * S, cout),
+                     self._w(flat, pre + "conv2.pointwise.weight"), V(dz2, 0, cout * S, cout), 0,
+                     A.ptr(pp2), N, S, st)
         self._seg(pp2, npw, cout * cout, 1, cout * cout, pre + "conv2.pointwise.weight")
         # (3) conv2.depthwise backward fused with LeakyReLU/Dropout/IN1 backward partials
         nch = nat.query("l3u_dw3_nchunk", N, cout, d, h, w)
@@ -463,16 +462,21 @@ class UNetEngine:
         self._seg_dw(pd2, N * nch, cout, pre + "conv2.depthwise.weight")
         self._seg(pid + 1, N * nch, 2, N * nch * 2, cout, pre + "norm1.weight", f64=1)
         self._seg(pid + 0, N * nch, 2, N * nch * 2, cout, pre + "norm1.bias", f64=1)
-        self._call("l3u_in_bwd_apply", dpre.data_ptr(), cout * S, y1.data_ptr(), cout * S, rec1,
-                   A.ptr(pi1), nch, dpre.data_ptr(), cout * S, N, cout, S, st)
-        dy1 = dpre
-        # (4) conv1.pointwise backward
+        # (4) conv1.pointwise backward, with the IN1 backward (dy1 from dpre) folded in when the
+        # fused kernel takes the shape
         dz1 = e(N, cin, S)
-        self._call("l3u_pw_fwd", dy1.data_ptr(), cout * S, self._w(flat, pre + "conv1.pointwise.weight"),
-                   1, None, dz1.data_ptr(), cin * S, 0, None, N, cout, cin, S, st)
         pp1 = A.alloc(npw * cout * cin)
-        self._call("l3u_pw_bwd_weight", dy1.data_ptr(), cout * S, z1.data_ptr(), cin * S, A.ptr(pp1),
-                   N, cout, cin, S, st)
+        dpv = V(dpre, 0, cout * S, cout)
+        w1 = self._w(flat, pre + "conv1.pointwise.weight")
+        if nat.query("l3u_pw_bwd_supported", cout, cin, S):
+            self._pw_bwd(dpv, (y1.data_ptr(), cout * S, rec1, A.ptr(pi1), nch),
+                         V(z1, 0, cin * S, cin), w1, V(dz1, 0, cin * S, cin), 0, A.ptr(pp1), N, S, st)
+        else:
+            self._call("l3u_in_bwd_apply", dpre.data_ptr(), cout * S, y1.data_ptr(), cout * S, rec1,
+                       A.ptr(pi1), nch, dpre.data_ptr(), cout * S, N, cout, S, st)
+            self._pw_bwd(dpv, None, V(z1, 0, cin * S, cin), w1, V(dz1, 0, cin * S, cin), 0,
+                         A.ptr(pp1), N, S, st)
+        dy1 = dpre
         self._seg(pp1, npw, cout * cin, 1, cout * cin, pre + "conv1.pointwise.weight")
         # (5) conv1.depthwise backward: writes d(input) (Conv1x1 shortcut) or accumulates into the
         # identity-shortcut gradient already there
@@ -484,14 +488,28 @@ class UNetEngine:
         self._seg_dw(pd1, N * nch1, cin, pre + "conv1.depthwise.weight")
         # (6) shortcut conv backward accumulates into d(input)
         if shortcut:
-            self._call("l3u_pw_fwd", drv.p, drv.ns, self._w(flat, pre + "shortcut.0.weight"), 1, None,
-                       dxv.p, dxv.ns, 1, None, N, cout, cin, S, st)
             ppr = A.alloc(npw * cout * cin)
-            self._call("l3u_pw_bwd_weight", drv.p, drv.ns, x.p, x.ns, A.ptr(ppr), N, cout, cin, S, st)
+            self._pw_bwd(drv, None, x, self._w(flat, pre + "shortcut.0.weight"), dxv, 1, A.ptr(ppr),
+                         N, S, st)
             self._seg(ppr, npw, cout * cin, 1, cout * cin, pre + "shortcut.0.weight")
         if self.debug is not None and not self._dry:
             self.debug[pre + "#"] = {"dy2": dy2, "dr": drv, "dz2": dz2, "dy1": dy1, "dz1": dz1,
                                      "dx": dxv}
+
+    def _pw_bwd(self, dy, pro, x, w, dx, accumulate, part, N, S, st):
+        """Backward of a 1x1 conv y = W x (W [J][K]): dx (+)= W^T dy and weight-gradient partials
+        [nparts][J][K].  pro = (y, y_nstride, rec, in_part, npart): dy holds dpre of the preceding
+        InstanceNorm and the fused kernel applies its backward on the fly."""
+        J, K = dy.C, x.C
+        if nat.query("l3u_pw_bwd_supported", J, K, S):
+            y, yns, rec, ip, npart = pro if pro is not None else (None, 0, None, None, 0)
+            self._call("l3u_pw_bwd", dy.p, dy.ns, y, yns, rec, ip, npart, x.p, x.ns, w, dx.p, dx.ns,
+                       accumulate, part, N, J, K, S, st)
+            return
+        assert pro is None
+        self._call("l3u_pw_fwd", dy.p, dy.ns, w, 1, None, dx.p, dx.ns, accumulate, None, N, J, K, S,
+                   st)
+        self._call("l3u_pw_bwd_weight", dy.p, dy.ns, x.p, x.ns, part, N, J, K, S, st)
 
     def _seg_dw(self, off, count, C, name):
         # dw_part layout [C][count][27] -> grad [C][27]

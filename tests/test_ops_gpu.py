@@ -230,6 +230,83 @@ def test_pw_bwd_weight(cuda, case):
     close(part.view(P, J, K).double().sum(0), ref, 1e-5, f"pw_bwd_weight {case}")
 
 
+# fused 1x1-conv backward: (N, J, K, S, with_in_prologue, accumulate)
+PW_BWD_CASES = [
+    (2, 16, 1, 6 * 8 * 10, True, False),       # init block conv1 (K = 1), ragged chunk
+    (2, 16, 16, 12 ** 3, False, False),
+    (1, 16, 32, 24 ** 3, True, False),         # up3 conv1 shape class, multi-iteration chunks
+    (2, 32, 16, 6 * 6 * 8, False, True),       # shortcut: accumulate into d(input)
+    (2, 32, 64, 8 ** 3, True, False),          # up2 conv1 (NJ 2, NK 4)
+    (3, 20, 40, 4 * 5 * 12, True, True),       # partial tiles in J and K
+]
+
+
+@pytest.mark.parametrize("case", PW_BWD_CASES)
+def test_pw_bwd_fused(cuda, case):
+    N, J, K, S, pro, acc = case
+    assert nat().query("l3u_pw_bwd_supported", J, K, S) == 1
+    gen = torch.Generator().manual_seed(11)
+    x = torch.randn(N, K, S, generator=gen, dtype=torch.float64)
+    w = torch.randn(J, K, generator=gen, dtype=torch.float64) / K ** 0.5
+    dpre = torch.randn(N, J, S, generator=gen, dtype=torch.float64)
+    if pro:   # dY = InstanceNorm backward of dpre (the in_bwd_apply reference above)
+        y = torch.randn(N, J, S, generator=gen, dtype=torch.float64) * 1.5 + 0.2
+        g = 1 + 0.3 * torch.randn(J, generator=gen, dtype=torch.float64)
+        yr = y.clone().requires_grad_(True)
+        F.instance_norm(yr, weight=g, eps=1e-5).backward(dpre)
+        dy = yr.grad
+        m = y.mean(-1)
+        rs = 1 / torch.sqrt(y.var(-1, unbiased=False) + 1e-5)
+        rec = torch.zeros(N, J, 8, dtype=torch.float64)
+        rec[..., 0], rec[..., 1], rec[..., 5] = m, rs, g.expand(N, J)
+        xhat = (y - m[..., None]) * rs[..., None]
+        nch = 3
+        part_in = torch.zeros(J, N, nch, 2, dtype=torch.float64)
+        part_in[:, :, 1, 0] = dpre.sum(-1).t()
+        part_in[:, :, 1, 1] = (dpre * xhat).sum(-1).t()
+    else:
+        dy = dpre
+    dx0 = torch.randn(N, K, S, generator=gen, dtype=torch.float64) if acc else torch.zeros(N, K, S,
+                                                                                            dtype=torch.float64)
+    ref_dx = torch.einsum("jk,njs->nks", w, dy) + dx0
+    ref_dw = torch.einsum("njs,nks->jk", dy, x)
+    P = nat().query("l3u_pw_bwd_weight_nparts", N, S)
+    part = torch.full((P * J * K,), float("nan"), device=cuda)
+    xd, wd, dd = x.float().to(cuda), w.float().to(cuda), dpre.float().to(cuda)
+    dx = dx0.float().to(cuda) if acc else torch.full((N, K, S), float("nan"), device=cuda)
+    if pro:
+        yd, recd, pid = y.float().to(cuda), rec.float().to(cuda), part_in.to(cuda)
+        pro_args = (yd.data_ptr(), J * S, recd.data_ptr(), pid.data_ptr(), nch)
+    else:
+        pro_args = (None, 0, None, None, 0)
+    nat().call("l3u_pw_bwd", dd.data_ptr(), J * S, *pro_args, xd.data_ptr(), K * S, wd.data_ptr(),
+               dx.data_ptr(), K * S, 1 if acc else 0, part.data_ptr(), N, J, K, S, st())
+    torch.cuda.synchronize()
+    close(dx, ref_dx, 1e-5, f"pw_bwd dx {case}")
+    close(part.view(P, J, K).double().sum(0), ref_dw, 2e-5, f"pw_bwd dw {case}")
+
+
+def test_pw_bwd_matches_unfused(cuda):
+    """The fused call reproduces in_bwd_apply + pw_fwd(data) + pw_bwd_weight to fp32 rounding."""
+    N, J, K, S = 2, 16, 32, 12 ** 3
+    gen = torch.Generator().manual_seed(12)
+    x = torch.randn(N, K, S, generator=gen).to(cuda)
+    w = torch.randn(J, K, generator=gen).to(cuda)
+    dy = torch.randn(N, J, S, generator=gen).to(cuda)
+    P = nat().query("l3u_pw_bwd_weight_nparts", N, S)
+    p1, p2 = torch.empty(P * J * K, device=cuda), torch.empty(P * J * K, device=cuda)
+    dx1, dx2 = torch.empty(N, K, S, device=cuda), torch.empty(N, K, S, device=cuda)
+    nat().call("l3u_pw_bwd", dy.data_ptr(), J * S, None, 0, None, None, 0, x.data_ptr(), K * S,
+               w.data_ptr(), dx1.data_ptr(), K * S, 0, p1.data_ptr(), N, J, K, S, st())
+    nat().call("l3u_pw_fwd", dy.data_ptr(), J * S, w.data_ptr(), 1, None, dx2.data_ptr(), K * S, 0,
+               None, N, J, K, S, st())
+    nat().call("l3u_pw_bwd_weight", dy.data_ptr(), J * S, x.data_ptr(), K * S, p2.data_ptr(), N, J,
+               K, S, st())
+    torch.cuda.synchronize()
+    close(dx1, dx2, 1e-6, "dx fused vs unfused")
+    close(p1.view(P, J, K).sum(0), p2.view(P, J, K).sum(0), 1e-5, "dw fused vs unfused")
+
+
 # ------------------------------------------------------------------------------ InstanceNorm
 def test_in_finalize_and_dropout(cuda):
     N, C, nsb = 3, 5, 7
@@ -381,15 +458,25 @@ def test_in_bwd_apply(cuda):
 
 
 # ------------------------------------------------------------------------------ pool / convT
-@pytest.mark.parametrize("shape", [(2, 3, 6, 8, 10), (4, 16, 48, 48, 48), (1, 2, 7, 5, 9)])
-def test_maxpool(cuda, shape):
+@pytest.mark.parametrize("shape,ties,with_add", [
+    ((2, 3, 6, 8, 10), False, True),      # scalar kernels (W % 4 != 0)
+    ((4, 16, 48, 48, 48), False, True),   # vector kernels
+    ((1, 2, 7, 5, 9), False, True),       # odd sizes: dropped border voxels get 0 (+ add)
+    ((2, 3, 6, 8, 12), True, True),       # vector, W/4 odd, tied maxima (first in scan order wins)
+    ((2, 4, 12, 12, 12), True, False),    # vector, no add
+])
+def test_maxpool(cuda, shape, ties, with_add):
     N, C, D, H, W = shape
     gen = torch.Generator().manual_seed(8)
-    x = torch.randn(shape, generator=gen, dtype=torch.float64)
+    if ties:
+        x = torch.randint(0, 3, shape, generator=gen).double()
+    else:
+        x = torch.randn(shape, generator=gen, dtype=torch.float64)
     xr = x.clone().requires_grad_(True)
     y = F.max_pool3d(xr, 2, 2)
     dy = torch.randn(y.shape, generator=gen, dtype=torch.float64)
-    add = torch.randn(shape, generator=gen, dtype=torch.float64)
+    add = (torch.randn(shape, generator=gen, dtype=torch.float64) if with_add
+           else torch.zeros(shape, dtype=torch.float64))
     y.backward(dy)
     So = y.shape[2] * y.shape[3] * y.shape[4]
     S = D * H * W
@@ -400,8 +487,8 @@ def test_maxpool(cuda, shape):
                N, C, D, H, W, st())
     dyd, ad = dy.float().to(cuda), add.float().to(cuda)
     dx = torch.empty(N, C, S, device=cuda)
-    nat().call("l3u_maxpool2_bwd", dyd.data_ptr(), C * So, idx.data_ptr(), ad.data_ptr(), C * S,
-               dx.data_ptr(), C * S, N, C, D, H, W, st())
+    nat().call("l3u_maxpool2_bwd", dyd.data_ptr(), C * So, idx.data_ptr(),
+               ad.data_ptr() if with_add else None, C * S, dx.data_ptr(), C * S, N, C, D, H, W, st())
     torch.cuda.synchronize()
     close(yd.view(y.shape), y, 1e-7, "maxpool fwd")
     close(dx.view(shape), xr.grad + add, 1e-6, "maxpool bwd")
