@@ -104,6 +104,27 @@ L3U_DEV double block_sum256d(double v, double* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// t[v] = sum_{i < n} p[i * NV + v] in index order (fp64); the loads of 8 steps are issued
+// together so a long partial list costs one memory latency per 8 entries, not one per entry.
+template <int NV>
+L3U_DEV void seq_sum(const double* __restrict__ p, int n, double t[NV]) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) t[v] = 0.0;
+  for (int i0 = 0; i0 < n; i0 += 8) {
+    double a[8][NV];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) a[u][v] = i0 + u < n ? p[(i0 + u) * NV + v] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + u < n) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) t[v] += a[u][v];
+      }
+  }
+}
+
 // Chan et al. parallel merge of (count, mean, M2) — deterministic when merged in fixed order.
 L3U_DEV void chan_merge(float& n_a, float& mean_a, float& m2_a, float n_b, float mean_b, float m2_b) {
   const float n = n_a + n_b;
@@ -130,7 +151,20 @@ L3U_DEV void finalize_record(const l3u_norm_src& s, int n, int c, int C, float r
   const int l = threadIdx.x & 63;
   const float* p = s.stat_part + ((long long)n * C + c) * s.nsb * 3;
   float cn = 0.f, mu = 0.f, m2 = 0.f;
-  for (int i = l; i < s.nsb; i += 64) chan_merge(cn, mu, m2, p[i * 3], p[i * 3 + 1], p[i * 3 + 2]);
+  // lane-strided sequential merges; the loads of 8 steps are issued together (one memory
+  // latency per 8 partials instead of one per partial), the merge order is unchanged
+  for (int i0 = l; i0 < s.nsb; i0 += 64 * 8) {
+    float v[8][3];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + 64 * u;
+      v[u][0] = v[u][1] = v[u][2] = 0.f;
+      if (i < s.nsb) { v[u][0] = p[i * 3]; v[u][1] = p[i * 3 + 1]; v[u][2] = p[i * 3 + 2]; }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + 64 * u < s.nsb) chan_merge(cn, mu, m2, v[u][0], v[u][1], v[u][2]);
+  }
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const float cb = __shfl_xor(cn, o, 64), mb = __shfl_xor(mu, o, 64), vb = __shfl_xor(m2, o, 64);

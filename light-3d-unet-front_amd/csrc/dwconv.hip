@@ -337,7 +337,10 @@ QGeom qgeom(int N, int C, int D, int H, int W) {
 #define L3U_TZ16_MIN_D 48
 #endif
   g.TZ = D >= L3U_TZ16_MIN_D ? 16 : (D >= 32 ? 8 : (D > 8 ? 4 : 8));   // compile-time in the kernels
-  while (g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < 1024) g.TZ >>= 1;   // {16, 8, 4, 2}
+#ifndef L3U_DW_MIN_BLOCKS
+#define L3U_DW_MIN_BLOCKS 1024
+#endif
+  while (g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < L3U_DW_MIN_BLOCKS) g.TZ >>= 1;   // {16, 8, 4, 2}
   g.nz = (D + g.TZ - 1) / g.TZ;
   return g;
 }

@@ -127,8 +127,9 @@ __global__ __launch_bounds__(256) void norm_act_bwd_apply_kernel(
     float* __restrict__ dr, long long drns, int N, int C, int S) {
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   const double* pp = part + ((long long)c * N + n) * npart * 3;
-  double t0 = 0.0, t1 = 0.0, t2 = 0.0;
-  for (int i = 0; i < npart; ++i) { t0 += pp[i * 3]; t1 += pp[i * 3 + 1]; t2 += pp[i * 3 + 2]; }
+  double t[3];
+  seq_sum<3>(pp, npart, t);
+  const double t0 = t[0], t1 = t[1], t2 = t[2];
   const float M0 = (float)(t0 / S), M1 = (float)(t1 / S), M2 = (float)(t2 / S);
   const float* q2 = rec2 + (long long)nc * kRec;
   const float mu2 = q2[0], rs2 = q2[1], f2 = q2[1] * q2[5];
@@ -175,8 +176,9 @@ __global__ __launch_bounds__(256) void in_bwd_apply_kernel(
     long long dyns, int N, int C, int S) {
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   const double* pp = part + ((long long)c * N + n) * npart * 2;
-  double t0 = 0.0, t1 = 0.0;
-  for (int i = 0; i < npart; ++i) { t0 += pp[i * 2]; t1 += pp[i * 2 + 1]; }
+  double t[2];
+  seq_sum<2>(pp, npart, t);
+  const double t0 = t[0], t1 = t[1];
   const float M1 = (float)(t0 / S), M2 = (float)(t1 / S);
   const float* q = rec + (long long)nc * kRec;
   const float mu = q[0], rs = q[1], f = q[1] * q[5];

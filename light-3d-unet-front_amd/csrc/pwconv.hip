@@ -497,7 +497,9 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 }
 
 // Fused backward of a 1x1 conv Y = W X (W [J][K]) for J <= 32, K <= 64 (the 48^3 / 24^3 levels):
-// one pass over a voxel chunk reads dY once and produces both
+// one pass over a voxel chunk (one wave per 64 voxels, up to 8 waves: a chunk is one sweep) reads
+// dY once per 16*NK columns of K (grid.y splits K for parallelism; dY re-reads hit L2) and
+// produces both
 //   dX[k][s]  = sum_j W[j][k] dY[j][s]              (data gradient, optional accumulate)
 //   part[j][k] = sum_{s in chunk} dY[j][s] X[k][s]  (weight-gradient partial, fixed order)
 // PRO 1 forms dY on the fly from the InstanceNorm backward of the preceding norm
@@ -509,31 +511,78 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 // the weight gradient and is loaded in its B layout.  The weights sit in LDS as W[j][k] with a
 // row stride = 16 mod 64 floats (conflict-free A-operand reads for the data gradient).
 template <int NJ, int NK, int PRO>
-__global__ __launch_bounds__(256) void pw_bwd_fused_kernel(
+__global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const float* __restrict__ dy, long long dyns, const float* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
     const float* __restrict__ x, long long xns, const float* __restrict__ w,
-    float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part, int J, int K,
-    int S, int SCH, int nsc) {
+    float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part, int N, int J,
+    int K, int S, int SCH, int nsc) {
   constexpr int TJ = 16 * NJ, TK = 16 * NK, JR = TJ / 4;
   constexpr int WS = TK + ((16 - TK) % 64 + 64) % 64;   // >= TK, = 16 mod 64
   constexpr int DS = 68;                                // dY tile row stride (floats)
+  constexpr int PS = 8;                                 // lanes per channel for the IN sums
+  static_assert(NK * 256 <= 16 * DS, "weight-gradient reduction must fit in the dY tiles");
   __shared__ __attribute__((aligned(16))) float w_l[TJ * WS];
   __shared__ __attribute__((aligned(16))) float coef[PRO ? TJ * 8 : 1];
-  __shared__ __attribute__((aligned(16))) float dyt[4][TJ * DS];
+  __shared__ double psum[PRO ? TJ * PS * 2 : 1];
+  __shared__ __attribute__((aligned(16))) float dyt[8][TJ * DS];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
-  const int sc = blockIdx.x % nsc, n = blockIdx.x / nsc;
+  const int nthr = blockDim.x, nwv = nthr >> 6;         // one sweep: SCH == 64 * nwv
+  const int sc = blockIdx.x % nsc, n = blockIdx.x / nsc, k0 = blockIdx.y * TK;
   const int s_lo = sc * SCH, s_hi = min(S, s_lo + SCH);
-  for (int i = tid; i < TJ * WS; i += 256) {
-    const int j = i / WS, k = i - j * WS;
-    w_l[i] = (j < J && k < K) ? w[(long long)j * K + k] : 0.f;
+  const int sw = s_lo + 64 * wave;
+  const int sd = sw + 4 * lr;                           // data-gradient layout voxels
+  const float* dyn = dy + (long long)n * dyns;
+  const float* xn = x + (long long)n * xns;
+  float* dxn = dx + (long long)n * dxns;
+
+  // 1. every streamed load of the tile is issued first ...
+  f4 g[JR], yv[PRO ? JR : 1];
+#pragma unroll
+  for (int jr = 0; jr < JR; ++jr) {
+    const int j = 4 * jr + lk;
+    g[jr] = f4{0.f, 0.f, 0.f, 0.f};
+    if (j < J && sd < s_hi) g[jr] = *reinterpret_cast<const f4*>(dyn + (long long)j * S + sd);
   }
+  if (PRO) {
+    const float* yn = yin + (long long)n * yns;
+#pragma unroll
+    for (int jr = 0; jr < JR; ++jr) {
+      const int j = 4 * jr + lk;
+      yv[jr] = f4{0.f, 0.f, 0.f, 0.f};
+      if (j < J && sd < s_hi) yv[jr] = *reinterpret_cast<const f4*>(yn + (long long)j * S + sd);
+    }
+  }
+  f4 xv[4][NK];
+#pragma unroll
+  for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+    for (int b = 0; b < NK; ++b)
+      xv[gg][b] = load_x4<true, false>(xn, k0 + 16 * b + lr, K, sw + 16 * gg + 4 * lk, s_hi, S, 0, 0);
+
+  // 2. ... then the small per-workgroup operands: the weight slice and (PRO) the per-channel
+  // InstanceNorm-backward coefficients, whose fp64 partial sums are spread over PS lanes per
+  // channel and combined in a fixed order
+  for (int i = tid; i < TJ * WS; i += nthr) {
+    const int j = i / WS, kc = i - j * WS, k = k0 + kc;
+    w_l[i] = (j < J && kc < TK && k < K) ? w[(long long)j * K + k] : 0.f;
+  }
+  if (PRO && tid < TJ * PS) {
+    const int j = tid / PS, sub = tid % PS;
+    double t0 = 0.0, t1 = 0.0;
+    if (j < J) {
+      const double* pp = in_part + ((long long)j * N + n) * npart * 2;
+      for (int i = sub; i < npart; i += PS) { t0 += pp[i * 2]; t1 += pp[i * 2 + 1]; }
+    }
+    psum[tid * 2] = t0;
+    psum[tid * 2 + 1] = t1;
+  }
+  __syncthreads();
   if (PRO && tid < TJ) {
     float* o = coef + tid * 8;
     if (tid < J) {
-      const double* pp = in_part + ((long long)tid * (gridDim.x / nsc) + n) * npart * 2;
       double t0 = 0.0, t1 = 0.0;
-      for (int i = 0; i < npart; ++i) { t0 += pp[i * 2]; t1 += pp[i * 2 + 1]; }
+      for (int i = 0; i < PS; ++i) { t0 += psum[(tid * PS + i) * 2]; t1 += psum[(tid * PS + i) * 2 + 1]; }
       const float* q = rec + ((long long)n * J + tid) * kRec;
       o[0] = q[1] * q[5];          // f = rstd * gamma
       o[1] = (float)(t0 / S);      // M1
@@ -544,109 +593,83 @@ __global__ __launch_bounds__(256) void pw_bwd_fused_kernel(
       o[0] = o[1] = o[2] = o[3] = o[4] = 0.f;
     }
   }
-  __syncthreads();
-  const float* dyn = dy + (long long)n * dyns;
-  const float* yn = PRO ? yin + (long long)n * yns : nullptr;
-  const float* xn = x + (long long)n * xns;
-  float* dxn = dx + (long long)n * dxns;
+  if (PRO) __syncthreads();
+
+  // 3. dY (PRO: formed from dpre as l3u_in_bwd_apply does), copy into the wave's LDS tile
+  if (PRO) {
+#pragma unroll
+    for (int jr = 0; jr < JR; ++jr) {
+      const int j = 4 * jr + lk;
+      const float* c = coef + j * 8;
+      const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
+      const bool ok = j < J && sd < s_hi;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) g[jr][q] = ok ? f * (g[jr][q] - M1 - (yv[jr][q] - mu) * rs * M2) : 0.f;
+    }
+  }
   float* tile = dyt[wave];
+#pragma unroll
+  for (int jr = 0; jr < JR; ++jr)
+    *reinterpret_cast<f4*>(tile + (4 * jr + lk) * DS + 4 * lr) = g[jr];
+
+  // 4. data gradient, one 16-row tile of dX at a time, from the registers
+#pragma unroll
+  for (int kt = 0; kt < NK; ++kt) {
+    f4 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int jr = 0; jr < JR; ++jr) {
+      const float a = w_l[(4 * jr + lk) * WS + 16 * kt + lr];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = mfma4(a, g[jr][q], acc[q]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k0 + 16 * kt + 4 * lk + r;
+      if (k < K && sd < s_hi) {
+        float* dst = dxn + (long long)k * S + sd;
+        f4 v = f4{acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
+        if (accumulate) v += *reinterpret_cast<const f4*>(dst);
+        *reinterpret_cast<f4*>(dst) = v;
+      }
+    }
+  }
+
+  // 5. weight gradient: dY rows back from the wave's LDS tile in the A layout
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   f4 gw[NJ][NK];
 #pragma unroll
   for (int a = 0; a < NJ; ++a)
 #pragma unroll
     for (int b = 0; b < NK; ++b) gw[a][b] = f4{0.f, 0.f, 0.f, 0.f};
-
-  for (int s_it = s_lo; s_it < s_hi; s_it += 256) {
-    const int sw = s_it + 64 * wave;
-    const int sd = sw + 4 * lr;                 // data-gradient layout voxels
-    f4 g[JR];
 #pragma unroll
-    for (int jr = 0; jr < JR; ++jr) {
-      const int j = 4 * jr + lk;
-      g[jr] = f4{0.f, 0.f, 0.f, 0.f};
-      if (j < J && sd < s_hi) g[jr] = *reinterpret_cast<const f4*>(dyn + (long long)j * S + sd);
-    }
-    f4 xv[4][NK];
+  for (int gg = 0; gg < 4; ++gg) {
+    f4 av[NJ];
 #pragma unroll
-    for (int gg = 0; gg < 4; ++gg)
+    for (int a = 0; a < NJ; ++a)
+      av[a] = *reinterpret_cast<const f4*>(tile + (16 * a + lr) * DS + 16 * gg + 4 * lk);
 #pragma unroll
-      for (int b = 0; b < NK; ++b)
-        xv[gg][b] = load_x4<true, false>(xn, 16 * b + lr, K, sw + 16 * gg + 4 * lk, s_hi, S, 0, 0);
-    if (PRO) {
-#pragma unroll
-      for (int jr = 0; jr < JR; ++jr) {
-        const int j = 4 * jr + lk;
-        f4 yv = f4{0.f, 0.f, 0.f, 0.f};
-        if (j < J && sd < s_hi) yv = *reinterpret_cast<const f4*>(yn + (long long)j * S + sd);
-        const float* c = coef + j * 8;
-        const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
-        const bool ok = j < J && sd < s_hi;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) g[jr][q] = ok ? f * (g[jr][q] - M1 - (yv[q] - mu) * rs * M2) : 0.f;
-      }
-    }
-#pragma unroll
-    for (int jr = 0; jr < JR; ++jr)
-      *reinterpret_cast<f4*>(tile + (4 * jr + lk) * DS + 4 * lr) = g[jr];
-    // data gradient, one 16-row tile of dX at a time
-#pragma unroll
-    for (int kt = 0; kt < NK; ++kt) {
-      f4 acc[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int jr = 0; jr < JR; ++jr) {
-        const float a = w_l[(4 * jr + lk) * WS + 16 * kt + lr];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = mfma4(a, g[jr][q], acc[q]);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int k = 16 * kt + 4 * lk + r;
-        if (k < K && sd < s_hi) {
-          float* dst = dxn + (long long)k * S + sd;
-          f4 v = f4{acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
-          if (accumulate) v += *reinterpret_cast<const f4*>(dst);
-          *reinterpret_cast<f4*>(dst) = v;
-        }
-      }
-    }
-    // weight gradient: dY rows back from the wave's LDS tile in the A layout
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      f4 av[NJ];
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int a = 0; a < NJ; ++a)
-        av[a] = *reinterpret_cast<const f4*>(tile + (16 * a + lr) * DS + 16 * gg + 4 * lk);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int a = 0; a < NJ; ++a)
-#pragma unroll
-          for (int b = 0; b < NK; ++b) gw[a][b] = mfma4(av[a][q], xv[gg][b][q], gw[a][b]);
-    }
-    __builtin_amdgcn_wave_barrier();
+        for (int b = 0; b < NK; ++b) gw[a][b] = mfma4(av[a][q], xv[gg][b][q], gw[a][b]);
   }
-  // fixed-order cross-wave reduction of the weight-gradient partial (reuses the dY tiles)
+
+  // 6. fixed-order cross-wave reduction (reuses the dY tiles): every wave parks its partial
+  // tile, wave 0 adds them in wave order
   __syncthreads();
   float* red = &dyt[0][0];
-  for (int wv = 0; wv < 4; ++wv) {
-    if (wave == wv) {
 #pragma unroll
-      for (int a = 0; a < NJ; ++a)
+  for (int a = 0; a < NJ; ++a)
 #pragma unroll
-        for (int b = 0; b < NK; ++b)
+    for (int b = 0; b < NK; ++b)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int idx = ((a * NK + b) * 4 + r) * 64 + l;
-            red[idx] = wv == 0 ? gw[a][b][r] : red[idx] + gw[a][b][r];
-          }
-    }
-    __syncthreads();
-  }
+      for (int r = 0; r < 4; ++r) red[((wave * NJ + a) * NK + b) * 256 + r * 64 + l] = gw[a][b][r];
+  __syncthreads();
   if (wave == 0) {
     float* o = part + (long long)blockIdx.x * J * K;
 #pragma unroll
@@ -655,8 +678,10 @@ __global__ __launch_bounds__(256) void pw_bwd_fused_kernel(
       for (int b = 0; b < NK; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int jj = 16 * a + 4 * lk + r, kk = 16 * b + lr;
-          if (jj < J && kk < K) o[(long long)jj * K + kk] = red[((a * NK + b) * 4 + r) * 64 + l];
+          float v = red[(a * NK + b) * 256 + r * 64 + l];
+          for (int wv = 1; wv < nwv; ++wv) v += red[((wv * NJ + a) * NK + b) * 256 + r * 64 + l];
+          const int jj = 16 * a + 4 * lk + r, kk = k0 + 16 * b + lr;
+          if (jj < J && kk < K) o[(long long)jj * K + kk] = v;
         }
   }
 }
@@ -815,6 +840,10 @@ int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, lon
   return pw_bwd_weight_launch(dy, dy_nstride, x, x_nstride, part, N, J, K, S, false, 0, 0, stream);
 }
 
+#ifndef L3U_PWBF_MIN_BLOCKS
+#define L3U_PWBF_MIN_BLOCKS 512
+#endif
+
 int l3u_pw_bwd_supported(int J, int K, int S) {
   return (J > 0 && J <= 32 && K > 0 && K <= 64 && S > 0 && S % 4 == 0) ? 1 : 0;
 }
@@ -831,14 +860,19 @@ int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long 
                   (y == nullptr || (((uintptr_t)y & 15) == 0 && y_nstride % 4 == 0));
   L3U_REQUIRE(al);
   const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
-  const int NJ = J <= 16 ? 1 : 2, NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
-  dim3 grid(N * nsc), block(256);
+  const int NJ = J <= 16 ? 1 : 2;
+  // K columns per workgroup: all of them unless the grid would be too small to fill the chip
+  int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
+  while (NK > 1 && (long long)N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < L3U_PWBF_MIN_BLOCKS) NK >>= 1;
+  const int nwv = SCH / 64;
+  L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);   // one sweep of the chunk per workgroup
+  dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
 #define PWBF(A_, B_) do { if (y) hipLaunchKernelGGL((pw_bwd_fused_kernel<A_, B_, 1>), grid, block, 0, \
       stream, dy, dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, \
-      accumulate, part, J, K, S, SCH, nsc); \
+      accumulate, part, N, J, K, S, SCH, nsc); \
     else hipLaunchKernelGGL((pw_bwd_fused_kernel<A_, B_, 0>), grid, block, 0, stream, dy, dy_nstride, \
-      y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, accumulate, part, J, K, S, \
-      SCH, nsc); } while (0)
+      y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, accumulate, part, N, J, K, \
+      S, SCH, nsc); } while (0)
   if (NJ == 1 && NK == 1) PWBF(1, 1);
   else if (NJ == 1 && NK == 2) PWBF(1, 2);
   else if (NJ == 1 && NK == 4) PWBF(1, 4);
