@@ -99,13 +99,17 @@ int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, lon
 
 /* fused backward of the same 1x1 conv (Y = W X, W = w[j*K + k], torch weight [J][K]) in one
  * pass over dY: dx[n][k][s] = sum_j W[j][k] dY[n][j][s] (accumulate != 0: dx += ...) and
- * part[N*nsc][J][K] weight-gradient partials (same layout and count as l3u_pw_bwd_weight).
+ * part[l3u_pw_bwd_nparts(N, J, K, S)][J][K] weight-gradient partials (summed over the first
+ * index they give the gradient).
  * y != NULL: dy holds dpre of the preceding InstanceNorm and dY is formed on the fly as
  * l3u_in_bwd_apply would (rec / in_part[J][N][npart][2] as for that call); dY is not stored.
  * Replaces the autograd backward of DepthwiseSeparableConv3d.pointwise (unet3d.py:18) and of the
  * shortcut conv (unet3d.py:70-73), with the InstanceNorm backward of unet3d.py:51 folded in.
- * Supported shapes: l3u_pw_bwd_supported(J, K, S) != 0 (J <= 32, K <= 64, S % 4 == 0).         */
+ * Supported shapes: l3u_pw_bwd_supported(J, K, S) != 0: S % 4 == 0 and either J <= 32, K <= 64
+ * (one workgroup per voxel chunk) or J in {64, 128}, any K (one per 64-voxel tile and 16 columns
+ * of K, for the small latency-bound levels).                                                     */
 int l3u_pw_bwd_supported(int J, int K, int S);
+int l3u_pw_bwd_nparts(int N, int J, int K, int S);
 int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long y_nstride,
                const float* rec, const double* in_part, int npart, const float* x,
                long long x_nstride, const float* w, float* dx, long long dx_nstride, int accumulate,

@@ -686,6 +686,157 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   }
 }
 
+// Fused 1x1-conv backward for wide J (J = 64 * JT, the 12^3 / 6^3 levels, latency-bound): one
+// workgroup per (64-voxel tile, 16 columns of K).  Wave w owns the dY rows [w*16*JT, +16*JT):
+// it forms its share of the data gradient (split-J partial, combined across the 4 waves through
+// LDS in wave order) and the weight-gradient rows of the same dY rows over the tile.  dY is read
+// in both MFMA layouts straight from global (the second read hits L1/L2; each wave needs only its
+// own rows), PRO 1 applies the InstanceNorm backward to both.  Partials are per 64-voxel tile:
+// part[N * ceil(S/64)][J][K].
+template <int JT, int PRO>
+__global__ __launch_bounds__(256) void pw_bwd_wide_kernel(
+    const float* __restrict__ dy, long long dyns, const float* __restrict__ yin, long long yns,
+    const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
+    const float* __restrict__ x, long long xns, const float* __restrict__ w,
+    float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part, int N, int J,
+    int K, int S) {
+  constexpr int JW = 16 * JT;                 // dY rows per wave
+  __shared__ __attribute__((aligned(16))) float coef[PRO ? 128 * 8 : 1];
+  __shared__ __attribute__((aligned(16))) float red[4][16 * 64];
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
+  const int ntile = (S + 63) / 64;
+  const int tile = blockIdx.x % ntile, n = blockIdx.x / ntile, k0 = blockIdx.y * 16;
+  const int v0 = tile * 64, jb = wave * JW;
+  const float* dyn = dy + (long long)n * dyns;
+  const float* xn = x + (long long)n * xns;
+
+  // streamed loads first: dY in the data-gradient B layout (rows jb + 4jr + lk, voxels
+  // v0 + 4lr..), dY in the weight-gradient A layout (rows jb + 16t + lr, voxels v0 + 16g + 4lk..),
+  // X in the B layout (rows k0 + lr), the weights W[jb + 4jr + lk][k0 + lr]
+  f4 gd[JT * 4], ga[JT][4], yd[PRO ? JT * 4 : 1], ya[PRO ? JT : 1][4], xb[4];
+  float wa[JT * 4];
+  const int vd = v0 + 4 * lr;
+#pragma unroll
+  for (int jr = 0; jr < JT * 4; ++jr) {
+    const int j = jb + 4 * jr + lk;
+    gd[jr] = f4{0.f, 0.f, 0.f, 0.f};
+    if (vd < S) gd[jr] = *reinterpret_cast<const f4*>(dyn + (long long)j * S + vd);
+    const int k = k0 + lr;
+    wa[jr] = k < K ? w[(long long)j * K + k] : 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < JT; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int j = jb + 16 * t + lr, v = v0 + 16 * g + 4 * lk;
+      ga[t][g] = f4{0.f, 0.f, 0.f, 0.f};
+      if (v < S) ga[t][g] = *reinterpret_cast<const f4*>(dyn + (long long)j * S + v);
+    }
+  if (PRO) {
+    const float* yn = yin + (long long)n * yns;
+#pragma unroll
+    for (int jr = 0; jr < JT * 4; ++jr) {
+      const int j = jb + 4 * jr + lk;
+      yd[jr] = f4{0.f, 0.f, 0.f, 0.f};
+      if (vd < S) yd[jr] = *reinterpret_cast<const f4*>(yn + (long long)j * S + vd);
+    }
+#pragma unroll
+    for (int t = 0; t < JT; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int j = jb + 16 * t + lr, v = v0 + 16 * g + 4 * lk;
+        ya[t][g] = f4{0.f, 0.f, 0.f, 0.f};
+        if (v < S) ya[t][g] = *reinterpret_cast<const f4*>(yn + (long long)j * S + v);
+      }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    xb[g] = load_x4<true, false>(xn, k0 + lr, K, v0 + 16 * g + 4 * lk, S, S, 0, 0);
+
+  if (PRO) {   // per-row InstanceNorm-backward coefficients (rows < J <= 128)
+    if (tid < J) {
+      double t[2];
+      seq_sum<2>(in_part + ((long long)tid * N + n) * npart * 2, npart, t);
+      const float* q = rec + ((long long)n * J + tid) * kRec;
+      float* o = coef + tid * 8;
+      o[0] = q[1] * q[5];
+      o[1] = (float)(t[0] / S);
+      o[2] = q[0];
+      o[3] = q[1];
+      o[4] = (float)(t[1] / S);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int jr = 0; jr < JT * 4; ++jr) {
+      const float* c = coef + (jb + 4 * jr + lk) * 8;
+      const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        gd[jr][q] = vd < S ? f * (gd[jr][q] - M1 - (yd[jr][q] - mu) * rs * M2) : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      const float* c = coef + (jb + 16 * t + lr) * 8;
+      const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const bool ok = v0 + 16 * g + 4 * lk < S;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          ga[t][g][q] = ok ? f * (ga[t][g][q] - M1 - (ya[t][g][q] - mu) * rs * M2) : 0.f;
+      }
+    }
+  }
+
+  // data gradient: this wave's split-J partial of dX[k0 + 4lk + r][vd + q]
+  f4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int jr = 0; jr < JT * 4; ++jr)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = mfma4(wa[jr], gd[jr][q], acc[q]);
+  // weight gradient of the wave's rows over the tile
+  f4 gw[JT];
+#pragma unroll
+  for (int t = 0; t < JT; ++t) {
+    gw[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gw[t] = mfma4(ga[t][g][q], xb[g][q], gw[t]);
+  }
+  float* o = part + (long long)blockIdx.x * J * K;
+#pragma unroll
+  for (int t = 0; t < JT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = jb + 16 * t + 4 * lk + r, k = k0 + lr;
+      if (k < K) o[(long long)j * K + k] = gw[t][r];
+    }
+  // combine the 4 split-J partials in wave order; wave w then stores rows r == w of each lane
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][(q * 4 + r) * 64 + l] = acc[q][r];
+  __syncthreads();
+  {
+    const int r = wave;
+    const int k = k0 + 4 * lk + r;
+    f4 v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = (q * 4 + r) * 64 + l;
+      v[q] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+    }
+    if (k < K && vd < S) {
+      float* dst = dx + (long long)n * dxns + (long long)k * S + vd;
+      if (accumulate) v += *reinterpret_cast<const f4*>(dst);
+      *reinterpret_cast<f4*>(dst) = v;
+    }
+  }
+}
+
 #ifndef L3U_PW_SCH_MAX
 #define L3U_PW_SCH_MAX 512
 #endif
@@ -844,8 +995,17 @@ int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, lon
 #define L3U_PWBF_MIN_BLOCKS 512
 #endif
 
+// wide form: J a multiple of 64 (<= 128), any K; narrow form: J <= 32, K <= 64
+bool pw_bwd_wide(int J) { return J == 64 || J == 128; }
+
 int l3u_pw_bwd_supported(int J, int K, int S) {
-  return (J > 0 && J <= 32 && K > 0 && K <= 64 && S > 0 && S % 4 == 0) ? 1 : 0;
+  if (!(J > 0 && K > 0 && S > 0 && S % 4 == 0)) return 0;
+  return (pw_bwd_wide(J) || (J <= 32 && K <= 64)) ? 1 : 0;
+}
+
+int l3u_pw_bwd_nparts(int N, int J, int K, int S) {
+  if (!l3u_pw_bwd_supported(J, K, S)) return 0;
+  return pw_bwd_wide(J) ? N * ((S + 63) / 64) : l3u_pw_bwd_weight_nparts(N, S);
 }
 
 int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long y_nstride,
@@ -859,6 +1019,16 @@ int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long 
                   (dx_nstride % 4 == 0) &&
                   (y == nullptr || (((uintptr_t)y & 15) == 0 && y_nstride % 4 == 0));
   L3U_REQUIRE(al);
+  if (pw_bwd_wide(J)) {
+    dim3 grid(N * ((S + 63) / 64), (K + 15) / 16), block(256);
+#define PWBW(T_, P_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T_, P_>), grid, block, 0, stream, dy, \
+      dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, accumulate, \
+      part, N, J, K, S)
+    if (J == 64) { if (y) PWBW(1, 1); else PWBW(1, 0); }
+    else { if (y) PWBW(2, 1); else PWBW(2, 0); }
+#undef PWBW
+    L3U_CHECK_LAUNCH();
+  }
   const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
   const int NJ = J <= 16 ? 1 : 2;
   // K columns per workgroup: all of them unless the grid would be too small to fill the chip

@@ -32,6 +32,7 @@ _SIGS = {
     "l3u_pw_bwd_weight_nparts": [I, I],
     "l3u_pw_bwd_weight": [P, L, P, L, P, I, I, I, I, P],
     "l3u_pw_bwd_supported": [I, I, I],
+    "l3u_pw_bwd_nparts": [I, I, I, I],
     "l3u_pw_bwd": [P, L, P, L, P, P, I, P, L, P, P, L, I, P, I, I, I, I, P],
     "l3u_in_finalize": [P, I, P, P, F, U64, P, I, P, I, I, P],
     "l3u_norm_act_nblocks": [I],
@@ -63,7 +64,7 @@ _SIGS = {
 }
 # query helpers that return a value instead of an error code
 _QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_weight_nparts",
-            "l3u_pw_bwd_supported",
+            "l3u_pw_bwd_supported", "l3u_pw_bwd_nparts",
             "l3u_norm_act_nblocks", "l3u_chan_sum_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks"}
 
 _lib = None

@@ -444,12 +444,8 @@ class UNetEngine:
                    cout * S, drv.p, drv.ns, N, cout, S, st)
         # (2) conv2.pointwise backward
         dz2 = e(N, cout, S)
-        npw = nat.query("l3u_pw_bwd_weight_nparts", N, S)
-        pp2 = A.alloc(npw * cout * cout)
-        self._pw_bwd(V(dy2, 0, cout * S, cout), None, V(z2, 0, cout * S, cout),
-                     self._w(flat, pre + "conv2.pointwise.weight"), V(dz2, 0, cout * S, cout), 0,
-                     A.ptr(pp2), N, S, st)
-        self._seg(pp2, npw, cout * cout, 1, cout * cout, pre + "conv2.pointwise.weight")
+        self._pw_bwd(flat, V(dy2, 0, cout * S, cout), None, V(z2, 0, cout * S, cout),
+                     pre + "conv2.pointwise.weight", V(dz2, 0, cout * S, cout), 0, N, S, st)
         # (3) conv2.depthwise backward fused with LeakyReLU/Dropout/IN1 backward partials
         nch = nat.query("l3u_dw3_nchunk", N, cout, d, h, w)
         pd2 = A.alloc(cout * N * nch * 27)
@@ -465,19 +461,17 @@ class UNetEngine:
         # (4) conv1.pointwise backward, with the IN1 backward (dy1 from dpre) folded in when the
         # fused kernel takes the shape
         dz1 = e(N, cin, S)
-        pp1 = A.alloc(npw * cout * cin)
         dpv = V(dpre, 0, cout * S, cout)
-        w1 = self._w(flat, pre + "conv1.pointwise.weight")
+        name1 = pre + "conv1.pointwise.weight"
         if nat.query("l3u_pw_bwd_supported", cout, cin, S):
-            self._pw_bwd(dpv, (y1.data_ptr(), cout * S, rec1, A.ptr(pi1), nch),
-                         V(z1, 0, cin * S, cin), w1, V(dz1, 0, cin * S, cin), 0, A.ptr(pp1), N, S, st)
+            self._pw_bwd(flat, dpv, (y1.data_ptr(), cout * S, rec1, A.ptr(pi1), nch),
+                         V(z1, 0, cin * S, cin), name1, V(dz1, 0, cin * S, cin), 0, N, S, st)
         else:
             self._call("l3u_in_bwd_apply", dpre.data_ptr(), cout * S, y1.data_ptr(), cout * S, rec1,
                        A.ptr(pi1), nch, dpre.data_ptr(), cout * S, N, cout, S, st)
-            self._pw_bwd(dpv, None, V(z1, 0, cin * S, cin), w1, V(dz1, 0, cin * S, cin), 0,
-                         A.ptr(pp1), N, S, st)
+            self._pw_bwd(flat, dpv, None, V(z1, 0, cin * S, cin), name1, V(dz1, 0, cin * S, cin), 0,
+                         N, S, st)
         dy1 = dpre
-        self._seg(pp1, npw, cout * cin, 1, cout * cin, pre + "conv1.pointwise.weight")
         # (5) conv1.depthwise backward: writes d(input) (Conv1x1 shortcut) or accumulates into the
         # identity-shortcut gradient already there
         nch1 = nat.query("l3u_dw3_nchunk", N, cin, d, h, w)
@@ -488,28 +482,33 @@ class UNetEngine:
         self._seg_dw(pd1, N * nch1, cin, pre + "conv1.depthwise.weight")
         # (6) shortcut conv backward accumulates into d(input)
         if shortcut:
-            ppr = A.alloc(npw * cout * cin)
-            self._pw_bwd(drv, None, x, self._w(flat, pre + "shortcut.0.weight"), dxv, 1, A.ptr(ppr),
-                         N, S, st)
-            self._seg(ppr, npw, cout * cin, 1, cout * cin, pre + "shortcut.0.weight")
+            self._pw_bwd(flat, drv, None, x, pre + "shortcut.0.weight", dxv, 1, N, S, st)
         if self.debug is not None and not self._dry:
             self.debug[pre + "#"] = {"dy2": dy2, "dr": drv, "dz2": dz2, "dy1": dy1, "dz1": dz1,
                                      "dx": dxv}
 
-    def _pw_bwd(self, dy, pro, x, w, dx, accumulate, part, N, S, st):
-        """Backward of a 1x1 conv y = W x (W [J][K]): dx (+)= W^T dy and weight-gradient partials
-        [nparts][J][K].  pro = (y, y_nstride, rec, in_part, npart): dy holds dpre of the preceding
-        InstanceNorm and the fused kernel applies its backward on the fly."""
+    def _pw_bwd(self, flat, dy, pro, x, name, dx, accumulate, N, S, st):
+        """Backward of a 1x1 conv y = W x (W = parameter `name`, [J][K]): dx (+)= W^T dy, and the
+        weight-gradient partials recorded for the reduction into gflat[name].
+        pro = (y, y_nstride, rec, in_part, npart): dy holds dpre of the preceding InstanceNorm
+        and the fused kernel applies its backward on the fly."""
         J, K = dy.C, x.C
+        w = self._w(flat, name)
+        A = self.bwd_arena
         if nat.query("l3u_pw_bwd_supported", J, K, S):
+            npw = nat.query("l3u_pw_bwd_nparts", N, J, K, S)
+            part = A.alloc(npw * J * K)
             y, yns, rec, ip, npart = pro if pro is not None else (None, 0, None, None, 0)
             self._call("l3u_pw_bwd", dy.p, dy.ns, y, yns, rec, ip, npart, x.p, x.ns, w, dx.p, dx.ns,
-                       accumulate, part, N, J, K, S, st)
-            return
-        assert pro is None
-        self._call("l3u_pw_fwd", dy.p, dy.ns, w, 1, None, dx.p, dx.ns, accumulate, None, N, J, K, S,
-                   st)
-        self._call("l3u_pw_bwd_weight", dy.p, dy.ns, x.p, x.ns, part, N, J, K, S, st)
+                       accumulate, A.ptr(part), N, J, K, S, st)
+        else:
+            assert pro is None
+            npw = nat.query("l3u_pw_bwd_weight_nparts", N, S)
+            part = A.alloc(npw * J * K)
+            self._call("l3u_pw_fwd", dy.p, dy.ns, w, 1, None, dx.p, dx.ns, accumulate, None, N, J, K,
+                       S, st)
+            self._call("l3u_pw_bwd_weight", dy.p, dy.ns, x.p, x.ns, A.ptr(part), N, J, K, S, st)
+        self._seg(part, npw, J * K, 1, J * K, name)
 
     def _seg_dw(self, off, count, C, name):
         # dw_part layout [C][count][27] -> grad [C][27]

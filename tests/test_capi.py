@@ -62,8 +62,15 @@ def test_host_queries_without_gpu():
     assert _native.query("l3u_dw3_nchunk", 4, 32, 48, 48, 48) == 30   # 3 z-slabs x 10 y-strips
     assert _native.query("l3u_pw_bwd_supported", 16, 32, 48 ** 3) == 1
     assert _native.query("l3u_pw_bwd_supported", 32, 64, 24 ** 3) == 1
-    assert _native.query("l3u_pw_bwd_supported", 64, 32, 12 ** 3) == 0
+    assert _native.query("l3u_pw_bwd_supported", 64, 32, 12 ** 3) == 1     # wide form
+    assert _native.query("l3u_pw_bwd_supported", 128, 256, 6 ** 3) == 1
+    assert _native.query("l3u_pw_bwd_supported", 48, 32, 12 ** 3) == 0
+    assert _native.query("l3u_pw_bwd_supported", 16, 128, 12 ** 3) == 0
     assert _native.query("l3u_pw_bwd_supported", 16, 16, 6 * 6 * 7 + 1) == 0
+    assert _native.query("l3u_pw_bwd_nparts", 4, 16, 32, 48 ** 3) == \
+        _native.query("l3u_pw_bwd_weight_nparts", 4, 48 ** 3)
+    assert _native.query("l3u_pw_bwd_nparts", 4, 64, 128, 12 ** 3) == 4 * 27
+    assert _native.query("l3u_pw_bwd_nparts", 4, 48, 32, 12 ** 3) == 0
     assert _native.query("l3u_dw3_nchunk", 4, 32, 24, 24, 24) == 18   # 6 z-slabs x 3 y-strips
     assert _native.query("l3u_dw3_nchunk", 4, 128, 6, 6, 6) == 1
     assert _native.query("l3u_pw_stat_nsb", 16, 16, 48 ** 3) == 432   # 256-voxel tiles

@@ -238,6 +238,11 @@ PW_BWD_CASES = [
     (2, 32, 16, 6 * 6 * 8, False, True),       # shortcut: accumulate into d(input)
     (2, 32, 64, 8 ** 3, True, False),          # up2 conv1 (NJ 2, NK 4)
     (3, 20, 40, 4 * 5 * 12, True, True),       # partial tiles in J and K
+    (2, 64, 32, 12 ** 3, True, False),         # wide form: down2 conv1
+    (2, 64, 128, 12 ** 3, False, True),        # up1 shortcut
+    (2, 128, 128, 6 ** 3, True, False),        # bottleneck conv1
+    (1, 128, 64, 6 ** 3, False, False),
+    (2, 64, 40, 5 * 6 * 8, True, True),        # ragged K, S not a multiple of 64
 ]
 
 
@@ -270,7 +275,7 @@ def test_pw_bwd_fused(cuda, case):
                                                                                             dtype=torch.float64)
     ref_dx = torch.einsum("jk,njs->nks", w, dy) + dx0
     ref_dw = torch.einsum("njs,nks->jk", dy, x)
-    P = nat().query("l3u_pw_bwd_weight_nparts", N, S)
+    P = nat().query("l3u_pw_bwd_nparts", N, J, K, S)
     part = torch.full((P * J * K,), float("nan"), device=cuda)
     xd, wd, dd = x.float().to(cuda), w.float().to(cuda), dpre.float().to(cuda)
     dx = dx0.float().to(cuda) if acc else torch.full((N, K, S), float("nan"), device=cuda)

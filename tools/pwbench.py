@@ -27,6 +27,15 @@ SHAPES = [
     (4, 32, 16, 24, False, True, "down1 shortcut"),
     (4, 32, 64, 24, True, False, "up2 conv1"),
     (4, 32, 64, 24, False, True, "up2 shortcut"),
+    (4, 64, 64, 12, False, False, "down2/up1 conv2"),
+    (4, 64, 32, 12, True, False, "down2 conv1"),
+    (4, 64, 32, 12, False, True, "down2 shortcut"),
+    (4, 64, 128, 12, True, False, "up1 conv1"),
+    (4, 64, 128, 12, False, True, "up1 shortcut"),
+    (4, 128, 128, 6, False, False, "down3/bottleneck conv2"),
+    (4, 128, 64, 6, True, False, "down3 conv1"),
+    (4, 128, 64, 6, False, True, "down3 shortcut"),
+    (4, 128, 128, 6, True, False, "bottleneck conv1"),
 ]
 
 
@@ -69,7 +78,7 @@ def main():
         rec = torch.rand(N * J, 8, device=dev)
         npart = 8
         ip = torch.rand(J * N * npart * 2, dtype=torch.float64, device=dev)
-        P = nat.query("l3u_pw_bwd_weight_nparts", N, S)
+        P = max(nat.query("l3u_pw_bwd_weight_nparts", N, S), nat.query("l3u_pw_bwd_nparts", N, J, K, S))
         part = torch.empty(P * J * K, device=dev)
 
         def fused():

@@ -1,18 +1,21 @@
-"""Per-launch list of one training step from a rocprofv3 kernel trace (kernel, grid, time)."""
+"""Per-launch list of a training step from a rocprofv3 kernel trace: kernel, grid and the
+duration averaged over all complete steps in the trace (steps end at each adamw launch)."""
 import csv
 import re
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-which = int(sys.argv[2]) if len(sys.argv) > 2 else -3
 ends = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
-seg = rows[ends[which] + 1:ends[which + 1] + 1]
+steps = [rows[a + 1:b + 1] for a, b in zip(ends[:-1], ends[1:])]
+n = len(steps[-1])
+steps = [s for s in steps if len(s) == n][1:]          # same launch sequence; drop the first
 tot = 0.0
-for r in seg:
-    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+for i in range(n):
+    r = steps[-1][i]
+    d = sum(int(s[i]["End_Timestamp"]) - int(s[i]["Start_Timestamp"]) for s in steps) / len(steps) / 1e3
     tot += d
-    n = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
-    n = re.sub(r"\(.*", "", n)
-    print(f"{d:7.1f} {n[:44]:44s} {r['Grid_Size_X']}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']}/"
+    name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+    name = re.sub(r"\(.*", "", name)
+    print(f"{d:7.1f} {name[:44]:44s} {r['Grid_Size_X']}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']}/"
           f"{r['Workgroup_Size_X']} v{r['VGPR_Count']}")
-print(f"sum {tot:.1f} us, {len(seg)} launches")
+print(f"sum {tot:.1f} us, {n} launches, mean of {len(steps)} steps")
