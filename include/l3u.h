@@ -178,6 +178,15 @@ int l3u_convt_fwd(const float* x, long long x_nstride, const float* w, const flo
 int l3u_convt_bwd(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
                   const float* w, float* dx, long long dx_nstride, float* wpart, double* bpart,
                   int N, int Ci, int Co, int D, int H, int W, hipStream_t stream);
+/* the same backward as ONE launch (one workgroup per 64 low-res voxels and 16 input channels,
+ * split over Co*8 rows by wave): dx, wpart[P][Ci][Co*8] and bpart[P][Co] (fp32) partials with
+ * P = l3u_convt_bwd_fused_nparts(...) (0: shape not offered -> use l3u_convt_bwd; offered for
+ * Co in {8, 16, 32, 64}, W % 4 == 0 and D*H*W <= 8192, where it beats the three-launch form).
+ * Replaces the autograd backward of UpBlock.up (unet3d.py:119).                              */
+int l3u_convt_bwd_fused_nparts(int N, int Ci, int Co, int D, int H, int W);
+int l3u_convt_bwd_fused(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
+                        const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
+                        int N, int Ci, int Co, int D, int H, int W, hipStream_t stream);
 int l3u_convt_s2d(const float* dy, long long dy_nstride, float* dyp, int N, int Co, int D, int H,
                   int W, hipStream_t stream);
 /* per-channel sums part[C][N][nblocks] (fp64; bias gradients)                                */

@@ -686,23 +686,30 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   }
 }
 
-// Fused 1x1-conv backward for wide J (J = 64 * JT, the 12^3 / 6^3 levels, latency-bound): one
-// workgroup per (64-voxel tile, 16 columns of K).  Wave w owns the dY rows [w*16*JT, +16*JT):
-// it forms its share of the data gradient (split-J partial, combined across the 4 waves through
-// LDS in wave order) and the weight-gradient rows of the same dY rows over the tile.  dY is read
-// in both MFMA layouts straight from global (the second read hits L1/L2; each wave needs only its
-// own rows), PRO 1 applies the InstanceNorm backward to both.  Partials are per 64-voxel tile:
-// part[N * ceil(S/64)][J][K].
-template <int JT, int PRO>
-__global__ __launch_bounds__(256) void pw_bwd_wide_kernel(
+// Fused 1x1-conv backward for wide J (J = 16 * JT * NWV: 64 / 128 for the 12^3 / 6^3 levels,
+// and the ConvTranspose3d(k2, s2) backward, J = Co*8 up to 512), latency-bound shapes: one
+// workgroup of NWV waves per (64-voxel tile, 16 columns of K).  Wave w owns the dY rows
+// [w*16*JT, +16*JT): it forms its share of the data gradient (split-J partial, combined across the
+// waves through LDS in wave order) and the weight-gradient rows of the same dY rows over the
+// tile.  dY is read in both MFMA layouts straight from global (the second read hits L1/L2; each
+// wave needs only its own rows); PRO 1 applies the InstanceNorm backward to both.
+// GATHER 1/2 (ConvTranspose3d): dY row j = co*8 + abc is read in place from the up-sampled
+// gradient (load_x4 GATHER; 2 = scalar gathers for W % 4 != 0); the weights are stored W[k][j]
+// (the ConvTranspose3d weight [Ci][Co*8]) and so are the partials; bpart != NULL receives the
+// bias partials sum_{tile, abc} dY[co] per (tile, co) from the K-tile-0 workgroups.
+// Partials are per 64-voxel tile: part[N * ceil(S/64)][J][K] ([K][J] for GATHER).
+template <int JT, int NWV, int PRO, int GATHER>
+__global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
     const float* __restrict__ dy, long long dyns, const float* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
     const float* __restrict__ x, long long xns, const float* __restrict__ w,
-    float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part, int N, int J,
-    int K, int S) {
+    float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part,
+    float* __restrict__ bpart, int N, int J, int K, int S, int Hq, int Wq) {
   constexpr int JW = 16 * JT;                 // dY rows per wave
+  constexpr bool GV = GATHER != 2;            // vector loads
+  constexpr bool G = GATHER != 0;
   __shared__ __attribute__((aligned(16))) float coef[PRO ? 128 * 8 : 1];
-  __shared__ __attribute__((aligned(16))) float red[4][16 * 64];
+  __shared__ __attribute__((aligned(16))) float red[NWV][16 * 64];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const int ntile = (S + 63) / 64;
   const int tile = blockIdx.x % ntile, n = blockIdx.x / ntile, k0 = blockIdx.y * 16;
@@ -719,39 +726,28 @@ __global__ __launch_bounds__(256) void pw_bwd_wide_kernel(
 #pragma unroll
   for (int jr = 0; jr < JT * 4; ++jr) {
     const int j = jb + 4 * jr + lk;
-    gd[jr] = f4{0.f, 0.f, 0.f, 0.f};
-    if (vd < S) gd[jr] = *reinterpret_cast<const f4*>(dyn + (long long)j * S + vd);
+    gd[jr] = load_x4<GV, G>(dyn, j, J, vd, S, S, Hq, Wq);
     const int k = k0 + lr;
-    wa[jr] = k < K ? w[(long long)j * K + k] : 0.f;
+    wa[jr] = k < K ? (G ? w[(long long)k * J + j] : w[(long long)j * K + k]) : 0.f;
   }
 #pragma unroll
   for (int t = 0; t < JT; ++t)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int j = jb + 16 * t + lr, v = v0 + 16 * g + 4 * lk;
-      ga[t][g] = f4{0.f, 0.f, 0.f, 0.f};
-      if (v < S) ga[t][g] = *reinterpret_cast<const f4*>(dyn + (long long)j * S + v);
-    }
+    for (int g = 0; g < 4; ++g)
+      ga[t][g] = load_x4<GV, G>(dyn, jb + 16 * t + lr, J, v0 + 16 * g + 4 * lk, S, S, Hq, Wq);
   if (PRO) {
     const float* yn = yin + (long long)n * yns;
 #pragma unroll
-    for (int jr = 0; jr < JT * 4; ++jr) {
-      const int j = jb + 4 * jr + lk;
-      yd[jr] = f4{0.f, 0.f, 0.f, 0.f};
-      if (vd < S) yd[jr] = *reinterpret_cast<const f4*>(yn + (long long)j * S + vd);
-    }
+    for (int jr = 0; jr < JT * 4; ++jr) yd[jr] = load_x4<true, false>(yn, jb + 4 * jr + lk, J, vd, S, S, 0, 0);
 #pragma unroll
     for (int t = 0; t < JT; ++t)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int j = jb + 16 * t + lr, v = v0 + 16 * g + 4 * lk;
-        ya[t][g] = f4{0.f, 0.f, 0.f, 0.f};
-        if (v < S) ya[t][g] = *reinterpret_cast<const f4*>(yn + (long long)j * S + v);
-      }
+      for (int g = 0; g < 4; ++g)
+        ya[t][g] = load_x4<true, false>(yn, jb + 16 * t + lr, J, v0 + 16 * g + 4 * lk, S, S, 0, 0);
   }
 #pragma unroll
   for (int g = 0; g < 4; ++g)
-    xb[g] = load_x4<true, false>(xn, k0 + lr, K, v0 + 16 * g + 4 * lk, S, S, 0, 0);
+    xb[g] = load_x4<GV, false>(xn, k0 + lr, K, v0 + 16 * g + 4 * lk, S, S, 0, 0);
 
   if (PRO) {   // per-row InstanceNorm-backward coefficients (rows < J <= 128)
     if (tid < J) {
@@ -772,7 +768,7 @@ __global__ __launch_bounds__(256) void pw_bwd_wide_kernel(
       const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        gd[jr][q] = vd < S ? f * (gd[jr][q] - M1 - (yd[jr][q] - mu) * rs * M2) : 0.f;
+        gd[jr][q] = vd + q < S ? f * (gd[jr][q] - M1 - (yd[jr][q] - mu) * rs * M2) : 0.f;
     }
 #pragma unroll
     for (int t = 0; t < JT; ++t) {
@@ -780,10 +776,10 @@ __global__ __launch_bounds__(256) void pw_bwd_wide_kernel(
       const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const bool ok = v0 + 16 * g + 4 * lk < S;
+        const int v = v0 + 16 * g + 4 * lk;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          ga[t][g][q] = ok ? f * (ga[t][g][q] - M1 - (ya[t][g][q] - mu) * rs * M2) : 0.f;
+          ga[t][g][q] = v + q < S ? f * (ga[t][g][q] - M1 - (ya[t][g][q] - mu) * rs * M2) : 0.f;
       }
     }
   }
@@ -812,27 +808,54 @@ __global__ __launch_bounds__(256) void pw_bwd_wide_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = jb + 16 * t + 4 * lk + r, k = k0 + lr;
-      if (k < K) o[(long long)j * K + k] = gw[t][r];
+      if (k < K) o[G ? (long long)k * J + j : (long long)j * K + k] = gw[t][r];
     }
-  // combine the 4 split-J partials in wave order; wave w then stores rows r == w of each lane
+  if (G && bpart != nullptr && blockIdx.y == 0) {
+    // bias partial of co = j / 8: row sums over the tile (lanes lk), then the 8 rows abc of
+    // each co (lanes lr & 7), both in a fixed xor-tree order
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      float sum = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) sum += (ga[t][g][0] + ga[t][g][1]) + (ga[t][g][2] + ga[t][g][3]);
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      sum += __shfl_xor(sum, 1, 64);
+      sum += __shfl_xor(sum, 2, 64);
+      sum += __shfl_xor(sum, 4, 64);
+      if (lk == 0 && (lr & 7) == 0) bpart[(long long)blockIdx.x * (J / 8) + (jb + 16 * t + lr) / 8] = sum;
+    }
+  }
+  // combine the NWV split-J partials in wave order; waves 0..3 then store rows r == wave
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][(q * 4 + r) * 64 + l] = acc[q][r];
   __syncthreads();
-  {
+  if (wave < 4) {
     const int r = wave;
     const int k = k0 + 4 * lk + r;
     f4 v;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = (q * 4 + r) * 64 + l;
-      v[q] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+      float sum = red[0][i];
+#pragma unroll
+      for (int wv = 1; wv < NWV; ++wv) sum += red[wv][i];
+      v[q] = sum;
     }
-    if (k < K && vd < S) {
+    if (k < K) {
       float* dst = dx + (long long)n * dxns + (long long)k * S + vd;
-      if (accumulate) v += *reinterpret_cast<const f4*>(dst);
-      *reinterpret_cast<f4*>(dst) = v;
+      if (GV) {
+        if (vd < S) {
+          if (accumulate) v += *reinterpret_cast<const f4*>(dst);
+          *reinterpret_cast<f4*>(dst) = v;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (vd + q < S) dst[q] = accumulate ? dst[q] + v[q] : v[q];
+      }
     }
   }
 }
@@ -991,12 +1014,18 @@ int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, lon
   return pw_bwd_weight_launch(dy, dy_nstride, x, x_nstride, part, N, J, K, S, false, 0, 0, stream);
 }
 
+#ifndef L3U_CONVT_ONEPASS_MAX_S
+#define L3U_CONVT_ONEPASS_MAX_S 8192
+#endif
 #ifndef L3U_PWBF_MIN_BLOCKS
 #define L3U_PWBF_MIN_BLOCKS 512
 #endif
 
 // wide form: J a multiple of 64 (<= 128), any K; narrow form: J <= 32, K <= 64
-bool pw_bwd_wide(int J) { return J == 64 || J == 128; }
+#ifndef L3U_PW_BWD_WIDE
+#define L3U_PW_BWD_WIDE 1
+#endif
+bool pw_bwd_wide(int J) { return L3U_PW_BWD_WIDE && (J == 64 || J == 128); }
 
 int l3u_pw_bwd_supported(int J, int K, int S) {
   if (!(J > 0 && K > 0 && S > 0 && S % 4 == 0)) return 0;
@@ -1021,9 +1050,9 @@ int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long 
   L3U_REQUIRE(al);
   if (pw_bwd_wide(J)) {
     dim3 grid(N * ((S + 63) / 64), (K + 15) / 16), block(256);
-#define PWBW(T_, P_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T_, P_>), grid, block, 0, stream, dy, \
-      dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, accumulate, \
-      part, N, J, K, S)
+#define PWBW(T_, P_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T_, 4, P_, 0>), grid, block, 0, stream, \
+      dy, dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, \
+      accumulate, part, nullptr, N, J, K, S, 0, 0)
     if (J == 64) { if (y) PWBW(1, 1); else PWBW(1, 0); }
     else { if (y) PWBW(2, 1); else PWBW(2, 0); }
 #undef PWBW
@@ -1050,6 +1079,39 @@ int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long 
   else if (NJ == 2 && NK == 2) PWBF(2, 2);
   else PWBF(2, 4);
 #undef PWBF
+  L3U_CHECK_LAUNCH();
+}
+
+// fused ConvTranspose3d backward: Co*8 = 16 * 2 * NWV rows (Co in {8, 16, 32, 64}).  Offered for
+// the mid-size levels only (measured, tools/pwbench.py --convt-only): at 24^3 the three-launch
+// path is as fast (the gathered A-layout reads coalesce poorly at that volume) and at 6^3
+// (W % 4 != 0: scalar gathers) it is faster.
+int l3u_convt_bwd_fused_nparts(int N, int Ci, int Co, int D, int H, int W) {
+  if (!(N > 0 && Ci > 0 && (Co == 8 || Co == 16 || Co == 32 || Co == 64) && D > 0 && H > 0 && W > 0))
+    return 0;
+  if (W % 4 != 0 || D * H * W > L3U_CONVT_ONEPASS_MAX_S) return 0;
+  return N * ((D * H * W + 63) / 64);
+}
+
+int l3u_convt_bwd_fused(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
+                        const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
+                        int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
+  L3U_REQUIRE(l3u_convt_bwd_fused_nparts(N, Ci, Co, D, H, W) > 0 && dy && x && w && dx && wpart);
+  const int S = D * H * W, J = Co * 8;
+  const bool vec = W % 4 == 0 && S % 4 == 0 && dy_nstride % 4 == 0 && x_nstride % 4 == 0 &&
+                   dx_nstride % 4 == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
+                   ((uintptr_t)dx & 15) == 0;
+  dim3 grid(N * ((S + 63) / 64), (Ci + 15) / 16);
+#define CTB(T_, NW_, G_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T_, NW_, 0, G_>), grid, dim3(64 * NW_), \
+      0, stream, dy, dy_nstride, nullptr, 0, nullptr, nullptr, 0, x, x_nstride, w, dx, dx_nstride, 0, \
+      wpart, bpart, N, J, Ci, S, H, W)
+#define CTB_G(T_, NW_) do { if (vec) CTB(T_, NW_, 1); else CTB(T_, NW_, 2); } while (0)
+  if (J == 64) CTB_G(1, 4);
+  else if (J == 128) CTB_G(2, 4);
+  else if (J == 256) CTB_G(2, 8);
+  else CTB_G(2, 16);
+#undef CTB_G
+#undef CTB
   L3U_CHECK_LAUNCH();
 }
 

@@ -45,6 +45,8 @@ _SIGS = {
     "l3u_convt_d2s": [P, P, P, L, I, I, I, I, I, P],
     "l3u_convt_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, P],
     "l3u_convt_bwd": [P, L, P, L, P, P, L, P, P, I, I, I, I, I, I, P],
+    "l3u_convt_bwd_fused_nparts": [I, I, I, I, I, I],
+    "l3u_convt_bwd_fused": [P, L, P, L, P, P, L, P, P, I, I, I, I, I, I, P],
     "l3u_convt_s2d": [P, L, P, I, I, I, I, I, P],
     "l3u_chan_sum_nblocks": [L],
     "l3u_chan_sum": [P, L, P, I, I, L, P],
@@ -64,7 +66,7 @@ _SIGS = {
 }
 # query helpers that return a value instead of an error code
 _QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_weight_nparts",
-            "l3u_pw_bwd_supported", "l3u_pw_bwd_nparts",
+            "l3u_pw_bwd_supported", "l3u_pw_bwd_nparts", "l3u_convt_bwd_fused_nparts",
             "l3u_norm_act_nblocks", "l3u_chan_sum_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks"}
 
 _lib = None

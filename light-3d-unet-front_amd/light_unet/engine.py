@@ -369,16 +369,25 @@ class UNetEngine:
             ci = prev.C
             d, hh, w = dims[lvl + 1]
             dprev = e(N, ci, S[lvl + 1])
-            npw = nat.query("l3u_pw_bwd_weight_nparts", N, S[lvl + 1])
-            pw = A.alloc(npw * ci * co * 8)
-            ncs = nat.query("l3u_chan_sum_nblocks", 8 * S[lvl + 1])
-            pb = A.alloc(2 * co * N * ncs)            # fp64 partials
             # dY read in place from the lower half of the concat gradient
-            self._call("l3u_convt_bwd", dcat.data_ptr(), 2 * co * S[lvl], prev.p, prev.ns,
-                       self._w(flat, up + "up.weight"), dprev.data_ptr(), ci * S[lvl + 1], A.ptr(pw),
-                       A.ptr(pb), N, ci, co, d, hh, w, st)
-            self._seg(pw, npw, ci * co * 8, 1, ci * co * 8, up + "up.weight")
-            self._seg(pb // 2, N * ncs, 1, N * ncs, co, up + "up.bias", f64=1)
+            npf = nat.query("l3u_convt_bwd_fused_nparts", N, ci, co, d, hh, w)
+            if npf > 0:   # one launch: data, weight and bias gradients
+                pw, pb = A.alloc(npf * ci * co * 8), A.alloc(npf * co)
+                self._call("l3u_convt_bwd_fused", dcat.data_ptr(), 2 * co * S[lvl], prev.p, prev.ns,
+                           self._w(flat, up + "up.weight"), dprev.data_ptr(), ci * S[lvl + 1],
+                           A.ptr(pw), A.ptr(pb), N, ci, co, d, hh, w, st)
+                self._seg(pw, npf, ci * co * 8, 1, ci * co * 8, up + "up.weight")
+                self._seg(pb, npf, co, 1, co, up + "up.bias")
+            else:
+                npw = nat.query("l3u_pw_bwd_weight_nparts", N, S[lvl + 1])
+                pw = A.alloc(npw * ci * co * 8)
+                ncs = nat.query("l3u_chan_sum_nblocks", 8 * S[lvl + 1])
+                pb = A.alloc(2 * co * N * ncs)            # fp64 partials
+                self._call("l3u_convt_bwd", dcat.data_ptr(), 2 * co * S[lvl], prev.p, prev.ns,
+                           self._w(flat, up + "up.weight"), dprev.data_ptr(), ci * S[lvl + 1],
+                           A.ptr(pw), A.ptr(pb), N, ci, co, d, hh, w, st)
+                self._seg(pw, npw, ci * co * 8, 1, ci * co * 8, up + "up.weight")
+                self._seg(pb // 2, N * ncs, 1, N * ncs, co, up + "up.bias", f64=1)
             dout = V(dprev, 0, ci * S[lvl + 1], ci)
         # ---- bottleneck
         dx4 = e(N, c3, S[3])

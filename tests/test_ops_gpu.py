@@ -743,6 +743,43 @@ def test_dw3_bwd_split_calls(cuda, shape, mode):
         assert torch.equal(a[2], b[2])
 
 
+# (N, Ci, Co, D, H, W): the network's three up-blocks (low-res volumes) plus ragged ones
+CONVT_ONEPASS = [(2, 32, 16, 8, 8, 8), (2, 64, 32, 6, 6, 8), (1, 128, 64, 3, 3, 4),
+                 (2, 24, 8, 5, 6, 4), (4, 64, 32, 12, 12, 12), (2, 16, 8, 4, 4, 12)]
+
+
+@pytest.mark.parametrize("case", CONVT_ONEPASS)
+def test_convt_bwd_onepass(cuda, case):
+    """l3u_convt_bwd_fused: data, weight and bias gradients of ConvTranspose3d(k2, s2) in one
+    launch, dY gathered in place from a concat gradient, vs torch autograd in fp64."""
+    N, Ci, Co, D, H, W = case
+    Si = D * H * W
+    So = 8 * Si
+    gen = torch.Generator().manual_seed(14)
+    x = torch.randn(N, Ci, D, H, W, generator=gen, dtype=torch.float64)
+    w = torch.randn(Ci, Co, 2, 2, 2, generator=gen, dtype=torch.float64)
+    b = torch.randn(Co, generator=gen, dtype=torch.float64)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    y = F.conv_transpose3d(xr, wr, br, stride=2)
+    dy = torch.randn(y.shape, generator=gen, dtype=torch.float64)
+    y.backward(dy)
+    dcat = torch.full((N, 2 * Co, So), 3.0, device=cuda)
+    dcat[:, :Co] = dy.reshape(N, Co, So).float().to(cuda)
+    xd, wd = x.float().to(cuda), w.float().to(cuda)
+    dx = torch.full((N, Ci, Si), float("nan"), device=cuda)
+    P = nat().query("l3u_convt_bwd_fused_nparts", N, Ci, Co, D, H, W)
+    assert P == N * ((Si + 63) // 64)
+    wp = torch.full((P * Ci * Co * 8,), float("nan"), device=cuda)
+    bp = torch.full((P * Co,), float("nan"), device=cuda)
+    nat().call("l3u_convt_bwd_fused", dcat.data_ptr(), 2 * Co * So, xd.data_ptr(), Ci * Si,
+               wd.data_ptr(), dx.data_ptr(), Ci * Si, wp.data_ptr(), bp.data_ptr(), N, Ci, Co, D, H,
+               W, st())
+    torch.cuda.synchronize()
+    close(dx.view(x.shape), xr.grad, 1e-5, f"convT dX {case}")
+    close(wp.view(P, Ci, Co * 8).double().sum(0).view(w.shape), wr.grad, 2e-5, "convT dW")
+    close(bp.view(P, Co).double().sum(0), br.grad, 1e-5, "convT db")
+
+
 @pytest.mark.parametrize("case", CONVT_FUSED)
 def test_convt_bwd_fused(cuda, case):
     """l3u_convt_bwd: data gradient with dY gathered in place from the lower half of a concat

@@ -64,7 +64,11 @@ def graph_time(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--convt-only", action="store_true")
     a = ap.parse_args()
+    if a.convt_only:
+        convt(a.iters)
+        return
     dev = torch.device("cuda:0")
     tag = os.path.basename(os.environ.get("L3U_LIB", "default"))
     for (N, J, K, L, pro, acc, role) in SHAPES:
@@ -104,6 +108,39 @@ def main():
         tu = graph_time(unfused, a.iters)
         print(f"{tag:12s} J{J:<3d} K{K:<3d} {L}^3 pro={int(pro)} acc={int(acc)} {role:24s} fused "
               f"{tf:7.2f} us ({nb / tf / 1e3:5.0f} GB/s)  unfused {tu:7.2f} us", flush=True)
+    convt(a.iters)
+
+
+def convt(iters):
+    dev = torch.device("cuda:0")
+    for (N, Ci, Co, L) in [(4, 32, 16, 24), (4, 64, 32, 12), (4, 128, 64, 6)]:
+        Si = L ** 3
+        dcat = torch.randn(N, 2 * Co, 8 * Si, device=dev)
+        x = torch.randn(N, Ci, Si, device=dev)
+        w = torch.randn(Ci, Co * 8, device=dev)
+        dx = torch.empty(N, Ci, Si, device=dev)
+        P = N * ((Si + 63) // 64)
+        if nat.query("l3u_convt_bwd_fused_nparts", N, Ci, Co, L, L, L) == 0:
+            print(f"convT bwd Ci{Ci} Co{Co} {L}^3: one-launch form not offered")
+            continue
+        wp, bp = torch.empty(P * Ci * Co * 8, device=dev), torch.empty(P * Co, device=dev)
+        P2 = nat.query("l3u_pw_bwd_weight_nparts", N, Si)
+        ncs = nat.query("l3u_chan_sum_nblocks", 8 * Si)
+        wp2 = torch.empty(P2 * Ci * Co * 8, device=dev)
+        bp2 = torch.empty(Co * N * ncs, dtype=torch.float64, device=dev)
+
+        def fused():
+            nat.call("l3u_convt_bwd_fused", dcat.data_ptr(), 2 * Co * 8 * Si, x.data_ptr(), Ci * Si,
+                     w.data_ptr(), dx.data_ptr(), Ci * Si, wp.data_ptr(), bp.data_ptr(), N, Ci, Co,
+                     L, L, L, torch.cuda.current_stream().cuda_stream)
+
+        def unfused():
+            nat.call("l3u_convt_bwd", dcat.data_ptr(), 2 * Co * 8 * Si, x.data_ptr(), Ci * Si,
+                     w.data_ptr(), dx.data_ptr(), Ci * Si, wp2.data_ptr(), bp2.data_ptr(), N, Ci, Co,
+                     L, L, L, torch.cuda.current_stream().cuda_stream)
+
+        print(f"convT bwd Ci{Ci} Co{Co} {L}^3: one launch {graph_time(fused, iters):7.2f} us  "
+              f"three launches {graph_time(unfused, iters):7.2f} us", flush=True)
 
 
 if __name__ == "__main__":
