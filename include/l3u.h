@@ -132,6 +132,16 @@ int l3u_norm_act_fwd(const float* y2, long long y2_nstride, const float* rec2,
                      const l3u_norm_src* src2, const float* r, long long r_nstride,
                      const float* rec_r, const l3u_norm_src* src_r, int shortcut, float* out,
                      long long out_nstride, int N, int C, int S, hipStream_t stream);
+/* the same block tail fused with the MaxPool3d(kernel 2, stride 2) that follows it in the encoder
+ * (DownBlock, unet3d.py:104-105): also writes pooled [N][C][D/2*H/2*W/2] (batch stride
+ * pooled_nstride) and idx (argmax in the window, as l3u_maxpool2_fwd).  Needs even D, H,
+ * W % 4 == 0 and 16-byte aligned activations.                                              */
+int l3u_norm_act_pool_fwd(const float* y2, long long y2_nstride, const float* rec2,
+                          const l3u_norm_src* src2, const float* r, long long r_nstride,
+                          const float* rec_r, const l3u_norm_src* src_r, int shortcut, float* out,
+                          long long out_nstride, float* pooled, long long pooled_nstride,
+                          unsigned char* idx, int N, int C, int D, int H, int W,
+                          hipStream_t stream);
 /* backward of the block tail: part[C][N][nblocks][3] (fp64) = {sum g, sum g*xhat2, sum g*xhat_r},
  * g = dout * lrelu'(out); then dy2 / dr (dr = g for the identity shortcut)                   */
 int l3u_norm_act_bwd_reduce(const float* dout, long long dout_nstride, const float* out,
@@ -171,12 +181,12 @@ int l3u_convt_fwd(const float* x, long long x_nstride, const float* w, const flo
                   float* out, long long out_nstride, int N, int Ci, int Co, int D, int H, int W,
                   hipStream_t stream);
 /* the whole backward reading dY in place from the up-sampled gradient (no space-to-depth copy):
- * dx = the data-gradient GEMM with its X operand gathered from dy; wpart[l3u_pw_bwd_weight_nparts
- * (N, D*H*W)][Ci][Co*8] weight partials; bpart[Co][N][l3u_chan_sum_nblocks(8*D*H*W)] (fp64) bias
- * partials (dy: [N][Co][2D][2H][2W] with batch stride dy_nstride, e.g. the lower half of the
- * decoder's concat gradient)                                                                   */
+ * dx = the data-gradient GEMM with its X operand gathered from dy; wpart[P][Ci][Co*8] weight
+ * partials and bpart[P][Co] bias partials (fp32, from the weight-gradient launch), P =
+ * l3u_pw_bwd_weight_nparts(N, D*H*W) (dy: [N][Co][2D][2H][2W] with batch stride dy_nstride,
+ * e.g. the lower half of the decoder's concat gradient)                                        */
 int l3u_convt_bwd(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
-                  const float* w, float* dx, long long dx_nstride, float* wpart, double* bpart,
+                  const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
                   int N, int Ci, int Co, int D, int H, int W, hipStream_t stream);
 /* the same backward as ONE launch (one workgroup per 64 low-res voxels and 16 input channels,
  * split over Co*8 rows by wave): dx, wpart[P][Ci][Co*8] and bpart[P][Co] (fp32) partials with
@@ -199,14 +209,16 @@ int l3u_chan_sum(const float* x, long long x_nstride, double* part, int N, int C
  *      ftl_part[N*nblocks][3] = {sum p*t, sum p, sum t} (reduce them with l3u_ftl_reduce)
  * bwd: dz = g*p*(1-p) with g = dp, or (dp == NULL) the FocalTversky gradient of the global sums
  *      (closed form, * gscale[0] if given); dh[c] = w[c]*dz;
- *      part[N*nblocks][C+1] (fp64) = {sum dz*h[c].., sum dz}                                  */
+ *      part[N*nblocks][C+1] (fp64) = {sum dz*h[c].., sum dz}; loss != NULL (dp == NULL): also
+ *      loss[0] = (1 - TI)^gamma of the sums (what l3u_ftl_loss computes; saves that launch)    */
 int l3u_outconv_nblocks(int S);
 int l3u_outconv_fwd(const float* h, long long h_nstride, const float* w, const float* b, float* p,
                     const float* t, float* ftl_part, int N, int C, int S, hipStream_t stream);
 int l3u_outconv_bwd(const float* dp, const float* p, const float* t, const double* sums,
                     double alpha, double beta, double gamma, double smooth, const float* gscale,
                     const float* h, long long h_nstride, const float* w, float* dh,
-                    long long dh_nstride, double* part, int N, int C, int S, hipStream_t stream);
+                    long long dh_nstride, double* part, float* loss, int N, int C, int S,
+                    hipStream_t stream);
 
 /* ---- FocalTverskyLoss (light_unet/models/losses.py:11-54) ----------------------------------
  * sums = {sum p*t, sum p, sum t} over ALL voxels of the batch (pred.view(-1), losses.py:40-46),

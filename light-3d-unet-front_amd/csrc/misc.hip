@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     const double* __restrict__ sums, double alpha, double beta, double gamma, double smooth,
     const float* __restrict__ gscale, const float* __restrict__ h, long long hns,
     const float* __restrict__ w, float* __restrict__ dh, long long dhns,
-    double* __restrict__ part, int C, int S) {
+    double* __restrict__ part, float* __restrict__ loss, int C, int S) {
   extern __shared__ double redd[];   // [4][C+1]
   __shared__ float coef[2];
   const int n = blockIdx.y, nb = gridDim.x;
@@ -207,6 +207,7 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
       const double s = gscale ? (double)gscale[0] : 1.0;
       coef[0] = (float)(r.A * s);
       coef[1] = (float)(r.B * s);
+      if (loss && blockIdx.x == 0 && blockIdx.y == 0) loss[0] = (float)r.loss;
     }
     __syncthreads();
   }
@@ -573,14 +574,14 @@ int l3u_outconv_fwd(const float* h, long long h_nstride, const float* w, const f
 int l3u_outconv_bwd(const float* dp, const float* p, const float* t, const double* sums, double alpha,
                     double beta, double gamma, double smooth, const float* gscale, const float* h,
                     long long h_nstride, const float* w, float* dh, long long dh_nstride,
-                    double* part, int N, int C, int S, hipStream_t stream) {
+                    double* part, float* loss, int N, int C, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && C <= 32 && S > 0);
   L3U_REQUIRE(dp != nullptr || (t != nullptr && sums != nullptr));
   const bool vec = S % 4 == 0 && h_nstride % 4 == 0 && dh_nstride % 4 == 0;
   dim3 grid((S + 1023) / 1024, N);
   const size_t lds = 4 * (C + 1) * sizeof(double);
-  if (vec) hipLaunchKernelGGL(outconv_bwd_kernel<true>, grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, C, S);
-  else hipLaunchKernelGGL(outconv_bwd_kernel<false>, grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, C, S);
+  if (vec) hipLaunchKernelGGL(outconv_bwd_kernel<true>, grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S);
+  else hipLaunchKernelGGL(outconv_bwd_kernel<false>, grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S);
   L3U_CHECK_LAUNCH();
 }
 

@@ -68,6 +68,70 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
   }
 }
 
+// The block tail fused with the MaxPool3d(2) that follows it in the encoder (unet3d.py:104-105):
+// a thread owns a 2x2x4 input block (two x-adjacent pooling windows), computes its 16 outputs
+// (four float4 rows), stores them and the two window maxima (float2) with their argmax bytes.
+// Same scan order and comparison as maxpool2_fwd_v_kernel (misc.hip).  Needs even D, H and
+// W % 4 == 0.
+template <bool HAS_SRC>
+__global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
+    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2, l3u_norm_src src2,
+    const float* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
+    int shortcut, float* __restrict__ out, long long ons, float* __restrict__ pooled,
+    long long pns, unsigned char* __restrict__ idx, int C, int D, int H, int W) {
+  __shared__ float sh[16];
+  const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f;
+  if (HAS_SRC) {
+    block_record2(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh);
+    m2 = sh[0]; a2 = sh[2]; b2 = sh[3];
+    if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; }
+  } else {
+    m2 = rec2[(long long)nc * kRec + 0];
+    a2 = rec2[(long long)nc * kRec + 2];
+    b2 = rec2[(long long)nc * kRec + 3];
+    if (shortcut) {
+      mr = recr[(long long)nc * kRec + 0];
+      ar = recr[(long long)nc * kRec + 2];
+      br = recr[(long long)nc * kRec + 3];
+    }
+  }
+  const long long S = (long long)D * H * W;
+  const int Ho = H / 2, W4 = W / 4;
+  const long long So = (long long)(D / 2) * Ho * (W / 2), Sp = So / 2;
+  const float* yp = y2 + (long long)n * y2ns + (long long)c * S;
+  const float* rp = r + (long long)n * rns + (long long)c * S;
+  float* op = out + (long long)n * ons + (long long)c * S;
+  float2* pp = reinterpret_cast<float2*>(pooled + (long long)n * pns + (long long)c * So);
+  unsigned short* ip = reinterpret_cast<unsigned short*>(idx + (long long)nc * So);
+  for (long long o = blockIdx.x * 256ll + threadIdx.x; o < Sp; o += (long long)gridDim.x * 256) {
+    const int q = (int)(o % W4), t = (int)(o / W4), oy = t % Ho, oz = t / Ho;
+    const long long base = ((long long)(2 * oz) * H + 2 * oy) * W + 4 * q;
+    f4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long off = base + ((long long)(j >> 1) * H + (j & 1)) * W;
+      const f4 yv = *reinterpret_cast<const f4*>(yp + off), rv = *reinterpret_cast<const f4*>(rp + off);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = lrelu(fmaf(a2, yv[e] - m2, b2) + fmaf(ar, rv[e] - mr, br));
+      *reinterpret_cast<f4*>(op + off) = v[j];
+    }
+    float b0 = v[0][0], b1 = v[0][2];
+    int i0 = 0, i1 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        if (j == 0 && dx == 0) continue;
+        const float u0 = v[j][dx], u1 = v[j][2 + dx];
+        if (u0 > b0 || u0 != u0) { b0 = u0; i0 = 2 * j + dx; }
+        if (u1 > b1 || u1 != u1) { b1 = u1; i1 = 2 * j + dx; }
+      }
+    pp[o] = make_float2(b0, b1);
+    ip[o] = (unsigned short)(i0 | (i1 << 8));
+  }
+}
+
 // partials per (c, n, block): [sum g, sum g*xhat2, sum g*xhat_r],  g = dout * lrelu'(out)
 template <bool VEC>
 __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
@@ -244,6 +308,31 @@ int l3u_norm_act_fwd(const float* y2, long long y2_nstride, const float* rec2,
   if (src2) { if (vec) NAF(true, true); else NAF(false, true); }
   else { if (vec) NAF(true, false); else NAF(false, false); }
 #undef NAF
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_norm_act_pool_fwd(const float* y2, long long y2_nstride, const float* rec2,
+                          const l3u_norm_src* src2, const float* r, long long r_nstride,
+                          const float* rec_r, const l3u_norm_src* src_r, int shortcut, float* out,
+                          long long out_nstride, float* pooled, long long pooled_nstride,
+                          unsigned char* idx, int N, int C, int D, int H, int W,
+                          hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && D >= 2 && H >= 2 && W >= 4);
+  L3U_REQUIRE(src2 ? (!shortcut || src_r) : (rec2 && (!shortcut || rec_r)));
+  L3U_REQUIRE(!(D & 1) && !(H & 1) && !(W & 3) && y2_nstride % 4 == 0 && r_nstride % 4 == 0 &&
+              out_nstride % 4 == 0 && pooled_nstride % 2 == 0 && ((uintptr_t)y2 & 15) == 0 &&
+              ((uintptr_t)r & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+              ((uintptr_t)pooled & 7) == 0 && ((uintptr_t)idx & 1) == 0);
+  const long long S = (long long)D * H * W;
+  dim3 grid(elem_blocks((int)S), N * C);
+  const l3u_norm_src z{};
+  const l3u_norm_src s2 = src2 ? *src2 : z, sr = src_r ? *src_r : z;
+#define NAP(S_) hipLaunchKernelGGL((norm_act_pool_fwd_kernel<S_>), grid, dim3(256), 0, stream, y2, \
+      y2_nstride, rec2, s2, r, r_nstride, rec_r, sr, shortcut, out, out_nstride, pooled, \
+      pooled_nstride, idx, C, D, H, W)
+  if (src2) NAP(true);
+  else NAP(false);
+#undef NAP
   L3U_CHECK_LAUNCH();
 }
 

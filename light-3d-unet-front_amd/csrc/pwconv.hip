@@ -421,7 +421,8 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
 template <int NJ, int NK, bool VEC, bool GATHER>
 __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
     const float* __restrict__ dy, long long dyns, const float* __restrict__ x, long long xns,
-    float* __restrict__ part, int J, int K, int S, int SCH, int nsc, int Hq, int Wq) {
+    float* __restrict__ part, float* __restrict__ bsum, int J, int K, int S, int SCH, int nsc,
+    int Hq, int Wq) {
   constexpr int TJ = 16 * NJ, TK = 16 * NK;
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [64][T]
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
@@ -437,6 +438,12 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
   for (int a = 0; a < NJ; ++a)
 #pragma unroll
     for (int b = 0; b < NK; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+  // bsum (GATHER, the ConvTranspose3d bias): row sums of the X operand over the chunk, by the
+  // workgroups of the first J tile
+  const bool do_b = GATHER && bsum != nullptr && j0 == 0;
+  float bacc[NK];
+#pragma unroll
+  for (int b = 0; b < NK; ++b) bacc[b] = 0.f;
 
 #pragma unroll 4
   for (int s = s_lo + wave * 16; s < s_hi; s += 64) {
@@ -460,6 +467,10 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 #pragma unroll
     for (int b = 0; b < NK; ++b)
       bv[b] = load_x4<VEC, GATHER>(xn, k0 + 16 * b + lr, K, sl, s_hi, S, Hq, Wq);
+    if (do_b) {
+#pragma unroll
+      for (int b = 0; b < NK; ++b) bacc[b] += (bv[b][0] + bv[b][1]) + (bv[b][2] + bv[b][3]);
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -493,6 +504,28 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
           const int jj = j0 + 16 * a + 4 * lk + r, kk = k0 + 16 * b + lr;
           if (jj < J && kk < K) o[(long long)jj * K + kk] = lds[((a * NK + b) * 4 + r) * 64 + l];
         }
+  }
+  if (do_b) {   // block-uniform: rows over the lanes lk, then the waves in order, then co = k/8
+    __syncthreads();
+    float* bl = lds;                                  // [4 waves][16 * NK]
+#pragma unroll
+    for (int b = 0; b < NK; ++b) {
+      float v = bacc[b];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lk == 0) bl[wave * 16 * NK + 16 * b + lr] = v;
+    }
+    __syncthreads();
+    if (tid < 2 * NK) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = 8 * tid + i;
+        v += ((bl[row] + bl[16 * NK + row]) + bl[32 * NK + row]) + bl[48 * NK + row];
+      }
+      const int co = (k0 >> 3) + tid;
+      if (8 * co < K) bsum[(long long)(blockIdx.x) * (K / 8) + co] = v;
+    }
   }
 }
 
@@ -942,8 +975,8 @@ int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout,
 }
 
 int pw_bwd_weight_launch(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
-                         float* part, int N, int J, int K, int S, bool gather, int Hq, int Wq,
-                         hipStream_t stream) {
+                         float* part, float* bsum, int N, int J, int K, int S, bool gather, int Hq,
+                         int Wq, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && J > 0 && K > 0 && S > 0);
   const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (dy_nstride % 4 == 0) &&
                    (!gather || Wq % 4 == 0);
@@ -961,7 +994,7 @@ int pw_bwd_weight_launch(const float* dy, long long dy_nstride, const float* x, 
   const size_t lds = 64 * (size_t)NJ * NK * 4 * sizeof(float);
   dim3 grid(N * nsc, ntj * ntk), block(256);
 #define PWB0(A_, B_, V_, G_) hipLaunchKernelGGL((pw_bwd_weight_kernel<A_, B_, V_, G_>), grid, block, lds, \
-      stream, dy, dy_nstride, x, x_nstride, part, J, K, S, SCH, nsc, Hq, Wq)
+      stream, dy, dy_nstride, x, x_nstride, part, bsum, J, K, S, SCH, nsc, Hq, Wq)
 #define PWB(A_, B_) do { if (gather) { if (vec) PWB0(A_, B_, true, true); else PWB0(A_, B_, false, true); } \
                          else { if (vec) PWB0(A_, B_, true, false); else PWB0(A_, B_, false, false); } } while (0)
   if (NJ == 1 && NK == 1) PWB(1, 1);
@@ -1011,7 +1044,8 @@ int l3u_pw_bwd_weight_nparts(int N, int S) {
 
 int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
                       float* part, int N, int J, int K, int S, hipStream_t stream) {
-  return pw_bwd_weight_launch(dy, dy_nstride, x, x_nstride, part, N, J, K, S, false, 0, 0, stream);
+  return pw_bwd_weight_launch(dy, dy_nstride, x, x_nstride, part, nullptr, N, J, K, S, false, 0, 0,
+                              stream);
 }
 
 #ifndef L3U_CONVT_ONEPASS_MAX_S
@@ -1116,7 +1150,7 @@ int l3u_convt_bwd_fused(const float* dy, long long dy_nstride, const float* x, l
 }
 
 int l3u_convt_bwd(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
-                  const float* w, float* dx, long long dx_nstride, float* wpart, double* bpart,
+                  const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
                   int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && Ci > 0 && Co > 0 && D > 0 && H > 0 && W > 0);
   const int S = D * H * W;
@@ -1124,11 +1158,10 @@ int l3u_convt_bwd(const float* dy, long long dy_nstride, const float* x, long lo
   int rc = pw_launch(dy, dy_nstride, w, 0, nullptr, dx, dx_nstride, 0, nullptr, N, Co * 8, Ci, S,
                      2, D, H, W, stream);
   if (rc != 0) return rc;
-  // dW[ci][co*8+abc] = sum_s x[ci][s] dY[co][up(s, abc)]
-  rc = pw_bwd_weight_launch(x, x_nstride, dy, dy_nstride, wpart, N, Ci, Co * 8, S, true, H, W, stream);
-  if (rc != 0) return rc;
-  // db[co] = sum of dY over the up-sampled volume (per-channel partials)
-  return l3u_chan_sum(dy, dy_nstride, bpart, N, Co, 8ll * S, stream);
+  // dW[ci][co*8+abc] = sum_s x[ci][s] dY[co][up(s, abc)] and, in the same launch,
+  // db[co] = sum of dY over the up-sampled volume: bpart[N*nsc][Co]
+  return pw_bwd_weight_launch(x, x_nstride, dy, dy_nstride, wpart, bpart, N, Ci, Co * 8, S, true, H,
+                              W, stream);
 }
 
 }  // extern "C"

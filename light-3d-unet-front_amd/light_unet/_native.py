@@ -37,6 +37,7 @@ _SIGS = {
     "l3u_in_finalize": [P, I, P, P, F, U64, P, I, P, I, I, P],
     "l3u_norm_act_nblocks": [I],
     "l3u_norm_act_fwd": [P, L, P, P, P, L, P, P, I, P, L, I, I, I, P],
+    "l3u_norm_act_pool_fwd": [P, L, P, P, P, L, P, P, I, P, L, P, L, P, I, I, I, I, I, P],
     "l3u_norm_act_bwd_reduce": [P, L, P, L, P, L, P, P, L, P, P, I, I, I, P],
     "l3u_norm_act_bwd_apply": [P, L, P, L, P, L, P, P, L, P, P, P, L, P, L, I, I, I, P],
     "l3u_in_bwd_apply": [P, L, P, L, P, P, I, P, L, I, I, I, P],
@@ -52,7 +53,7 @@ _SIGS = {
     "l3u_chan_sum": [P, L, P, I, I, L, P],
     "l3u_outconv_nblocks": [I],
     "l3u_outconv_fwd": [P, L, P, P, P, P, P, I, I, I, P],
-    "l3u_outconv_bwd": [P, P, P, P, D, D, D, D, P, P, L, P, P, L, P, I, I, I, P],
+    "l3u_outconv_bwd": [P, P, P, P, D, D, D, D, P, P, L, P, P, L, P, P, I, I, I, P],
     "l3u_ftl_nblocks": [L],
     "l3u_ftl_sums": [P, P, L, P, P, P],
     "l3u_ftl_reduce": [P, I, P, P],

@@ -204,18 +204,25 @@ class UNetEngine:
         x3 = V(cat1, c2 * S[2], 2 * c2 * S[2], c2)
         x4v = V(x4, 0, c3 * S[3], c3)
         blk = {}
-        blk["init_conv."] = self._block_fwd(flat, "init_conv.", 0, x_in, x1, dims[0], drop, cptr, st, dev)
-        pools = []
+        # the encoder's MaxPool3d inputs x1..x3 and their pooled tensors (DownBlock,
+        # unet3d.py:104-105); the pool runs in the producing block's tail when the shape allows
+        pools = [(e(N, src.C, S[k + 1]),
+                  self._empty(N, src.C, S[k + 1], dtype=torch.uint8, device=dev))
+                 for k, src in enumerate((x1, x2, x3))]
+        fuse = [self._pool_fusable(src, dims[k]) for k, src in enumerate((x1, x2, x3))]
+        blk["init_conv."] = self._block_fwd(flat, "init_conv.", 0, x_in, x1, dims[0], drop, cptr, st,
+                                            dev, pool=pools[0] if fuse[0] else None)
         for k, (name, src, dst) in enumerate((("down1.res_block.", x1, x2), ("down2.res_block.", x2, x3),
                                               ("down3.res_block.", x3, x4v))):
             d, h, w = dims[k]
-            pooled = e(N, src.C, S[k + 1])
-            idx = self._empty(N, src.C, S[k + 1], dtype=torch.uint8, device=dev)
-            self._call("l3u_maxpool2_fwd", src.p, src.ns, pooled.data_ptr(), src.C * S[k + 1],
-                       idx.data_ptr(), N, src.C, d, h, w, st)
-            pools.append((pooled, idx))
+            pooled, idx = pools[k]
+            if not fuse[k]:
+                self._call("l3u_maxpool2_fwd", src.p, src.ns, pooled.data_ptr(), src.C * S[k + 1],
+                           idx.data_ptr(), N, src.C, d, h, w, st)
             pv = V(pooled, 0, src.C * S[k + 1], src.C)
-            blk[name] = self._block_fwd(flat, name, k + 1, pv, dst, dims[k + 1], drop, cptr, st, dev)
+            nxt = pools[k + 1] if k + 1 < 3 and fuse[k + 1] else None
+            blk[name] = self._block_fwd(flat, name, k + 1, pv, dst, dims[k + 1], drop, cptr, st, dev,
+                                        pool=nxt)
         sv["pools"] = pools
         bott = e(N, c3, S[3])
         blk["bottleneck."] = self._block_fwd(flat, "bottleneck.", 4, x4v, V(bott, 0, c3 * S[3], c3),
@@ -254,8 +261,14 @@ class UNetEngine:
                            self._w(flat, norm_prefix + "weight"), self._w(flat, norm_prefix + "bias"),
                            float(drop), self.seed, cptr or 0, rec_out)
 
-    def _block_fwd(self, flat, pre, layer, x, out, dims, drop, cptr, st, dev):
-        """ResidualBlock.forward (unet3d.py:77-93) into the view `out`."""
+    @staticmethod
+    def _pool_fusable(v, dims):
+        d, h, w = dims
+        return d % 2 == 0 and h % 2 == 0 and w % 4 == 0 and v.ns % 4 == 0 and v.p % 16 == 0
+
+    def _block_fwd(self, flat, pre, layer, x, out, dims, drop, cptr, st, dev, pool=None):
+        """ResidualBlock.forward (unet3d.py:77-93) into the view `out`; pool = (pooled, idx):
+        also the MaxPool3d(2) of the output (the next DownBlock's pool) in the same launch."""
         N = x.t.shape[0]
         d, h, w = dims
         S = d * h * w
@@ -298,9 +311,16 @@ class UNetEngine:
         self._call("l3u_pw_fwd", z2.data_ptr(), cout * S, self._w(flat, pre + "conv2.pointwise.weight"),
                    0, None, y2.data_ptr(), cout * S, 0, self.fwd_arena.ptr(s2), N, cout, cout, S, st)
         src2 = self._src(flat, pre + "norm2.", s2, nsb2, rec2, 0.0, cptr, 0)
-        self._call("l3u_norm_act_fwd", y2.data_ptr(), cout * S, None, nat.norm_src_ptr(src2), rv.p,
-                   rv.ns, None, nat.norm_src_ptr(src_r), 1 if shortcut else 0, out.p, out.ns, N,
-                   cout, S, st)
+        if pool is None:
+            self._call("l3u_norm_act_fwd", y2.data_ptr(), cout * S, None, nat.norm_src_ptr(src2),
+                       rv.p, rv.ns, None, nat.norm_src_ptr(src_r), 1 if shortcut else 0, out.p,
+                       out.ns, N, cout, S, st)
+        else:
+            pooled, idx = pool
+            self._call("l3u_norm_act_pool_fwd", y2.data_ptr(), cout * S, None,
+                       nat.norm_src_ptr(src2), rv.p, rv.ns, None, nat.norm_src_ptr(src_r),
+                       1 if shortcut else 0, out.p, out.ns, pooled.data_ptr(), cout * (S // 8),
+                       idx.data_ptr(), N, cout, d, h, w, st)
         sv.update(z1=z1, y1=y1, z2=z2, y2=y2, dims=dims, shortcut=shortcut)
         return sv
 
@@ -308,7 +328,8 @@ class UNetEngine:
     def backward(self, flat, gflat, sv, dp, need_dx=False, ftl=None):
         """Given dL/dp write all parameter gradients into gflat (overwrite) and return dL/dx if
         need_dx.  dp = None: the loss is FocalTversky and ftl = (target, global sums [3] fp64,
-        (alpha, beta, gamma, smooth)); its gradient is formed inside the out_conv backward."""
+        (alpha, beta, gamma, smooth)[, loss tensor]); its gradient is formed inside the out_conv
+        backward, which also writes the loss value when a loss tensor is given."""
         N = sv["N"]
         D, H, W = sv["dims"][0]
         key = ("b", N, D, H, W, bool(need_dx))
@@ -345,14 +366,17 @@ class UNetEngine:
         dh = e(N, c0, S[0])
         nb = nat.query("l3u_outconv_nblocks", S[0])
         po = A.alloc(2 * N * nb * (c0 + 1))          # fp64 partials
+        loss_ptr = None
         if dp is not None:
             g = (dp.data_ptr(), None, None, 0.0, 0.0, 0.0, 0.0, None)
         else:   # FocalTversky gradient formed inside the kernel from the global sums
-            t, sums, (alpha, beta, gamma, smooth) = ftl
+            t, sums, (alpha, beta, gamma, smooth) = ftl[:3]
             g = (None, t.data_ptr(), sums.data_ptr(), alpha, beta, gamma, smooth, None)
+            if len(ftl) > 3 and ftl[3] is not None:   # the loss value, written by the same launch
+                loss_ptr = ftl[3].data_ptr()
         self._call("l3u_outconv_bwd", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
-                   self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po), N, c0,
-                   S[0], st)
+                   self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po), loss_ptr,
+                   N, c0, S[0], st)
         self._seg(po // 2, N * nb, c0 + 1, 1, c0, "out_conv.weight", f64=1)
         self._seg(po // 2 + c0, N * nb, c0 + 1, 1, 1, "out_conv.bias", f64=1)
         dcat3, dcat2, dcat1 = e(N, 2 * c0, S[0]), e(N, 2 * c1, S[1]), e(N, 2 * c2, S[2])
@@ -380,14 +404,12 @@ class UNetEngine:
                 self._seg(pb, npf, co, 1, co, up + "up.bias")
             else:
                 npw = nat.query("l3u_pw_bwd_weight_nparts", N, S[lvl + 1])
-                pw = A.alloc(npw * ci * co * 8)
-                ncs = nat.query("l3u_chan_sum_nblocks", 8 * S[lvl + 1])
-                pb = A.alloc(2 * co * N * ncs)            # fp64 partials
+                pw, pb = A.alloc(npw * ci * co * 8), A.alloc(npw * co)
                 self._call("l3u_convt_bwd", dcat.data_ptr(), 2 * co * S[lvl], prev.p, prev.ns,
                            self._w(flat, up + "up.weight"), dprev.data_ptr(), ci * S[lvl + 1],
                            A.ptr(pw), A.ptr(pb), N, ci, co, d, hh, w, st)
                 self._seg(pw, npw, ci * co * 8, 1, ci * co * 8, up + "up.weight")
-                self._seg(pb // 2, N * ncs, 1, N * ncs, co, up + "up.bias", f64=1)
+                self._seg(pb, npw, co, 1, co, up + "up.bias")
             dout = V(dprev, 0, ci * S[lvl + 1], ci)
         # ---- bottleneck
         dx4 = e(N, c3, S[3])

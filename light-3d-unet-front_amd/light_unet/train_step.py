@@ -58,12 +58,11 @@ class TrainStep:
         return p, sv, sums
 
     def _bwd(self, p, sv, t, sums):
-        st = nat.stream()
-        nat.call("l3u_ftl_loss", sums.data_ptr(), self.alpha, self.beta, self.gamma, self.smooth,
-                 self.loss.data_ptr(), st)
-        # dL/dp is formed inside the out_conv backward from t and the (global) sums
+        # dL/dp is formed inside the out_conv backward from t and the (global) sums; the same
+        # launch writes the loss value (losses.py:52-54)
         self.engine.backward(self.flat, self.gflat, sv, None, need_dx=False,
-                             ftl=(t, sums, (self.alpha, self.beta, self.gamma, self.smooth)))
+                             ftl=(t, sums, (self.alpha, self.beta, self.gamma, self.smooth),
+                                  self.loss))
 
     def _grad_exchange(self):
         exchange_grads(self.gflat, self.ftl_mode, self.group)

@@ -434,6 +434,51 @@ def test_norm_act_fwd_bwd(cuda, shape, shortcut):
         close(p[:, 2], grr.grad, 1e-5, "dgamma_r")
 
 
+@pytest.mark.parametrize("shape,shortcut,with_src", [((2, 3, 4, 6, 8), True, False),
+                                                    ((4, 16, 48, 48, 48), False, True),
+                                                    ((2, 32, 12, 12, 12), True, True)])
+def test_norm_act_pool_fwd(cuda, shape, shortcut, with_src):
+    """l3u_norm_act_pool_fwd == l3u_norm_act_fwd followed by l3u_maxpool2_fwd, bit for bit."""
+    N, C, D, H, W = shape
+    S, So = D * H * W, D * H * W // 8
+    gen = torch.Generator().manual_seed(16)
+    y2 = torch.randn(N, C, S, generator=gen).to(cuda)
+    r = torch.randn(N, C, S, generator=gen).to(cuda)
+    if with_src:   # in-kernel finalize from (count, mean, M2) partials
+        keep = []
+
+        def src_of(v):
+            part = torch.stack([torch.full((N, C), float(S), device=cuda), v.mean(-1),
+                                ((v - v.mean(-1, keepdim=True)) ** 2).sum(-1)], -1).contiguous()
+            g = (1 + 0.2 * torch.randn(C, generator=gen)).to(cuda)
+            b = (0.2 * torch.randn(C, generator=gen)).to(cuda)
+            ro = torch.empty(N * C * 8, device=cuda)
+            keep.extend([part, g, b, ro])
+            return nat().NormSrc(part.data_ptr(), 1, 0, g.data_ptr(), b.data_ptr(), 0.0, 0, None,
+                                 ro.data_ptr())
+        s2, sr = src_of(y2), src_of(r)
+        recs = (None, nat().norm_src_ptr(s2), None, nat().norm_src_ptr(sr) if shortcut else None)
+    else:
+        rec2 = torch.rand(N * C, 8, generator=gen).to(cuda)
+        recr = torch.rand(N * C, 8, generator=gen).to(cuda)
+        recs = (rec2.data_ptr(), None, recr.data_ptr() if shortcut else None, None)
+    o1, o2 = torch.empty(N, C, S, device=cuda), torch.empty(N, C, S, device=cuda)
+    p1, p2 = torch.empty(N, C, So, device=cuda), torch.empty(N, C, So, device=cuda)
+    i1 = torch.empty(N, C, So, dtype=torch.uint8, device=cuda)
+    i2 = torch.empty(N, C, So, dtype=torch.uint8, device=cuda)
+    nat().call("l3u_norm_act_fwd", y2.data_ptr(), C * S, recs[0], recs[1], r.data_ptr(), C * S,
+               recs[2], recs[3], int(shortcut), o1.data_ptr(), C * S, N, C, S, st())
+    nat().call("l3u_maxpool2_fwd", o1.data_ptr(), C * S, p1.data_ptr(), C * So, i1.data_ptr(), N, C,
+               D, H, W, st())
+    nat().call("l3u_norm_act_pool_fwd", y2.data_ptr(), C * S, recs[0], recs[1], r.data_ptr(), C * S,
+               recs[2], recs[3], int(shortcut), o2.data_ptr(), C * S, p2.data_ptr(), C * So,
+               i2.data_ptr(), N, C, D, H, W, st())
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert torch.equal(p1, p2)
+    assert torch.equal(i1, i2)
+
+
 def test_in_bwd_apply(cuda):
     N, C, D, H, W = 2, 4, 6, 5, 7
     S = D * H * W
@@ -562,8 +607,8 @@ def test_outconv(cuda, case):
     dh = torch.empty(N, C, S, device=cuda)
     dpd = dp.float().to(cuda)
     nat().call("l3u_outconv_bwd", dpd.data_ptr(), pd.data_ptr(), None, None, 0.0, 0.0, 0.0, 0.0,
-               None, hd.data_ptr(), C * S, wd.data_ptr(), dh.data_ptr(), C * S, part.data_ptr(), N,
-               C, S, st())
+               None, hd.data_ptr(), C * S, wd.data_ptr(), dh.data_ptr(), C * S, part.data_ptr(), None,
+               N, C, S, st())
     torch.cuda.synchronize()
     close(pd, p, 1e-6, "outconv p")
     close(dh, hr.grad, 1e-5, "outconv dh")
@@ -688,10 +733,12 @@ def test_outconv_ftl_fused(cuda, case):
     nat().call("l3u_ftl_loss", sums.data_ptr(), 0.7, 0.3, 0.75, 1e-6, lossd.data_ptr(), st())
     part = torch.empty(N * nb * (C + 1), dtype=torch.float64, device=cuda)
     dh = torch.empty(N, C, S, device=cuda)
+    loss2 = torch.full((), float("nan"), device=cuda)
     nat().call("l3u_outconv_bwd", None, pd.data_ptr(), td.data_ptr(), sums.data_ptr(), 0.7, 0.3, 0.75,
                1e-6, None, hd.data_ptr(), C * S, wd.data_ptr(), dh.data_ptr(), C * S, part.data_ptr(),
-               N, C, S, st())
+               loss2.data_ptr(), N, C, S, st())
     torch.cuda.synchronize()
+    assert torch.equal(loss2, lossd)   # the loss written by the backward launch
     pr = p.detach()
     ref_sums = torch.stack([(pr * t).sum(), pr.sum(), t.sum()])
     close(sums.cpu(), ref_sums, 1e-5, "ftl sums")
@@ -801,11 +848,10 @@ def test_convt_bwd_fused(cuda, case):
     dx = torch.full((N, Ci, Si), float("nan"), device=cuda)
     P = nat().query("l3u_pw_bwd_weight_nparts", N, Si)
     wp = torch.full((P * Ci * Co * 8,), float("nan"), device=cuda)
-    ncs = nat().query("l3u_chan_sum_nblocks", 8 * Si)
-    bp = torch.full((Co * N * ncs,), float("nan"), dtype=torch.float64, device=cuda)
+    bp = torch.full((P * Co,), float("nan"), device=cuda)
     nat().call("l3u_convt_bwd", dcat.data_ptr(), 2 * Co * So, xd.data_ptr(), Ci * Si, wd.data_ptr(),
                dx.data_ptr(), Ci * Si, wp.data_ptr(), bp.data_ptr(), N, Ci, Co, D, H, W, st())
     torch.cuda.synchronize()
     close(dx.view(x.shape), xr.grad, 1e-5, f"convT dX {case}")
     close(wp.view(P, Ci, Co * 8).double().sum(0).view(w.shape), wr.grad, 1e-5, "convT dW")
-    close(bp.view(Co, -1).double().sum(1), br.grad, 1e-5, "convT db")
+    close(bp.view(P, Co).double().sum(0), br.grad, 1e-5, "convT db")

@@ -125,9 +125,8 @@ def convt(iters):
             continue
         wp, bp = torch.empty(P * Ci * Co * 8, device=dev), torch.empty(P * Co, device=dev)
         P2 = nat.query("l3u_pw_bwd_weight_nparts", N, Si)
-        ncs = nat.query("l3u_chan_sum_nblocks", 8 * Si)
         wp2 = torch.empty(P2 * Ci * Co * 8, device=dev)
-        bp2 = torch.empty(Co * N * ncs, dtype=torch.float64, device=dev)
+        bp2 = torch.empty(P2 * Co, device=dev)
 
         def fused():
             nat.call("l3u_convt_bwd_fused", dcat.data_ptr(), 2 * Co * 8 * Si, x.data_ptr(), Ci * Si,
