@@ -139,9 +139,12 @@ class UNetEngine:
         """Record reduction items: grad[dst_name][dst_elem + t] = sum_i part[src_off+i*is+t*ts].
         f64=1: the partials are fp64 and src_off/strides count doubles from the arena base."""
         base = self.offsets[dst_name][0] + dst_elem
+        # outputs per item (one 256-thread workgroup each): fewer for long partial lists so that
+        # every thread's serial share stays short (256 / cap threads share each output's terms)
+        cap = 32 if count <= 128 else (16 if count <= 384 else 8)
         t0 = 0
-        while t0 < length:   # <= 32 outputs per item: >= 8 threads share each output's terms
-            ln = min(32, length - t0)
+        while t0 < length:
+            ln = min(cap, length - t0)
             self._items_rec.append((src_off + t0 * tstride, count, istride, tstride, ln,
                                     base + t0, accumulate, f64))
             t0 += ln
