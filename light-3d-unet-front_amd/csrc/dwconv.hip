@@ -13,6 +13,9 @@
 // MODE 1 fuses the InstanceNorm-apply + LeakyReLU + Dropout3d transform of the previous layer
 // (unet3d.py:84-88) into the input load: a = lrelu(scale*y + shift), with zero padding applied in
 // the transformed domain (as the reference pads the conv input a).
+#include <type_traits>
+#include <utility>
+
 #include "common.h"
 using namespace l3u;
 
@@ -312,6 +315,16 @@ int pick_tz(int D) { return D <= 8 ? D : 4; }
 #define L3U_GW_SCALAR 1
 #endif
 
+// TZ = 24 slabs for D % 24 == 0 (two slabs at 48^3): measured variant switch
+#ifndef L3U_TZ24
+#define L3U_TZ24 0
+#endif
+#if L3U_TZ24
+#define TZ24(X) if (g.TZ == 24) X; else
+#else
+#define TZ24(X)
+#endif
+
 struct QGeom {
   int WQ, RPW, NW, RB, ny, TZ, nz, threads;
 };
@@ -323,8 +336,12 @@ QGeom qgeom(int N, int C, int D, int H, int W) {
   g.RPW = 64 / g.WQ;
   int best = 1;
   double beff = -1.0;
+#ifndef L3U_DW_NWMIN
+#define L3U_DW_NWMIN 1
+#endif
   for (int nw = 1; nw <= 4; ++nw) {
     if ((nw - 1) * g.RPW >= H) break;   // a wave with no row at all
+    if (nw < L3U_DW_NWMIN && nw * g.RPW < H) continue;
     const int rb = nw * g.RPW, ny = (H + rb - 1) / rb;
     const double eff = (double)H / (ny * rb);
     if (eff > beff + 1e-9) { beff = eff; best = nw; }
@@ -337,10 +354,11 @@ QGeom qgeom(int N, int C, int D, int H, int W) {
 #define L3U_TZ16_MIN_D 48
 #endif
   g.TZ = D >= L3U_TZ16_MIN_D ? 16 : (D >= 32 ? 8 : (D > 8 ? 4 : 8));   // compile-time in the kernels
+  if (L3U_TZ24 && D >= 48 && D % 24 == 0) g.TZ = 24;
 #ifndef L3U_DW_MIN_BLOCKS
 #define L3U_DW_MIN_BLOCKS 1024
 #endif
-  while (g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < L3U_DW_MIN_BLOCKS) g.TZ >>= 1;   // {16, 8, 4, 2}
+  while (g.TZ != 24 && g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < L3U_DW_MIN_BLOCKS) g.TZ >>= 1;   // {16, 8, 4, 2}
   g.nz = (D + g.TZ - 1) / g.TZ;
   return g;
 }
@@ -424,8 +442,9 @@ struct QMap {
   bool ok[2];
 };
 
-L3U_DEV QMap q_map(int y0, int rows, int H, int W, int WQ) {
+L3U_DEV QMap q_map(int y0, int rows, int H, int W, int WQ, int lpitch = 0, int lofs = 0) {
   QMap m;
+  if (lpitch == 0) lpitch = W;
   const int nq = (rows + 2) * WQ;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -434,7 +453,7 @@ L3U_DEV QMap q_map(int y0, int rows, int H, int W, int WQ) {
     const int lr = qc / WQ, x = (qc - lr * WQ) * 4, y = y0 - 1 + lr;
     m.ok[k] = q < nq && y >= 0 && y < H;
     m.goff[k] = min(max(y, 0), H - 1) * W + x;
-    m.loff[k] = lr * W + x;
+    m.loff[k] = lr * lpitch + lofs + x;
   }
   return m;
 }
@@ -854,6 +873,309 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ?
 }
 
 // ------------------------------------------------------------------------------------------------
+// Single-pass backward with packed FP32 FMAs (v_pk_fma_f32): data gradient AND weight gradient
+// from one read of dZ and A and one write of dX (3 tensors of HBM traffic instead of the split
+// passes' 4).  The 54 FMAs per voxel are what bounded the earlier fused kernel (VALU-bound at one
+// FMA per instruction); here almost all of them issue two per instruction:
+//   data   dA(plane p)[i] += wf(kd, r, dx) * dZ(zd, row r)[i + dx]   (wf = flipped taps)
+//          planes zd-1 (kd 0) and zd (kd 1) are one accumulator PAIR per voxel i, multiplied by
+//          the tap PAIR (wf(0,.), wf(1,.)) (uniform: SGPRs) and the neighbour broadcast through
+//          op_sel; plane zd+1 (kd 2) pairs voxels (i, i+1) where the neighbour pair is an
+//          aligned register pair (dx = 1), scalar otherwise.
+//   weight gw(kd, r, dx) += sum_i g_kd[i] * A(za, row r)[i + dx]   (g_kd = own dZ quad of
+//          plane za+1-kd): per (kd, r) the pairs (dx 0, dx 1) and (dx 1, dx 2) take the voxels
+//          whose neighbour pair is aligned (i = 1, 3 and i = 0, 2), four products stay scalar.
+// The step index is a compile-time constant (index_sequence expansion), so the boundary steps
+// skip the work that only touches planes outside the slab: per owned voxel the kernel issues
+// exactly the 27 + 27 tap products.
+// ------------------------------------------------------------------------------------------------
+#ifndef L3U_DWP_WAVES
+#define L3U_DWP_WAVES 3
+#endif
+#ifndef L3U_DWP_PD
+#define L3U_DWP_PD 2
+#endif
+#ifndef L3U_DWP_PIN
+#define L3U_DWP_PIN 1
+#endif
+#ifndef L3U_DW_FUSED
+#define L3U_DW_FUSED 1
+#endif
+
+template <class F, int... I>
+L3U_DEV void run_steps(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+
+// LDS row image of the packed kernel: pitch W + 8 floats, x at offset 4, four zero floats on each
+// side (the conv's zero padding; never written after the initial clear).  A row read returns the
+// quad m = x..x+3 (ds_read_b128) and the aligned pairs n2 = (x-2, x-1), p2 = (x+4, x+5)
+// (ds_read_b64): the x-neighbours come from LDS with no lane exchange and no row-end selects.
+// L3U_DWP_LDSNB = 0 (default, measured faster): unpadded rows, the neighbours by DPP from the
+// adjacent lanes (one ds_read_b128 per row; ds_read2_b64 costs 8 LDS cycles vs 4 for b128, and
+// the LDS pipe also carries the ds_write_b128 commits at ~13 cycles each).
+#ifndef L3U_DWP_LDSNB
+#define L3U_DWP_LDSNB 0
+#endif
+constexpr int kLPad = L3U_DWP_LDSNB ? 8 : 0, kLOfs = L3U_DWP_LDSNB ? 4 : 0;
+constexpr int kNH = L3U_DWP_LDSNB ? 1 : 0;   // half of n2 holding x-1
+
+// row read: n2[kNH] = x-1, m = x..x+3, p2.x = x+4 (zero beyond the row)
+L3U_DEV void q_row3(const float* plane, int row, int lp, int ox, bool el, bool er, f2& n2, f4& m,
+                    f2& p2) {
+  const float* q = plane + row * lp + ox;
+#if L3U_DWP_LDSNB
+  n2 = *reinterpret_cast<const f2*>(q + kLOfs - 2);
+  m = *reinterpret_cast<const f4*>(q + kLOfs);
+  p2 = *reinterpret_cast<const f2*>(q + kLOfs + 4);
+#else
+  m = *reinterpret_cast<const f4*>(q);
+  const float pl = lane_prev(m[3]), pr = lane_next(m[0]);
+  const float l = el ? 0.f : pl, r = er ? 0.f : pr;
+  n2 = f2{l, l};
+  p2 = f2{r, r};
+#endif
+}
+
+// acc + a * {b[H], b[H]}: the product with one half of an aligned register pair broadcast to both
+// lanes of the packed FMA (op_sel picks the half; the compiler only folds the low-half case)
+template <int H>
+L3U_DEV f2 pk_bc(f2 acc, f2 a, f2 b) {
+  if (H == 0) return pfma(a, f2{b.x, b.x}, acc);
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(a), "v"(b));
+  return acc;
+}
+// scalar FMAs kept scalar: left to the SLP vectorizer, neighbouring ones get packed with v_mov
+// pairing that costs more than it saves
+#ifndef L3U_DWP_ASMS
+#define L3U_DWP_ASMS 1
+#endif
+L3U_DEV float sfma_s(float acc, float a, float b) {   // a wave-uniform
+#if L3U_DWP_ASMS
+  asm("v_fmac_f32 %0, %1, %2" : "+v"(acc) : "s"(a), "v"(b));
+  return acc;
+#else
+  return fmaf(a, b, acc);
+#endif
+}
+L3U_DEV float sfma_v(float acc, float a, float b) {
+#if L3U_DWP_ASMS
+  asm("v_fmac_f32 %0, %1, %2" : "+v"(acc) : "v"(a), "v"(b));
+  return acc;
+#else
+  return fmaf(a, b, acc);
+#endif
+}
+template <int H>
+L3U_DEV f2 pk_bc_s(f2 acc, f2 a, f2 b) {   // a wave-uniform (SGPR pair)
+  if (H == 0) return pfma(a, f2{b.x, b.x}, acc);
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(a), "v"(b));
+  return acc;
+}
+
+template <int MODE, int TZC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L3U_DWP_WAVES))) void dw3p_bwd_kernel(
+    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
+    const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
+    long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part,
+    int N, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int WQ = W >> 2, LP = W + kLPad, PP = (RB + 2) * LP, HW = H * W;
+  const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
+  const long long cofs = (long long)b.c * D * HW;
+  const float* dzp = dz + (long long)b.n * dzns + cofs;
+  const float* xp = x + (long long)b.n * xns + cofs;
+  float* dxp = dx + (long long)b.n * dxns + cofs;
+  float* dzb = lds;             // 2 planes
+  float* ab = lds + 2 * PP;     // 2 planes
+  // flipped data-gradient taps: pair (kd 0, kd 1) and kd 2 per in-plane tap (r, dx)
+  f2 wp[9];
+  float w2[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int tf = 8 - t;
+    wp[t] = f2{w[b.c * 27 + tf], w[b.c * 27 + 9 + tf]};
+    w2[t] = w[b.c * 27 + 18 + tf];
+  }
+  float sc = 1.f, sh = 0.f, kk = 1.f, mean = 0.f, rstd = 1.f;
+  if (MODE == 1) {
+    const float* r = rec + (long long)b.nc * kRec;
+    mean = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];
+  }
+  for (int i = threadIdx.x; i < 4 * PP; i += blockDim.x) lds[i] = 0.f;
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  const f2 zero2 = {0.f, 0.f};
+  f2 P[4];                      // (dA plane zd-1, dA plane zd) per voxel of the quad
+  f2 S01 = zero2, S23 = zero2;  // dA plane zd+1, voxels (0,1), (2,3)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) P[i] = zero2;
+  f2 GA[9], GB[9];              // per (kd, r): (gw dx0, gw dx1 part a), (gw dx1 part b, gw dx2)
+#pragma unroll
+  for (int t = 0; t < 9; ++t) GA[t] = GB[t] = zero2;
+  f4 g0 = zero4, g1 = zero4, g2 = zero4;   // own dZ quads of planes zd, zd-1, zd-2
+  float s1 = 0.f, s2 = 0.f;
+  const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
+  const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
+  // register staging PD planes ahead (sets alternate by step parity when PD = 2)
+  constexpr int PD = L3U_DWP_PD;
+  QPre pzs[PD], pas[PD];
+  const QMap qm = q_map(b.y0, b.rows, H, W, WQ, LP, kLOfs);
+  auto in_rng = [&](int z) { return z >= zlo && z <= zhi; };
+  auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };
+#pragma unroll
+  for (int k = 0; k < PD; ++k) {
+    q_fetch(pzs[k], dzp + zc(b.z0 - 1 + k), qm);
+    q_fetch(pas[k], xp + zc(b.z0 - 2 + k), qm);
+  }
+  __syncthreads();
+  auto step = [&](auto I) {
+    constexpr int s = decltype(I)::value;
+    QPre& pz = pzs[s % PD];
+    QPre& pa = pas[s % PD];
+    // planes of the slab are z0 .. z0+TZC-1 (z1 may cut it short at run time)
+    constexpr bool doP = s >= 1 && s <= TZC + 1;    // dA planes zd-1 / zd touch the slab
+    constexpr bool doS = s <= TZC - 1;              // dA plane zd+1 in the slab
+    constexpr bool own0 = s >= 1 && s <= TZC;       // dZ plane zd owned
+    constexpr bool use1 = s >= 2 && s <= TZC + 1;   // dZ plane zd-1 owned
+    constexpr bool use2 = s >= 3 && s <= TZC + 2;   // dZ plane zd-2 owned
+    constexpr bool fin = s >= 2 && s <= TZC + 1;    // dA plane zd-1 completes in the slab
+    const int zd = b.z0 - 1 + s, za = zd - 1;
+    float* dbuf = dzb + (s & 1) * PP;
+    float* abuf = ab + (s & 1) * PP;
+    q_commit<false>(pz, dbuf, qm, in_rng(zd), 1.f, 0.f, 0.f);
+    q_commit<MODE == 1>(pa, abuf, qm, in_rng(za), sc, mean, sh);
+    if constexpr (s + PD < TZC + 3) {
+      q_fetch(pz, dzp + zc(zd + PD), qm);
+      q_fetch(pa, xp + zc(za + PD), qm);
+    }
+    const int zf = zd - 1;
+    f4 epi = zero4;
+    if constexpr (MODE != 0 && fin)
+      epi = *reinterpret_cast<const f4*>((MODE == 1 ? xp : dxp) + (long long)min(max(zf, 0), D - 1) * HW + qofs);
+    __syncthreads();
+    if constexpr (doP || doS || own0) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        f2 n2, p2;
+        f4 m;
+        q_row3(dbuf, b.oy + r, LP, b.ox, b.el, b.er, n2, m, p2);
+        const f2 m01 = {m[0], m[1]}, m23 = {m[2], m[3]};
+        if (r == 1 && own0) g0 = (b.own && zd < b.z1) ? m : zero4;
+        if constexpr (doP) {
+          // v[j] = x-1+j: l = n2.hi, m0 = m01.lo, m1 = m01.hi, m2 = m23.lo, m3 = m23.hi, r = p2.lo
+          const f2 w0 = wp[r * 3], w1 = wp[r * 3 + 1], w2p = wp[r * 3 + 2];
+          P[0] = pk_bc_s<kNH>(P[0], w0, n2);  P[0] = pk_bc_s<0>(P[0], w1, m01); P[0] = pk_bc_s<1>(P[0], w2p, m01);
+          P[1] = pk_bc_s<0>(P[1], w0, m01); P[1] = pk_bc_s<1>(P[1], w1, m01); P[1] = pk_bc_s<0>(P[1], w2p, m23);
+          P[2] = pk_bc_s<1>(P[2], w0, m01); P[2] = pk_bc_s<0>(P[2], w1, m23); P[2] = pk_bc_s<1>(P[2], w2p, m23);
+          P[3] = pk_bc_s<0>(P[3], w0, m23); P[3] = pk_bc_s<1>(P[3], w1, m23); P[3] = pk_bc_s<0>(P[3], w2p, p2);
+        }
+        if constexpr (doS) {
+          const float a0 = w2[r * 3], a1 = w2[r * 3 + 1], a2 = w2[r * 3 + 2];
+          S01.x = sfma_s(S01.x, a0, n2.y);
+          S01.y = sfma_s(S01.y, a0, m[0]);
+          S23.x = sfma_s(S23.x, a0, m[1]);
+          S23.y = sfma_s(S23.y, a0, m[2]);
+          S01 = pfma(f2{a1, a1}, m01, S01);
+          S23 = pfma(f2{a1, a1}, m23, S23);
+          S01.x = sfma_s(S01.x, a2, m[1]);
+          S01.y = sfma_s(S01.y, a2, m[2]);
+          S23.x = sfma_s(S23.x, a2, m[3]);
+          S23.y = sfma_s(S23.y, a2, p2.x);
+        }
+      }
+    }
+    if constexpr (own0 || use1 || use2) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        f2 n2, p2;
+        f4 m;
+        q_row3(abuf, b.oy + r, LP, b.ox, b.el, b.er, n2, m, p2);
+        const f2 m01 = {m[0], m[1]}, m23 = {m[2], m[3]};
+        auto acc = [&](const f4& g, f2& A, f2& B) {
+          const f2 g01 = {g[0], g[1]}, g23 = {g[2], g[3]};
+          A = pk_bc<1>(A, m01, g01);   // g1 * (m0, m1)
+          A = pk_bc<1>(A, m23, g23);   // g3 * (m2, m3)
+          B = pk_bc<0>(B, m01, g01);   // g0 * (m0, m1)
+          B = pk_bc<0>(B, m23, g23);   // g2 * (m2, m3)
+          A.x = sfma_v(A.x, g[0], n2.y);
+          A.x = sfma_v(A.x, g[2], m[1]);
+          B.y = sfma_v(B.y, g[1], m[2]);
+          B.y = sfma_v(B.y, g[3], p2.x);
+        };
+        if constexpr (own0) acc(g0, GA[r], GB[r]);          // kd 0: dZ plane za+1 = zd
+        if constexpr (use1) acc(g1, GA[3 + r], GB[3 + r]);  // kd 1: dZ plane za = zd-1
+        if constexpr (use2) acc(g2, GA[6 + r], GB[6 + r]);  // kd 2: dZ plane za-1 = zd-2
+      }
+    }
+    if constexpr (fin) {
+      f4 o = {P[0].x, P[1].x, P[2].x, P[3].x};
+      const bool st = b.own && zf < b.z1;
+      if (MODE == 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float pre = fmaf(sc, epi[i] - mean, sh);
+          const float dp = o[i] * kk * lrelu_d(pre);
+          o[i] = dp;
+          s1 += st ? dp : 0.f;
+          s2 += st ? dp * ((epi[i] - mean) * rstd) : 0.f;
+        }
+      } else if (MODE == 2) {
+        o += epi;
+      }
+      if (st) *reinterpret_cast<f4*>(dxp + (long long)zf * HW + qofs) = o;
+    }
+#if L3U_DWP_PIN
+    // keep each step's accumulation inside the step (no sinking of FMAs past later barriers)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) { pin(GA[t]); pin(GB[t]); }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pin(P[i]);
+    pin(S01);
+    pin(S23);
+#endif
+    P[0] = f2{P[0].y, S01.x};
+    P[1] = f2{P[1].y, S01.y};
+    P[2] = f2{P[2].y, S23.x};
+    P[3] = f2{P[3].y, S23.y};
+    S01 = S23 = zero2;
+    g2 = g1;
+    g1 = g0;
+  };
+  run_steps(step, std::make_integer_sequence<int, TZC + 3>{});
+  // fixed-order workgroup reduction of the 27 taps (+ the IN sums)
+  __syncthreads();
+  float* red = lds;                                        // [nwaves][32]
+  double* redd = reinterpret_cast<double*>(lds + 4 * 32);  // [nwaves][2]
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {   // t = kd * 3 + r
+    const float r0 = wave_sum(GA[t].x), r1 = wave_sum(GA[t].y + GB[t].x), r2 = wave_sum(GB[t].y);
+    if (ln == 0) {
+      red[wv * 32 + t * 3 + 0] = r0;
+      red[wv * 32 + t * 3 + 1] = r1;
+      red[wv * 32 + t * 3 + 2] = r2;
+    }
+  }
+  if (MODE == 1) {
+    const double r1 = wave_sum_d((double)s1), r2 = wave_sum_d((double)s2);
+    if (ln == 0) { redd[wv * 2] = r1; redd[wv * 2 + 1] = r2; }
+  }
+  __syncthreads();
+  const int nchunk = nz * ny;
+  if (threadIdx.x < 27) {
+    float r = 0.f;
+    for (int k = 0; k < nw; ++k) r += red[k * 32 + threadIdx.x];
+    dw_part[((long long)b.c * N * nchunk + (long long)b.n * nchunk + b.ck) * 27 + threadIdx.x] = r;
+  }
+  if (MODE == 1 && threadIdx.x >= 32 && threadIdx.x < 34) {
+    const int j = threadIdx.x - 32;
+    double r = 0.0;
+    for (int k = 0; k < nw; ++k) r += redd[k * 2 + j];
+    in_part[(((long long)b.c * N + b.n) * nchunk + b.ck) * 2 + j] = r;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Whole-volume variants for small planes/volumes (the 12^3 and 6^3 levels): one workgroup per
 // (n, c) holds the whole zero-padded volume [(D+2)(H+2)(W+2)] in LDS and each thread computes
 // voxels v = tid, tid + 256, ... with all 27 taps read straight from LDS.  One load phase and
@@ -1048,8 +1370,8 @@ int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float
 #define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<M_, 0, T_>), grid, block, lds, stream, x, \
       x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W, g.RB, g.RPW, \
       g.ny, g.TZ, g.nz)
-    if (xf) { if (g.TZ == 16) DWQF(1, 16); else if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
-    else { if (g.TZ == 16) DWQF(0, 16); else if (g.TZ == 8) DWQF(0, 8); else if (g.TZ == 4) DWQF(0, 4); else DWQF(0, 2); }
+    if (xf) { TZ24(DWQF(1, 24)) if (g.TZ == 16) DWQF(1, 16); else if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
+    else { TZ24(DWQF(0, 24)) if (g.TZ == 16) DWQF(0, 16); else if (g.TZ == 8) DWQF(0, 8); else if (g.TZ == 4) DWQF(0, 4); else DWQF(0, 2); }
 #undef DWQF
     L3U_CHECK_LAUNCH();
   }
@@ -1099,6 +1421,21 @@ int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long l
   if (use_quads(H, W) && x_nstride % 4 == 0 && dz_nstride % 4 == 0 && dx_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
+    if (L3U_DW_FUSED && parts == 3 && rec == nullptr) {   // MODE 1 measured faster split
+      // single pass: data + weight gradient from one read of dZ and A
+      size_t lds = 4 * (size_t)(g.RB + 2) * (W + kLPad) * sizeof(float);
+      if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch
+#define DWPB(M_, T_) hipLaunchKernelGGL((dw3p_bwd_kernel<M_, T_>), grid, block, lds, stream, dz, \
+      dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
+      g.RPW, g.ny, g.TZ, g.nz)
+#define DWPB_T(M_) do { TZ24(DWPB(M_, 24)) if (g.TZ == 16) DWPB(M_, 16); else if (g.TZ == 8) DWPB(M_, 8); else if (g.TZ == 4) DWPB(M_, 4); else DWPB(M_, 2); } while (0)
+      if (rec) DWPB_T(1);
+      else if (accumulate) DWPB_T(2);
+      else DWPB_T(0);
+#undef DWPB_T
+#undef DWPB
+      L3U_CHECK_LAUNCH();
+    }
     if (dw_split(H, W) || parts != 3) {
       // data gradient = the forward stencil with flipped taps (+ epilogue), then the weight
       // gradient on its own; both use the same tile geometry, so the chunking of dw_part /
@@ -1110,7 +1447,7 @@ int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long l
 #define DWQX(E_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<0, E_, T_>), grid, block, lds, stream, dz, \
       dz_nstride, w, rec, z, 0, dx, dx_nstride, (E_ == 1 ? x : dx), (E_ == 1 ? x_nstride : dx_nstride), \
       in_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
-#define DWQX_T(E_) do { if (g.TZ == 16) DWQX(E_, 16); else if (g.TZ == 8) DWQX(E_, 8); else if (g.TZ == 4) DWQX(E_, 4); else DWQX(E_, 2); } while (0)
+#define DWQX_T(E_) do { TZ24(DWQX(E_, 24)) if (g.TZ == 16) DWQX(E_, 16); else if (g.TZ == 8) DWQX(E_, 8); else if (g.TZ == 4) DWQX(E_, 4); else DWQX(E_, 2); } while (0)
         if (rec) DWQX_T(1);
         else if (accumulate) DWQX_T(2);
         else DWQX_T(3);
@@ -1122,7 +1459,7 @@ int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long l
         if (lds2 < 128 * sizeof(float)) lds2 = 128 * sizeof(float);
 #define DWQW(X_, T_) hipLaunchKernelGGL((dw3q_dw_kernel<X_, T_>), grid, block, lds2, stream, dz, \
       dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
-#define DWQW_T(X_) do { if (g.TZ == 16) DWQW(X_, 16); else if (g.TZ == 8) DWQW(X_, 8); else if (g.TZ == 4) DWQW(X_, 4); else DWQW(X_, 2); } while (0)
+#define DWQW_T(X_) do { TZ24(DWQW(X_, 24)) if (g.TZ == 16) DWQW(X_, 16); else if (g.TZ == 8) DWQW(X_, 8); else if (g.TZ == 4) DWQW(X_, 4); else DWQW(X_, 2); } while (0)
         if (rec) DWQW_T(1);
         else DWQW_T(0);
 #undef DWQW_T
@@ -1135,7 +1472,7 @@ int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long l
 #define DWQB(M_, T_) hipLaunchKernelGGL((dw3q_bwd_kernel<M_, T_>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
       g.RPW, g.ny, g.TZ, g.nz)
-#define DWQB_T(M_) do { if (g.TZ == 16) DWQB(M_, 16); else if (g.TZ == 8) DWQB(M_, 8); else if (g.TZ == 4) DWQB(M_, 4); else DWQB(M_, 2); } while (0)
+#define DWQB_T(M_) do { TZ24(DWQB(M_, 24)) if (g.TZ == 16) DWQB(M_, 16); else if (g.TZ == 8) DWQB(M_, 8); else if (g.TZ == 4) DWQB(M_, 4); else DWQB(M_, 2); } while (0)
     if (rec) DWQB_T(1);
     else if (accumulate) DWQB_T(2);
     else DWQB_T(0);

@@ -753,8 +753,9 @@ def test_outconv_ftl_fused(cuda, case):
                                    (1, 5, 7, 12, 8)])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_dw3_bwd_split_calls(cuda, shape, mode):
-    """l3u_dw3_bwd_data + l3u_dw3_bwd_weight (the engine issues them on two streams) give
-    bitwise the results of the combined l3u_dw3_bwd (mode 2 = accumulate into dx)."""
+    """l3u_dw3_bwd_data + l3u_dw3_bwd_weight agree with the combined single-pass l3u_dw3_bwd
+    (mode 2 = accumulate into dx).  The combined call sums the taps in another order (packed
+    FMAs), so the comparison is to fp32 rounding: 1e-5 of the tensor's max."""
     N, C, D, H, W = shape
     S = D * H * W
     gen = torch.Generator().manual_seed(31)
@@ -784,10 +785,12 @@ def test_dw3_bwd_split_calls(cuda, shape, mode):
         return dx, dwp, inp
 
     a, b = run(False), run(True)
-    assert torch.equal(a[0], b[0])
-    assert torch.equal(a[1], b[1])
+    close(a[0], b[0], 1e-5, f"dx {shape} mode{mode}")
+    close(a[1].view(C, -1, 27).double().sum(1), b[1].view(C, -1, 27).double().sum(1), 1e-5,
+          f"dW {shape} mode{mode}")
     if rec is not None:
-        assert torch.equal(a[2], b[2])
+        close(a[2].view(C, N, -1, 2).sum(2), b[2].view(C, N, -1, 2).sum(2), 1e-5,
+              f"IN sums {shape}")
 
 
 # (N, Ci, Co, D, H, W): the network's three up-blocks (low-res volumes) plus ragged ones
