@@ -9,7 +9,8 @@ timed step).  N > 1: one process per GPU (torch.distributed.run), exact global-b
 (3-float all-reduce) + one flat-gradient RCCL all-reduce per step; per-GPU batch fixed (weak
 scaling); time = max over ranks.
 
-Also reported: eval forward ms/patch (bs 1 and 4), the config-4 whole-volume sliding-window
+Also reported: eval forward ms/patch (bs 1 and 4), config 5 (32->256, 64^3, step-based mixed
+domains) on one GPU, the config-4 whole-volume sliding-window
 inference of a 256^3 synthetic PET volume (seconds, ms/window; light_unet.utils), the roofline of
 the dominant kernel measured with HIP events around back-to-back replays of its C-ABI call, and
 the CPU baseline (the torch-CPU oracle restatement of the same network on this host's cores,
@@ -48,6 +49,7 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--ftl-mode", default="exact", choices=["exact", "local"])
     ap.add_argument("--no-sliding", action="store_true", help="skip the config-4 inference timing")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (32->256, 64^3) timing")
     # multi-rank rehearsal on a one-GPU box: every rank on cuda:0, collectives over gloo
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--one-device", action="store_true")
@@ -218,6 +220,50 @@ def sliding_bench(model, device, size=256):
             "note": "includes the host->device upload and the prob-map copy back"}
 
 
+def config5_bench(device, steps=20, warmup=5, bs=4, size=64, enc=(32, 64, 128, 256)):
+    """SURVEY §8d config 5 on this GPU: encoder 32->64->128->256 (812,284 parameters), 64^3
+    patches, bs 4, the reference's step-based mixed-domain epoch (trainer.py:260-347) with
+    dlbcl_steps_ratio 1.0: the FL stream's steps, then as many DLBCL steps, two synthetic
+    streams seeded 42 and 43 (loader.py:37 seed+1).  Graph-replayed step; per-GPU figure (the
+    8-GPU run of this config is the driver's)."""
+    from light_unet.models.unet3d import Lightweight3DUNet
+    from light_unet.train_step import TrainStep
+    torch.manual_seed(42)
+    model = Lightweight3DUNet(encoder_channels=list(enc), dropout_p=0.1).to(device).train()
+    step = TrainStep(model, {"alpha": 0.7, "beta": 0.3, "gamma": 0.75}, lr=1e-4, weight_decay=1e-5)
+    streams = []
+    for seed in (42, 43):   # FL, DLBCL
+        rng = np.random.default_rng(seed)
+        x = torch.from_numpy(rng.random((bs, 1, size, size, size), dtype=np.float32)).to(device)
+        t = torch.from_numpy((rng.random((bs, 1, size, size, size)) > 0.97).astype(np.float32)).to(device)
+        streams.append((x, t))
+    xs, ts = streams[0][0].clone(), streams[0][1].clone()
+    step.capture(xs, ts, warmup=2)
+    half = steps // 2
+
+    def run(i, n):
+        src = streams[0] if i < n // 2 else streams[1]   # FL stage, then the DLBCL stage
+        xs.copy_(src[0], non_blocking=True)
+        ts.copy_(src[1], non_blocking=True)
+        return step.replay()
+
+    for i in range(warmup):
+        run(i, warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = run(i, steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    lv = float(loss.item())
+    if not np.isfinite(lv):
+        raise SystemExit(f"config 5: non-finite loss {lv}")
+    return {"workload": f"Lightweight3DUNet {'->'.join(map(str, enc))} train step, {size}^3, bs {bs}, "
+                        f"step-based FL ({half} steps) then DLBCL ({steps - half} steps)",
+            "params": int(model.flat_parameters().numel()), "patches_per_s_per_gpu": round(steps * bs / dt, 2),
+            "ms_per_step": round(1000 * dt / steps, 4), "final_loss": round(lv, 6)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -295,6 +341,7 @@ def main():
         raise SystemExit(f"non-finite loss {final_loss}")
 
     sliding = sliding_bench(model, device) if (rank == 0 and not args.no_sliding) else None
+    cfg5 = config5_bench(device) if (rank == 0 and not args.no_config5) else None
     fwd1 = fwd_ms_per_patch(model, 1, args.size, device) if rank == 0 else None
     fwd4 = fwd_ms_per_patch(model, args.batch, args.size, device) if rank == 0 else None
     out = None
@@ -327,6 +374,7 @@ def main():
             "fwd_ms_per_patch": {"bs1": round(fwd1, 4), f"bs{args.batch}": round(fwd4, 4)},
             "final_loss": round(final_loss, 6),
             "sliding_window_256": sliding,
+            "config5_1gpu": cfg5,
             "roofline": {
                 "kernel": f"l3u_dw3_bwd [{N},{cdom},{args.size}^3] (up3.res_block.conv1.depthwise "
                           "backward: flipped-tap data-gradient stencil + weight-gradient pass, "
