@@ -377,8 +377,8 @@ def main():
             "config5_1gpu": cfg5,
             "roofline": {
                 "kernel": f"l3u_dw3_bwd [{N},{cdom},{args.size}^3] (up3.res_block.conv1.depthwise "
-                          "backward: flipped-tap data-gradient stencil + weight-gradient pass, "
-                          "timed together as one C-ABI call)",
+                          "backward: one single-pass launch, data and weight gradients from one "
+                          "LDS-DMA-staged read of dZ and A)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS,

@@ -937,6 +937,22 @@ L3U_DEV void q_row3(const float* plane, int row, int lp, int ox, bool el, bool e
 #endif
 }
 
+// the same from an already-read quad m0 (neighbours by DPP, or from LDS in the padded layout)
+L3U_DEV void q_nbr3(const f4& m0, const float* plane, int row, int lp, int ox, bool el, bool er,
+                    f2& n2, f4& m, f2& p2) {
+  m = m0;
+#if L3U_DWP_LDSNB
+  const float* q = plane + row * lp + ox;
+  n2 = *reinterpret_cast<const f2*>(q + kLOfs - 2);
+  p2 = *reinterpret_cast<const f2*>(q + kLOfs + 4);
+#else
+  const float pl = lane_prev(m[3]), pr = lane_next(m[0]);
+  const float l = el ? 0.f : pl, r = er ? 0.f : pr;
+  n2 = f2{l, l};
+  p2 = f2{r, r};
+#endif
+}
+
 // acc + a * {b[H], b[H]}: the product with one half of an aligned register pair broadcast to both
 // lanes of the packed FMA (op_sel picks the half; the compiler only folds the low-half case)
 template <int H>
@@ -973,8 +989,46 @@ L3U_DEV f2 pk_bc_s(f2 acc, f2 a, f2 b) {   // a wave-uniform (SGPR pair)
   return acc;
 }
 
-template <int MODE, int TZC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L3U_DWP_WAVES))) void dw3p_bwd_kernel(
+// LDS-DMA staging (GL = true, one-wave tiles): each plane goes global -> LDS with
+// global_load_lds_dwordx4 (no staging VGPRs, no ds_write), PD planes ahead in a ring of PD + 1
+// buffers of 128 quads per tensor.  Lane l of slot k lands at quad 64k + l, which is the q_map
+// order; lanes whose quad lies outside the volume (rows y = -1 / H, planes z = -1 / D) or past
+// the tile (slot-1 tail) read a zero page instead, so every wave issues exactly 2 DMAs per
+// tensor per step and the waits are static counts.  The DMA is inline asm (M0 is written in the
+// same statement), so its completion is counted here, not by the compiler: see dw_wait_vm.
+#ifndef L3U_DWG
+#define L3U_DWG 1
+#endif
+#ifndef L3U_DWG_PD
+#define L3U_DWG_PD 1
+#endif
+#ifndef L3U_DWG_WAVES
+#define L3U_DWG_WAVES 4
+#endif
+__device__ __attribute__((aligned(16))) float g_l3u_zero_page[256];   // 1 KiB of zeros (64 lanes x 16 B)
+
+L3U_DEV void glds16(const float* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+// DMAs issued for plane step t (2 slots per loaded tensor; see gissue)
+template <int TZC>
+constexpr int gl_n(int t) { return 2 * ((t < TZC + 2 ? 1 : 0) + (t > 0 ? 1 : 0)); }
+// DMAs younger than plane step s's when step s waits for it (planes s+1 .. s+PD, if issued)
+template <int TZC, int PD>
+constexpr int gl_younger(int s) {
+  int n = 0;
+  for (int t = s + 1; t <= s + PD && t < TZC + 3; ++t) n += gl_n<TZC>(t);
+  return n;
+}
+template <int NOUT>
+L3U_DEV void dw_wait_vm() {   // at most NOUT vector-memory operations still outstanding
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NOUT) : "memory");
+}
+
+template <int MODE, int TZC, bool GL = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? L3U_DWG_WAVES : L3U_DWP_WAVES))) void dw3p_bwd_kernel(
     const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
     long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part,
@@ -988,6 +1042,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L3U_DWP_WAV
   float* dxp = dx + (long long)b.n * dxns + cofs;
   float* dzb = lds;             // 2 planes
   float* ab = lds + 2 * PP;     // 2 planes
+  constexpr int GNB = L3U_DWG_PD + 1;                  // DMA ring buffers per tensor
+  const int GPS = (RB + 2) * W;                        // floats per ring buffer (nq quads)
   // flipped data-gradient taps: pair (kd 0, kd 1) and kd 2 per in-plane tap (r, dx)
   f2 wp[9];
   float w2[9];
@@ -1002,7 +1058,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L3U_DWP_WAV
     const float* r = rec + (long long)b.nc * kRec;
     mean = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];
   }
-  for (int i = threadIdx.x; i < 4 * PP; i += blockDim.x) lds[i] = 0.f;
+  if (!GL)
+    for (int i = threadIdx.x; i < 4 * PP; i += blockDim.x) lds[i] = 0.f;
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
   const f2 zero2 = {0.f, 0.f};
   f2 P[4];                      // (dA plane zd-1, dA plane zd) per voxel of the quad
@@ -1017,15 +1074,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L3U_DWP_WAV
   const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
   const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
   // register staging PD planes ahead (sets alternate by step parity when PD = 2)
-  constexpr int PD = L3U_DWP_PD;
+  constexpr int PD = GL ? 1 : L3U_DWP_PD;
   QPre pzs[PD], pas[PD];
   const QMap qm = q_map(b.y0, b.rows, H, W, WQ, LP, kLOfs);
   auto in_rng = [&](int z) { return z >= zlo && z <= zhi; };
   auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };
+  const unsigned lbase = (unsigned)(size_t)lds;
+  const float* zpage = g_l3u_zero_page + 4 * (threadIdx.x & 63);
+  // DMA of plane step t (dZ plane z0-1+t, A plane z0-2+t) into ring buffer t % GNB.  Step 0's A
+  // plane and the last step's dZ plane are never used: not loaded (gl_n gives the DMA count).
+  // Slot 1 is issued by the lanes of its nq - 64 quads only (nq > 64 for one-wave tiles, so the
+  // instruction always issues and the count stays static).
+  const int nq = (RB + 2) * WQ;
+  auto gissue = [&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const int z_d = b.z0 - 1 + t, z_a = z_d - 1;
+    const bool ind = in_rng(z_d), ina = in_rng(z_a);
+    const unsigned bz = lbase + (unsigned)((t % GNB) * GPS) * 4u;
+    const unsigned ba = lbase + (unsigned)((GNB + t % GNB) * GPS) * 4u;
 #pragma unroll
-  for (int k = 0; k < PD; ++k) {
-    q_fetch(pzs[k], dzp + zc(b.z0 - 1 + k), qm);
-    q_fetch(pas[k], xp + zc(b.z0 - 2 + k), qm);
+    for (int k = 0; k < 2; ++k) {
+      if (k == 1 && (int)threadIdx.x >= nq - 64) continue;
+      const float* sd = (qm.ok[k] && ind) ? dzp + (long long)z_d * HW + qm.goff[k] : zpage;
+      const float* sa = (qm.ok[k] && ina) ? xp + (long long)z_a * HW + qm.goff[k] : zpage;
+      if constexpr (t < TZC + 2) glds16(sd, bz + k * 1024u);
+      if constexpr (t > 0) glds16(sa, ba + k * 1024u);
+    }
+  };
+  if constexpr (GL) {
+    run_steps(gissue, std::make_integer_sequence<int, L3U_DWG_PD>{});
+  } else {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      q_fetch(pzs[k], dzp + zc(b.z0 - 1 + k), qm);
+      q_fetch(pas[k], xp + zc(b.z0 - 2 + k), qm);
+    }
   }
   __syncthreads();
   auto step = [&](auto I) {
@@ -1040,25 +1123,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L3U_DWP_WAV
     constexpr bool use2 = s >= 3 && s <= TZC + 2;   // dZ plane zd-2 owned
     constexpr bool fin = s >= 2 && s <= TZC + 1;    // dA plane zd-1 completes in the slab
     const int zd = b.z0 - 1 + s, za = zd - 1;
-    float* dbuf = dzb + (s & 1) * PP;
-    float* abuf = ab + (s & 1) * PP;
-    q_commit<false>(pz, dbuf, qm, in_rng(zd), 1.f, 0.f, 0.f);
-    q_commit<MODE == 1>(pa, abuf, qm, in_rng(za), sc, mean, sh);
-    if constexpr (s + PD < TZC + 3) {
-      q_fetch(pz, dzp + zc(zd + PD), qm);
-      q_fetch(pa, xp + zc(za + PD), qm);
+    float* dbuf = GL ? lds + (s % GNB) * GPS : dzb + (s & 1) * PP;
+    float* abuf = GL ? lds + (GNB + s % GNB) * GPS : ab + (s & 1) * PP;
+    if constexpr (GL) {
+      // issue plane s + PD (its ring buffer was last read in step s - 1), then wait for plane s:
+      // younger than plane s's 4 DMAs are those of planes s+1 .. s+PD (stores between them only
+      // make the wait longer)
+      if constexpr (s + L3U_DWG_PD < TZC + 3) gissue(std::integral_constant<int, s + L3U_DWG_PD>{});
+      dw_wait_vm<gl_younger<TZC, L3U_DWG_PD>(s)>();
+    } else {
+      q_commit<false>(pz, dbuf, qm, in_rng(zd), 1.f, 0.f, 0.f);
+      q_commit<MODE == 1>(pa, abuf, qm, in_rng(za), sc, mean, sh);
+      if constexpr (s + PD < TZC + 3) {
+        q_fetch(pz, dzp + zc(zd + PD), qm);
+        q_fetch(pa, xp + zc(za + PD), qm);
+      }
     }
     const int zf = zd - 1;
     f4 epi = zero4;
     if constexpr (MODE != 0 && fin)
       epi = *reinterpret_cast<const f4*>((MODE == 1 ? xp : dxp) + (long long)min(max(zf, 0), D - 1) * HW + qofs);
     __syncthreads();
-    if constexpr (doP || doS || own0) {
+    // all six LDS rows of the step are read up front (one latency for the step, not three)
+    constexpr bool needD = doP || doS || own0, needA = own0 || use1 || use2;
+    f4 rowd[3], rowa[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      if (needD) rowd[r] = *reinterpret_cast<const f4*>(dbuf + (b.oy + r) * LP + kLOfs + b.ox);
+      if (needA) rowa[r] = *reinterpret_cast<const f4*>(abuf + (b.oy + r) * LP + kLOfs + b.ox);
+    }
+    if constexpr (needD) {
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         f2 n2, p2;
         f4 m;
-        q_row3(dbuf, b.oy + r, LP, b.ox, b.el, b.er, n2, m, p2);
+        q_nbr3(rowd[r], dbuf, b.oy + r, LP, b.ox, b.el, b.er, n2, m, p2);
         const f2 m01 = {m[0], m[1]}, m23 = {m[2], m[3]};
         if (r == 1 && own0) g0 = (b.own && zd < b.z1) ? m : zero4;
         if constexpr (doP) {
@@ -1084,12 +1183,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L3U_DWP_WAV
         }
       }
     }
-    if constexpr (own0 || use1 || use2) {
+    if constexpr (needA) {
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         f2 n2, p2;
         f4 m;
-        q_row3(abuf, b.oy + r, LP, b.ox, b.el, b.er, n2, m, p2);
+        q_nbr3(rowa[r], abuf, b.oy + r, LP, b.ox, b.el, b.er, n2, m, p2);
         const f2 m01 = {m[0], m[1]}, m23 = {m[2], m[3]};
         auto acc = [&](const f4& g, f2& A, f2& B) {
           const f2 g01 = {g[0], g[1]}, g23 = {g[2], g[3]};
@@ -1425,9 +1524,14 @@ int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long l
       // single pass: data + weight gradient from one read of dZ and A
       size_t lds = 4 * (size_t)(g.RB + 2) * (W + kLPad) * sizeof(float);
       if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch
-#define DWPB(M_, T_) hipLaunchKernelGGL((dw3p_bwd_kernel<M_, T_>), grid, block, lds, stream, dz, \
+      const bool gl = L3U_DWG && g.threads == 64 && (g.RB + 2) * g.WQ <= 128 && g.WQ * 4 == W;
+      if (gl) lds = 2 * (L3U_DWG_PD + 1) * (size_t)(g.RB + 2) * g.WQ * 16;
+#define DWPB(M_, T_) do { if (gl) hipLaunchKernelGGL((dw3p_bwd_kernel<M_, T_, true>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
-      g.RPW, g.ny, g.TZ, g.nz)
+      g.RPW, g.ny, g.TZ, g.nz); \
+      else hipLaunchKernelGGL((dw3p_bwd_kernel<M_, T_>), grid, block, lds, stream, dz, \
+      dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
+      g.RPW, g.ny, g.TZ, g.nz); } while (0)
 #define DWPB_T(M_) do { TZ24(DWPB(M_, 24)) if (g.TZ == 16) DWPB(M_, 16); else if (g.TZ == 8) DWPB(M_, 8); else if (g.TZ == 4) DWPB(M_, 4); else DWPB(M_, 2); } while (0)
       if (rec) DWPB_T(1);
       else if (accumulate) DWPB_T(2);
