@@ -1005,6 +1005,12 @@ L3U_DEV f2 pk_bc_s(f2 acc, f2 a, f2 b) {   // a wave-uniform (SGPR pair)
 #ifndef L3U_DWG_WAVES
 #define L3U_DWG_WAVES 4
 #endif
+#ifndef L3U_DWG_WAVES1
+#define L3U_DWG_WAVES1 3   // the IN-fused MODE 1 (measured: 3 > 4, which spills)
+#endif
+#ifndef L3U_DWG_MODE1
+#define L3U_DWG_MODE1 1    // MODE 1 on the LDS-DMA single pass (0: the split passes)
+#endif
 __device__ __attribute__((aligned(16))) float g_l3u_zero_page[256];   // 1 KiB of zeros (64 lanes x 16 B)
 
 L3U_DEV void glds16(const float* gsrc, unsigned lds_dst) {
@@ -1028,7 +1034,7 @@ L3U_DEV void dw_wait_vm() {   // at most NOUT vector-memory operations still out
 }
 
 template <int MODE, int TZC, bool GL = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? L3U_DWG_WAVES : L3U_DWP_WAVES))) void dw3p_bwd_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE == 1 ? L3U_DWG_WAVES1 : L3U_DWG_WAVES) : L3U_DWP_WAVES))) void dw3p_bwd_kernel(
     const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
     long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part,
@@ -1080,6 +1086,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? L3U_DW
   auto in_rng = [&](int z) { return z >= zlo && z <= zhi; };
   auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };
   const unsigned lbase = (unsigned)(size_t)lds;
+  float rv[3];   // MODE 1 (GL): row r of the thread's 3-row window lies inside the volume
+#pragma unroll
+  for (int r = 0; r < 3; ++r) rv[r] = (unsigned)(b.y0 + b.oy + r - 1) < (unsigned)H ? 1.f : 0.f;
   const float* zpage = g_l3u_zero_page + 4 * (threadIdx.x & 63);
   // DMA of plane step t (dZ plane z0-1+t, A plane z0-2+t) into ring buffer t % GNB.  Step 0's A
   // plane and the last step's dZ plane are never used: not loaded (gl_n gives the DMA count).
@@ -1141,7 +1150,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? L3U_DW
     }
     const int zf = zd - 1;
     f4 epi = zero4;
-    if constexpr (MODE != 0 && fin)
+    // GL + MODE 1: the pre-IN activation of plane zf = za is the tile's own raw A row in LDS
+    if constexpr (MODE != 0 && fin && !(GL && MODE == 1))
       epi = *reinterpret_cast<const f4*>((MODE == 1 ? xp : dxp) + (long long)min(max(zf, 0), D - 1) * HW + qofs);
     __syncthreads();
     // all six LDS rows of the step are read up front (one latency for the step, not three)
@@ -1151,6 +1161,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? L3U_DW
     for (int r = 0; r < 3; ++r) {
       if (needD) rowd[r] = *reinterpret_cast<const f4*>(dbuf + (b.oy + r) * LP + kLOfs + b.ox);
       if (needA) rowa[r] = *reinterpret_cast<const f4*>(abuf + (b.oy + r) * LP + kLOfs + b.ox);
+    }
+    f4 pre1 = zero4, d1 = zero4;   // GL + MODE 1: own row's pre-activation and (y - mean)
+    if constexpr (GL && MODE == 1 && needA) {
+      // the DMA staged y itself: A = lrelu(scale*(y-mean)+shift) is formed at the read (packed
+      // ops), with the conv's zero padding in the A domain: rows / planes outside the volume
+      // hold zero-page values and get scale = shift = 0
+      float zm = in_rng(za) ? 1.f : 0.f;
+      pin(zm);   // formed here: keeps the compiler from hoisting 3 x (TZC+3) masks
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const float mr = zm * rv[r];
+        const f2 sc2 = {sc * mr, sc * mr}, sh2 = {sh * mr, sh * mr}, mu2 = {mean, mean};
+        f2 lo = f2{rowa[r][0], rowa[r][1]} - mu2, hi = f2{rowa[r][2], rowa[r][3]} - mu2;
+        if (fin && r == 1) d1 = f4{lo.x, lo.y, hi.x, hi.y};
+        lo = pfma(sc2, lo, sh2);
+        hi = pfma(sc2, hi, sh2);
+        if (fin && r == 1) pre1 = f4{lo.x, lo.y, hi.x, hi.y};
+        const f2 ls = lo * f2{kSlope, kSlope}, hs = hi * f2{kSlope, kSlope};
+        rowa[r] = f4{fmaxf(lo.x, ls.x), fmaxf(lo.y, ls.y), fmaxf(hi.x, hs.x), fmaxf(hi.y, hs.y)};
+      }
     }
     if constexpr (needD) {
 #pragma unroll
@@ -1209,7 +1239,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? L3U_DW
     if constexpr (fin) {
       f4 o = {P[0].x, P[1].x, P[2].x, P[3].x};
       const bool st = b.own && zf < b.z1;
-      if (MODE == 1) {
+      if (MODE == 1 && GL) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float dp = o[i] * kk * lrelu_d(pre1[i]);
+          o[i] = dp;
+          s1 += st ? dp : 0.f;
+          s2 += st ? dp * (d1[i] * rstd) : 0.f;
+        }
+      } else if (MODE == 1) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float pre = fmaf(sc, epi[i] - mean, sh);
@@ -1231,6 +1269,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? L3U_DW
     for (int i = 0; i < 4; ++i) pin(P[i]);
     pin(S01);
     pin(S23);
+    if constexpr (MODE == 1 && fin) { pin(s1); pin(s2); }   // else the IN sums sink to the end
 #endif
     P[0] = f2{P[0].y, S01.x};
     P[1] = f2{P[1].y, S01.y};
@@ -1520,11 +1559,12 @@ int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long l
   if (use_quads(H, W) && x_nstride % 4 == 0 && dz_nstride % 4 == 0 && dx_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
-    if (L3U_DW_FUSED && parts == 3 && rec == nullptr) {   // MODE 1 measured faster split
+    const bool gl = L3U_DWG && g.threads == 64 && (g.RB + 2) * g.WQ <= 128 && g.WQ * 4 == W;
+    // MODE 1 (IN-fused) only on the LDS-DMA variant: register-staged it measured faster split
+    if (L3U_DW_FUSED && parts == 3 && (rec == nullptr || (gl && L3U_DWG_MODE1))) {
       // single pass: data + weight gradient from one read of dZ and A
       size_t lds = 4 * (size_t)(g.RB + 2) * (W + kLPad) * sizeof(float);
       if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch
-      const bool gl = L3U_DWG && g.threads == 64 && (g.RB + 2) * g.WQ <= 128 && g.WQ * 4 == W;
       if (gl) lds = 2 * (L3U_DWG_PD + 1) * (size_t)(g.RB + 2) * g.WQ * 16;
 #define DWPB(M_, T_) do { if (gl) hipLaunchKernelGGL((dw3p_bwd_kernel<M_, T_, true>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
