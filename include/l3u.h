@@ -242,6 +242,30 @@ int l3u_adamw(float* p, const float* g, float* m, float* v, long long numel, con
               float beta1, float beta2, float eps, float weight_decay, int* step, float grad_scale,
               hipStream_t stream);
 
+/* ---- grouped / dense 3x3x3 conv (stride 1, padding 1, no bias): the
+ * use_depthwise_separable=False path of ResidualBlock (GroupedConv3d unet3d.py:26-34, chosen at
+ * :46-47 / :57-58; nn.Conv3d unet3d.py:49 / :60, G = 1).  w: torch weight [Cout][Cin/G][3][3][3].
+ * fwd: rec != NULL transforms the input on load, a = lrelu(scale*(x-mean)+shift) (the record of
+ *      the preceding InstanceNorm + LeakyReLU + Dropout3d, unet3d.py:84-88); stat_part != NULL
+ *      also writes the (count, mean, M2) partials [N][Cout][l3u_gconv3_nblocks(S)][3] that
+ *      l3u_in_finalize / l3u_norm_src consume (the format of l3u_pw_fwd).
+ * bwd_data: dx (+)= conv^T(dy); rec != NULL: the IN-fused form, dx = dpre = conv^T(dy)*k*
+ *      lrelu'(pre) with pre from ep (the saved pre-IN activation) and the IN-backward partials
+ *      in_part[Cin][N][l3u_gconv3_nblocks(S)][2] as l3u_dw3_bwd writes them.
+ * bwd_weight: part[P][Cout][Cin/G][27], P = l3u_gconv3_wgrad_nparts(N, S); rec as in fwd.      */
+int l3u_gconv3_nblocks(int S);
+int l3u_gconv3_wgrad_nparts(int N, int S);
+int l3u_gconv3_fwd(const float* x, long long x_nstride, const float* w, const float* rec,
+                   float* y, long long y_nstride, float* stat_part, int N, int Cin, int Cout,
+                   int G, int D, int H, int W, hipStream_t stream);
+int l3u_gconv3_bwd_data(const float* dy, long long dy_nstride, const float* w, const float* rec,
+                        const float* ep, long long ep_nstride, float* dx, long long dx_nstride,
+                        int accumulate, double* in_part, int N, int Cin, int Cout, int G, int D,
+                        int H, int W, hipStream_t stream);
+int l3u_gconv3_bwd_weight(const float* dy, long long dy_nstride, const float* x,
+                          long long x_nstride, const float* rec, float* part, int N, int Cin,
+                          int Cout, int G, int D, int H, int W, hipStream_t stream);
+
 /* ---- deterministic second-stage reduction --------------------------------------------------
  * items[nitems][8] int64 = {src_off, count, istride, tstride, len<=256, dst_off, accumulate, f64}:
  * dst[dst_off+t] (+)= sum_{i<count} src[src_off + i*istride + t*tstride], summed in fp64;

@@ -35,25 +35,43 @@ class V:
         return self.t.data_ptr() + F32 * self.off
 
 
-def param_layout(enc, in_channels=1, out_channels=1):
+def conv_kinds(cin, cout, use_depthwise_separable=True, use_grouped=True, groups=8):
+    """(conv1, conv2) of a ResidualBlock as the reference chooses them (unet3d.py:43-60):
+    ("ds", 0) DepthwiseSeparableConv3d, ("grouped", G) GroupedConv3d, ("dense", 1) nn.Conv3d."""
+    if use_depthwise_separable:
+        return ("ds", 0), ("ds", 0)
+    k1 = ("grouped", groups) if (use_grouped and groups > 1 and cin >= groups and cout >= groups) \
+        else ("dense", 1)
+    k2 = ("grouped", groups) if (use_grouped and groups > 1 and cout >= groups) else ("dense", 1)
+    return k1, k2
+
+
+def _conv_params(pre, kind, cin, cout):
+    if kind[0] == "ds":
+        return [(pre + "depthwise.weight", (cin, 1, 3, 3, 3)),
+                (pre + "pointwise.weight", (cout, cin, 1, 1, 1))]
+    if kind[0] == "grouped":
+        return [(pre + "conv.weight", (cout, cin // kind[1], 3, 3, 3))]
+    return [(pre + "weight", (cout, cin, 3, 3, 3))]
+
+
+def param_layout(enc, in_channels=1, out_channels=1, use_depthwise_separable=True,
+                 use_grouped=True, groups=8):
     """(name, shape) in reference registration order (unet3d.py:146-202)."""
     out = []
 
-    def rb(pre, cin, cout):
-        out.extend([
-            (pre + "conv1.depthwise.weight", (cin, 1, 3, 3, 3)),
-            (pre + "conv1.pointwise.weight", (cout, cin, 1, 1, 1)),
-            (pre + "norm1.weight", (cout,)), (pre + "norm1.bias", (cout,)),
-            (pre + "conv2.depthwise.weight", (cout, 1, 3, 3, 3)),
-            (pre + "conv2.pointwise.weight", (cout, cout, 1, 1, 1)),
-            (pre + "norm2.weight", (cout,)), (pre + "norm2.bias", (cout,)),
-        ])
+    def rb(pre, cin, cout, grouped=True):
+        k1, k2 = conv_kinds(cin, cout, use_depthwise_separable, use_grouped and grouped, groups)
+        out.extend(_conv_params(pre + "conv1.", k1, cin, cout))
+        out.extend([(pre + "norm1.weight", (cout,)), (pre + "norm1.bias", (cout,))])
+        out.extend(_conv_params(pre + "conv2.", k2, cout, cout))
+        out.extend([(pre + "norm2.weight", (cout,)), (pre + "norm2.bias", (cout,))])
         if cin != cout:
             out.extend([(pre + "shortcut.0.weight", (cout, cin, 1, 1, 1)),
                         (pre + "shortcut.1.weight", (cout,)), (pre + "shortcut.1.bias", (cout,))])
 
     c0, c1, c2, c3 = enc
-    rb("init_conv.", in_channels, c0)
+    rb("init_conv.", in_channels, c0, grouped=False)   # first layer: regular conv (:163-167)
     rb("down1.res_block.", c0, c1)
     rb("down2.res_block.", c1, c2)
     rb("down3.res_block.", c2, c3)
@@ -93,7 +111,7 @@ class UNetEngine:
               "bottleneck.", "up1.res_block.", "up2.res_block.", "up3.res_block.")
 
     def __init__(self, encoder_channels=(16, 32, 64, 128), in_channels=1, out_channels=1,
-                 seed=0x5EED):
+                 seed=0x5EED, use_depthwise_separable=True, use_grouped=True, groups=8):
         if in_channels != 1 or out_channels != 1:
             raise NotImplementedError("the MI355X path implements in_channels = out_channels = 1 "
                                       "(the reference's only configuration, trainer.py:57-66)")
@@ -103,7 +121,20 @@ class UNetEngine:
         if enc[0] > 32:
             raise NotImplementedError("out_conv kernel supports encoder_channels[0] <= 32")
         self.enc = enc
-        self.layout = param_layout(enc)
+        self.layout = param_layout(enc, use_depthwise_separable=use_depthwise_separable,
+                                   use_grouped=use_grouped, groups=groups)
+        chans = {"init_conv.": (1, enc[0], False), "down1.res_block.": (enc[0], enc[1], True),
+                 "down2.res_block.": (enc[1], enc[2], True), "down3.res_block.": (enc[2], enc[3], True),
+                 "bottleneck.": (enc[3], enc[3], True), "up1.res_block.": (enc[3], enc[2], True),
+                 "up2.res_block.": (enc[2], enc[1], True), "up3.res_block.": (enc[1], enc[0], True)}
+        # per block: the conv kinds of conv1 / conv2 (unet3d.py:43-60)
+        self.kinds = {pre: conv_kinds(ci, co, use_depthwise_separable, use_grouped and g, groups)
+                      for pre, (ci, co, g) in chans.items()}
+        for pre, ks in self.kinds.items():
+            for k, (ci, co) in zip(ks, ((chans[pre][0], chans[pre][1]), (chans[pre][1], chans[pre][1]))):
+                if k[0] == "grouped" and (ci % k[1] or co % k[1]):
+                    raise ValueError(f"{pre}: in_channels {ci} / out_channels {co} must be divisible "
+                                     f"by groups {k[1]} (nn.Conv3d)")
         self.offsets = {}
         off = 0
         for name, shape in self.layout:
@@ -272,6 +303,8 @@ class UNetEngine:
     def _block_fwd(self, flat, pre, layer, x, out, dims, drop, cptr, st, dev, pool=None):
         """ResidualBlock.forward (unet3d.py:77-93) into the view `out`; pool = (pooled, idx):
         also the MaxPool3d(2) of the output (the next DownBlock's pool) in the same launch."""
+        if self.kinds[pre][0][0] != "ds":
+            return self._block_fwd_g(flat, pre, layer, x, out, dims, drop, cptr, st, dev, pool)
         N = x.t.shape[0]
         d, h, w = dims
         S = d * h * w
@@ -325,6 +358,66 @@ class UNetEngine:
                        1 if shortcut else 0, out.p, out.ns, pooled.data_ptr(), cout * (S // 8),
                        idx.data_ptr(), N, cout, d, h, w, st)
         sv.update(z1=z1, y1=y1, z2=z2, y2=y2, dims=dims, shortcut=shortcut)
+        return sv
+
+    def _conv_w(self, flat, pre, which):
+        kind = self.kinds[pre][which - 1]
+        name = pre + f"conv{which}." + ("conv.weight" if kind[0] == "grouped" else "weight")
+        return name, self._w(flat, name), (kind[1] if kind[0] == "grouped" else 1)
+
+    def _block_fwd_g(self, flat, pre, layer, x, out, dims, drop, cptr, st, dev, pool=None):
+        """ResidualBlock.forward with grouped / dense 3^3 convs (use_depthwise_separable=False,
+        unet3d.py:43-60,77-93): conv1 -> IN1 (record finalized from the conv's statistics
+        partials) -> conv2 with IN1 + LeakyReLU + Dropout3d applied on its input load -> the
+        same fused block tail as the depthwise-separable path."""
+        N = x.t.shape[0]
+        d, h, w = dims
+        S = d * h * w
+        cin, cout = x.C, out.C
+        e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
+        nsb = nat.query("l3u_pw_stat_nsb", cin, cout, S)
+        nbg = nat.query("l3u_gconv3_nblocks", S)
+        recs = e(3, N * cout, 8)
+        rec_r, rec1, rec2 = (recs[0].data_ptr(), recs[1].data_ptr(), recs[2].data_ptr())
+        sv = {"x": x, "out": out, "recs": recs}
+        shortcut = self._has(pre + "shortcut.0.weight")
+        src_r = None
+        if shortcut:
+            r = e(N, cout, S)
+            so = self.fwd_arena.alloc(N * cout * nsb * 3)
+            self._call("l3u_pw_fwd", x.p, x.ns, self._w(flat, pre + "shortcut.0.weight"), 0, None,
+                       r.data_ptr(), cout * S, 0, self.fwd_arena.ptr(so), N, cin, cout, S, st)
+            src_r = self._src(flat, pre + "shortcut.1.", so, nsb, rec_r, 0.0, cptr, 0)
+            rv = V(r, 0, cout * S, cout)
+            sv["r"] = rv
+        else:
+            rv = x
+            sv["r"] = None
+        _, w1, g1 = self._conv_w(flat, pre, 1)
+        _, w2, g2 = self._conv_w(flat, pre, 2)
+        y1 = e(N, cout, S)
+        s1 = self.fwd_arena.alloc(N * cout * nbg * 3)
+        self._call("l3u_gconv3_fwd", x.p, x.ns, w1, None, y1.data_ptr(), cout * S,
+                   self.fwd_arena.ptr(s1), N, cin, cout, g1, d, h, w, st)
+        self._call("l3u_in_finalize", self.fwd_arena.ptr(s1), nbg, self._w(flat, pre + "norm1.weight"),
+                   self._w(flat, pre + "norm1.bias"), float(drop), self.seed, cptr, 1 + layer, rec1,
+                   N, cout, st)
+        y2 = e(N, cout, S)
+        s2 = self.fwd_arena.alloc(N * cout * nbg * 3)
+        self._call("l3u_gconv3_fwd", y1.data_ptr(), cout * S, w2, rec1, y2.data_ptr(), cout * S,
+                   self.fwd_arena.ptr(s2), N, cout, cout, g2, d, h, w, st)
+        src2 = self._src(flat, pre + "norm2.", s2, nbg, rec2, 0.0, cptr, 0)
+        if pool is None:
+            self._call("l3u_norm_act_fwd", y2.data_ptr(), cout * S, None, nat.norm_src_ptr(src2),
+                       rv.p, rv.ns, None, nat.norm_src_ptr(src_r), 1 if shortcut else 0, out.p,
+                       out.ns, N, cout, S, st)
+        else:
+            pooled, idx = pool
+            self._call("l3u_norm_act_pool_fwd", y2.data_ptr(), cout * S, None,
+                       nat.norm_src_ptr(src2), rv.p, rv.ns, None, nat.norm_src_ptr(src_r),
+                       1 if shortcut else 0, out.p, out.ns, pooled.data_ptr(), cout * (S // 8),
+                       idx.data_ptr(), N, cout, d, h, w, st)
+        sv.update(y1=y1, y2=y2, dims=dims, shortcut=shortcut)
         return sv
 
     # ------------------------------------------------------------------ backward
@@ -441,9 +534,91 @@ class UNetEngine:
                         st, dev)
         return dx if need_dx else None
 
+    def _tail_bwd(self, pre, sv, dout, dxv, N, cout, S, st, dev):
+        """Backward of the block tail out = lrelu(IN2(y2) + residual): d y2 and d residual (the
+        shortcut-conv output, or dxv itself for the identity shortcut), with the norm2 / shortcut
+        IN parameter-gradient reductions recorded."""
+        A = self.bwd_arena
+        out, recs = sv["out"], sv["recs"]
+        rec_r, rec2 = recs[0].data_ptr(), recs[2].data_ptr()
+        shortcut = sv["shortcut"]
+        rv = sv["r"] if shortcut else sv["x"]
+        y2 = sv["y2"]
+        nb = nat.query("l3u_norm_act_nblocks", S)
+        pn = A.alloc(2 * cout * N * nb * 3)            # fp64 partials
+        pnd = pn // 2
+        self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(), cout * S,
+                   rec2, rv.p, rv.ns, rec_r if shortcut else None, A.ptr(pn), N, cout, S, st)
+        self._seg(pnd + 1, N * nb, 3, N * nb * 3, cout, pre + "norm2.weight", f64=1)
+        self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "norm2.bias", f64=1)
+        dy2 = self._empty(N, cout, S, device=dev)
+        if shortcut:
+            dr = self._empty(N, cout, S, device=dev)
+            drv = V(dr, 0, cout * S, cout)
+            self._seg(pnd + 2, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.weight", f64=1)
+            self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.bias", f64=1)
+        else:
+            drv = dxv   # identity shortcut: d(input) starts as g
+        self._call("l3u_norm_act_bwd_apply", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(), cout * S,
+                   rec2, rv.p, rv.ns, rec_r if shortcut else None, A.ptr(pn), dy2.data_ptr(),
+                   cout * S, drv.p, drv.ns, N, cout, S, st)
+        return dy2, drv
+
+    def _block_bwd_g(self, flat, pre, sv, dout, dxv, st, dev):
+        """Backward of the grouped / dense ResidualBlock (_block_fwd_g)."""
+        A = self.bwd_arena
+        x, recs = sv["x"], sv["recs"]
+        if self.debug is not None and not self._dry:
+            self.debug[pre] = dout
+        d, h, w = sv["dims"]
+        S = d * h * w
+        N = x.t.shape[0]
+        cin, cout = x.C, sv["out"].C
+        rec1 = recs[1].data_ptr()
+        shortcut = sv["shortcut"]
+        y1 = sv["y1"]
+        dy2, drv = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev)
+        n1, w1, g1 = self._conv_w(flat, pre, 1)
+        n2, w2, g2 = self._conv_w(flat, pre, 2)
+        nbg = nat.query("l3u_gconv3_nblocks", S)
+        P = nat.query("l3u_gconv3_wgrad_nparts", N, S)
+        # conv2: data gradient with the LeakyReLU/Dropout/IN1 backward partials, weight gradient
+        # against the IN1-transformed input (recomputed from y1)
+        pi1 = A.alloc(2 * cout * N * nbg * 2)          # fp64 partials
+        pid = pi1 // 2
+        dpre = self._empty(N, cout, S, device=dev)
+        self._call("l3u_gconv3_bwd_data", dy2.data_ptr(), cout * S, w2, rec1, y1.data_ptr(), cout * S,
+                   dpre.data_ptr(), cout * S, 0, A.ptr(pi1), N, cout, cout, g2, d, h, w, st)
+        pw2 = A.alloc(P * cout * (cout // g2) * 27)
+        self._call("l3u_gconv3_bwd_weight", dy2.data_ptr(), cout * S, y1.data_ptr(), cout * S, rec1,
+                   A.ptr(pw2), N, cout, cout, g2, d, h, w, st)
+        n2w = cout * (cout // g2) * 27
+        self._seg(pw2, P, n2w, 1, n2w, n2)
+        self._seg(pid + 1, N * nbg, 2, N * nbg * 2, cout, pre + "norm1.weight", f64=1)
+        self._seg(pid + 0, N * nbg, 2, N * nbg * 2, cout, pre + "norm1.bias", f64=1)
+        # IN1 backward: dy1 = IN-backward(dpre) in place
+        self._call("l3u_in_bwd_apply", dpre.data_ptr(), cout * S, y1.data_ptr(), cout * S, rec1,
+                   A.ptr(pi1), nbg, dpre.data_ptr(), cout * S, N, cout, S, st)
+        dy1 = dpre
+        # conv1: d(input) (overwrite for the Conv1x1 shortcut, accumulate onto the identity
+        # shortcut's gradient) and the weight gradient
+        self._call("l3u_gconv3_bwd_data", dy1.data_ptr(), cout * S, w1, None, None, 0, dxv.p, dxv.ns,
+                   0 if shortcut else 1, None, N, cin, cout, g1, d, h, w, st)
+        pw1 = A.alloc(P * cout * (cin // g1) * 27)
+        self._call("l3u_gconv3_bwd_weight", dy1.data_ptr(), cout * S, x.p, x.ns, None, A.ptr(pw1),
+                   N, cin, cout, g1, d, h, w, st)
+        n1w = cout * (cin // g1) * 27
+        self._seg(pw1, P, n1w, 1, n1w, n1)
+        if shortcut:
+            self._pw_bwd(flat, drv, None, x, pre + "shortcut.0.weight", dxv, 1, N, S, st)
+        if self.debug is not None and not self._dry:
+            self.debug[pre + "#"] = {"dy2": dy2, "dr": drv, "dy1": dy1, "dx": dxv}
+
     def _block_bwd(self, flat, pre, sv, dout, dxv, st, dev):
         """Backward of ResidualBlock.forward (unet3d.py:77-93).  Writes d(block input) into dxv
         (overwrite) and records the block's weight-gradient reductions."""
+        if self.kinds[pre][0][0] != "ds":
+            return self._block_bwd_g(flat, pre, sv, dout, dxv, st, dev)
         A = self.bwd_arena
         x, out, recs = sv["x"], sv["out"], sv["recs"]
         if self.debug is not None and not self._dry:

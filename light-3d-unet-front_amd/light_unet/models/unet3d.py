@@ -11,9 +11,9 @@ parameter containers only (their own forward is never called on this path).  All
 views into ONE flat fp32 buffer (`flat_parameters()`), which is what the kernels, the fused
 AdamW and the single-bucket RCCL all-reduce operate on.
 
-Not on the MI355X path (raise NotImplementedError): use_depthwise_separable=False (dense /
-grouped 3^3 conv, unet3d.py:26-34,46-49,57-60 — not used by any shipped config), and
-volumes whose D, H, W are not multiples of 8 (the pad branch of UpBlock, unet3d.py:130-138).
+use_depthwise_separable=False (GroupedConv3d / dense nn.Conv3d 3^3 convs, unet3d.py:26-34,43-60)
+runs on the csrc/gconv.hip kernels.  Not on the MI355X path (raise NotImplementedError): volumes
+whose D, H, W are not multiples of 8 (the pad branch of UpBlock, unet3d.py:130-138).
 """
 import torch
 import torch.nn as nn
@@ -38,29 +38,43 @@ class DepthwiseSeparableConv3d(nn.Module):
 
 
 class GroupedConv3d(nn.Module):
-    """unet3d.py:26-34 (dead code under every shipped config)."""
+    """unet3d.py:26-34 — grouped 3^3 conv (stride 1, padding 1, no bias); runs in the
+    csrc/gconv.hip kernels (l3u_gconv3_*)."""
 
-    def __init__(self, *a, **k):
-        raise NotImplementedError(
-            "GroupedConv3d (use_depthwise_separable=False) is not on the MI355X path yet "
-            "(SURVEY §8f rank 3)")
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=1, groups=8,
+                 bias=False):
+        super().__init__()
+        if kernel_size != 3 or stride != 1 or padding != 1 or bias:
+            raise NotImplementedError("MI355X path: grouped 3x3x3, stride 1, padding 1, no bias")
+        self.conv = nn.Conv3d(in_channels, out_channels, kernel_size=kernel_size,
+                              stride=stride, padding=padding, groups=groups, bias=bias)
+
+    def forward(self, x):
+        raise RuntimeError("submodules are parameter containers; call Lightweight3DUNet")
 
 
 class ResidualBlock(nn.Module):
     """unet3d.py:37-93 — same submodule names (conv1, norm1, relu1, conv2, norm2, relu2, dropout,
-    shortcut) so parameter names match."""
+    shortcut) so parameter names match.  conv1 / conv2 are chosen exactly as the reference does
+    (:43-60): depthwise-separable, GroupedConv3d, or a dense nn.Conv3d."""
 
     def __init__(self, in_channels, out_channels, use_depthwise_separable=True,
                  use_grouped=True, groups=8, dropout_p=0.1):
         super().__init__()
-        if not use_depthwise_separable:
-            raise NotImplementedError(
-                "use_depthwise_separable=False (dense/grouped 3^3 conv) is not on the MI355X path "
-                "yet; every shipped config uses depthwise-separable convs (SURVEY §0.2)")
-        self.conv1 = DepthwiseSeparableConv3d(in_channels, out_channels, kernel_size=3, padding=1)
+        if use_depthwise_separable:
+            self.conv1 = DepthwiseSeparableConv3d(in_channels, out_channels, kernel_size=3, padding=1)
+        elif use_grouped and groups > 1 and in_channels >= groups and out_channels >= groups:
+            self.conv1 = GroupedConv3d(in_channels, out_channels, kernel_size=3, padding=1, groups=groups)
+        else:
+            self.conv1 = nn.Conv3d(in_channels, out_channels, kernel_size=3, padding=1, bias=False)
         self.norm1 = nn.InstanceNorm3d(out_channels, affine=True)
         self.relu1 = nn.LeakyReLU(0.01, inplace=True)
-        self.conv2 = DepthwiseSeparableConv3d(out_channels, out_channels, kernel_size=3, padding=1)
+        if use_depthwise_separable:
+            self.conv2 = DepthwiseSeparableConv3d(out_channels, out_channels, kernel_size=3, padding=1)
+        elif use_grouped and groups > 1 and out_channels >= groups:
+            self.conv2 = GroupedConv3d(out_channels, out_channels, kernel_size=3, padding=1, groups=groups)
+        else:
+            self.conv2 = nn.Conv3d(out_channels, out_channels, kernel_size=3, padding=1, bias=False)
         self.norm2 = nn.InstanceNorm3d(out_channels, affine=True)
         self.relu2 = nn.LeakyReLU(0.01, inplace=True)
         self.dropout = nn.Dropout3d(dropout_p) if dropout_p > 0 else None
@@ -155,7 +169,9 @@ class Lightweight3DUNet(nn.Module):
         self.out_conv = nn.Conv3d(encoder_channels[0], out_channels, kernel_size=1)
         self.sigmoid = nn.Sigmoid()
 
-        self.engine = _engine.UNetEngine(encoder_channels, in_channels, out_channels)
+        self.engine = _engine.UNetEngine(encoder_channels, in_channels, out_channels,
+                                         use_depthwise_separable=use_depthwise_separable,
+                                         use_grouped=use_grouped, groups=groups)
         names = [n for n, _ in self.named_parameters()]
         if names != [n for n, _ in self.engine.layout]:
             raise AssertionError("parameter registration order diverged from the engine layout")

@@ -3,6 +3,7 @@
 Written from the reference's documented behaviour, as plain aten calls on a flat state_dict:
 
   depthwise 3^3 conv      unet3d.py:16-17   conv3d(groups=C, padding=1, no bias)
+  grouped / dense 3^3     unet3d.py:26-34,43-60  conv3d(groups=G or 1, padding=1, no bias)
   pointwise 1^3 conv      unet3d.py:18      conv3d 1x1x1, no bias
   InstanceNorm3d(affine)  unet3d.py:51,62,72  per-(n,c) biased var, eps=1e-5, no running stats
   LeakyReLU(0.01)         unet3d.py:52,63
@@ -26,22 +27,32 @@ def _in(x, w, b):
     return F.instance_norm(x, weight=w, bias=b, eps=EPS)
 
 
+def conv3(sd, pre, x):
+    """ResidualBlock.conv1 / conv2 (unet3d.py:43-60), told apart by the parameter names:
+    DepthwiseSeparableConv3d (:12-23: depthwise groups=C then pointwise 1x1), GroupedConv3d
+    (:26-34: conv3d groups=G, G = Cin / weight.shape[1]) or a dense nn.Conv3d (:49, :60)."""
+    cin = x.shape[1]
+    if pre + "depthwise.weight" in sd:
+        h = F.conv3d(x, sd[pre + "depthwise.weight"], padding=1, groups=cin)
+        return F.conv3d(h, sd[pre + "pointwise.weight"])
+    if pre + "conv.weight" in sd:
+        w = sd[pre + "conv.weight"]
+        return F.conv3d(x, w, padding=1, groups=cin // w.shape[1])
+    return F.conv3d(x, sd[pre + "weight"], padding=1)
+
+
 def residual_block(sd, pre, x, drop_mask=None, drop_p=0.0):
     """unet3d.py:77-93.  `pre` is the state_dict prefix (e.g. 'down1.res_block.')."""
-    cin = x.shape[1]
     if pre + "shortcut.0.weight" in sd:
         r = F.conv3d(x, sd[pre + "shortcut.0.weight"])
         r = _in(r, sd[pre + "shortcut.1.weight"], sd[pre + "shortcut.1.bias"])
     else:
         r = x
-    h = F.conv3d(x, sd[pre + "conv1.depthwise.weight"], padding=1, groups=cin)
-    h = F.conv3d(h, sd[pre + "conv1.pointwise.weight"])
+    h = conv3(sd, pre + "conv1.", x)
     h = F.leaky_relu(_in(h, sd[pre + "norm1.weight"], sd[pre + "norm1.bias"]), SLOPE)
     if drop_mask is not None:
         h = h * drop_mask[:, :, None, None, None] / (1.0 - drop_p)
-    cout = h.shape[1]
-    h = F.conv3d(h, sd[pre + "conv2.depthwise.weight"], padding=1, groups=cout)
-    h = F.conv3d(h, sd[pre + "conv2.pointwise.weight"])
+    h = conv3(sd, pre + "conv2.", h)
     h = _in(h, sd[pre + "norm2.weight"], sd[pre + "norm2.bias"])
     return F.leaky_relu(h + r, SLOPE)
 
@@ -108,17 +119,26 @@ def ftl_grad_closed_form(pred, target, alpha=0.7, beta=0.3, gamma=0.75, smooth=1
     return g.reshape(pred.shape)
 
 
-def param_names(enc=(16, 32, 64, 128)):
-    """Parameter names/shapes in reference registration order (unet3d.py:146-202)."""
+def param_names(enc=(16, 32, 64, 128), use_depthwise_separable=True, use_grouped=True, groups=8):
+    """Parameter names/shapes in reference registration order (unet3d.py:146-202); the conv
+    kinds of each block follow unet3d.py:43-60 (the first block never groups, :163-167)."""
     out = []
 
-    def rb(pre, cin, cout):
-        out.append((pre + "conv1.depthwise.weight", (cin, 1, 3, 3, 3)))
-        out.append((pre + "conv1.pointwise.weight", (cout, cin, 1, 1, 1)))
+    def conv(pre, cin, cout, grouped_ok):
+        if use_depthwise_separable:
+            out.append((pre + "depthwise.weight", (cin, 1, 3, 3, 3)))
+            out.append((pre + "pointwise.weight", (cout, cin, 1, 1, 1)))
+        elif grouped_ok:
+            out.append((pre + "conv.weight", (cout, cin // groups, 3, 3, 3)))
+        else:
+            out.append((pre + "weight", (cout, cin, 3, 3, 3)))
+
+    def rb(pre, cin, cout, grouped=True):
+        g = use_grouped and grouped and groups > 1
+        conv(pre + "conv1.", cin, cout, g and cin >= groups and cout >= groups)
         out.append((pre + "norm1.weight", (cout,)))
         out.append((pre + "norm1.bias", (cout,)))
-        out.append((pre + "conv2.depthwise.weight", (cout, 1, 3, 3, 3)))
-        out.append((pre + "conv2.pointwise.weight", (cout, cout, 1, 1, 1)))
+        conv(pre + "conv2.", cout, cout, g and cout >= groups)
         out.append((pre + "norm2.weight", (cout,)))
         out.append((pre + "norm2.bias", (cout,)))
         if cin != cout:
@@ -127,7 +147,7 @@ def param_names(enc=(16, 32, 64, 128)):
             out.append((pre + "shortcut.1.bias", (cout,)))
 
     c0, c1, c2, c3 = enc
-    rb("init_conv.", 1, c0)
+    rb("init_conv.", 1, c0, grouped=False)
     rb("down1.res_block.", c0, c1)
     rb("down2.res_block.", c1, c2)
     rb("down3.res_block.", c2, c3)

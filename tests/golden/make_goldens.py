@@ -60,11 +60,12 @@ def grads_to_np(model):
             for k, p in model.named_parameters()}
 
 
-def model_golden(fname, enc, shape, seed, fp64=True, full=True):
+def model_golden(fname, enc, shape, seed, fp64=True, full=True, **variant):
     """Whole Lightweight3DUNet forward + FocalTversky + backward (dropout_p=0: Dropout3d RNG
-    cannot be bit-matched).  Inputs: x ~ U[0,1), target = U[0,1) > 0.97."""
+    cannot be bit-matched).  Inputs: x ~ U[0,1), target = U[0,1) > 0.97.
+    variant: use_depthwise_separable / use_grouped / groups constructor keywords."""
     torch.manual_seed(42)                                  # trainer.py:44 seed
-    model = unet3d.Lightweight3DUNet(encoder_channels=list(enc), dropout_p=0.0)
+    model = unet3d.Lightweight3DUNet(encoder_channels=list(enc), dropout_p=0.0, **variant)
     perturb_affine(model, seed + 1000)
     weights = sd_to_np(model)
     rng = np.random.default_rng(seed)
@@ -82,6 +83,8 @@ def model_golden(fname, enc, shape, seed, fp64=True, full=True):
     rec = dict(weights)
     rec.update(x=x, target=t, loss=np.array(loss.item()), seed=np.array(seed),
                enc=np.array(enc), n_params=np.array(model.count_parameters()["total"]))
+    for k, v in variant.items():
+        rec["variant/" + k] = np.array(v)
     o = out.detach().numpy().astype(np.float32)
     if full:
         rec["out"] = o
@@ -100,17 +103,33 @@ def model_golden(fname, enc, shape, seed, fp64=True, full=True):
     print(fname, "loss", loss.item(), "params", rec["n_params"])
 
 
-def block_goldens():
+BLOCK_CASES = [
+    ("rb_a", lambda: unet3d.ResidualBlock(3, 8, dropout_p=0.0), [(2, 3, 7, 6, 9)]),
+    ("rb_id", lambda: unet3d.ResidualBlock(8, 8, dropout_p=0.0), [(2, 8, 5, 7, 6)]),
+    ("rb_c1", lambda: unet3d.ResidualBlock(1, 4, use_grouped=False, dropout_p=0.0), [(1, 1, 9, 8, 10)]),
+    ("down", lambda: unet3d.DownBlock(4, 8, dropout_p=0.0), [(2, 4, 10, 8, 12)]),
+    ("up", lambda: unet3d.UpBlock(8, 4, dropout_p=0.0), [(2, 8, 3, 4, 5), (2, 4, 6, 8, 10)]),
+]
+# use_depthwise_separable=False: GroupedConv3d (unet3d.py:26-34) and dense nn.Conv3d (:49, :60)
+BLOCK_CASES_G = [
+    ("g_rb", lambda: unet3d.ResidualBlock(8, 16, use_depthwise_separable=False, dropout_p=0.0),
+     [(2, 8, 6, 7, 5)]),
+    ("g_rb_id", lambda: unet3d.ResidualBlock(16, 16, use_depthwise_separable=False, groups=4,
+                                             dropout_p=0.0), [(2, 16, 5, 6, 7)]),
+    ("g_rb_mixed", lambda: unet3d.ResidualBlock(4, 8, use_depthwise_separable=False, groups=8,
+                                                dropout_p=0.0), [(1, 4, 6, 5, 8)]),
+    ("d_rb", lambda: unet3d.ResidualBlock(3, 6, use_depthwise_separable=False, use_grouped=False,
+                                          dropout_p=0.0), [(2, 3, 5, 6, 7)]),
+    ("g_up", lambda: unet3d.UpBlock(16, 8, use_depthwise_separable=False, dropout_p=0.0),
+     [(2, 16, 3, 4, 2), (2, 8, 6, 8, 4)]),
+]
+
+
+def block_goldens(cases=None, fname="blocks.npz"):
     """Per-block KATs at small ragged shapes: ResidualBlock (Cin!=Cout and identity shortcut),
     DownBlock, UpBlock (unet3d.py:37-143), fp64, dropout 0, with a random upstream gradient."""
     rec = {}
-    cases = [
-        ("rb_a", lambda: unet3d.ResidualBlock(3, 8, dropout_p=0.0), [(2, 3, 7, 6, 9)]),
-        ("rb_id", lambda: unet3d.ResidualBlock(8, 8, dropout_p=0.0), [(2, 8, 5, 7, 6)]),
-        ("rb_c1", lambda: unet3d.ResidualBlock(1, 4, use_grouped=False, dropout_p=0.0), [(1, 1, 9, 8, 10)]),
-        ("down", lambda: unet3d.DownBlock(4, 8, dropout_p=0.0), [(2, 4, 10, 8, 12)]),
-        ("up", lambda: unet3d.UpBlock(8, 4, dropout_p=0.0), [(2, 8, 3, 4, 5), (2, 4, 6, 8, 10)]),
-    ]
+    cases = BLOCK_CASES if cases is None else cases
     for i, (name, ctor, shapes) in enumerate(cases):
         torch.manual_seed(100 + i)
         blk = ctor()
@@ -148,8 +167,8 @@ def block_goldens():
             rec[f"{name}/din{j}"] = tt.grad.numpy().astype(np.float32)
         for k, p in blk.named_parameters():
             rec[f"{name}/g/{k}"] = p.grad.numpy().astype(np.float32)
-    np.savez_compressed(os.path.join(OUT, "blocks.npz"), **rec)
-    print("blocks.npz", len(rec), "arrays")
+    np.savez_compressed(os.path.join(OUT, fname), **rec)
+    print(fname, len(rec), "arrays")
 
 
 def ftl_goldens():
@@ -215,8 +234,21 @@ def sliding_goldens():
     print("sliding.npz", len(rec))
 
 
+def variant_goldens():
+    """The use_depthwise_separable=False network family (grouped and dense 3^3 convs)."""
+    block_goldens(BLOCK_CASES_G, "blocks_g.npz")
+    model_golden("model_g_b2_16.npz", (8, 16, 32, 64), (2, 1, 16, 16, 16), seed=45,
+                 use_depthwise_separable=False, use_grouped=True, groups=8)
+    model_golden("model_d_b1_16.npz", (4, 8, 16, 32), (1, 1, 16, 16, 16), seed=46,
+                 use_depthwise_separable=False, use_grouped=False, groups=8)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
+    if sys.argv[1:] == ["variants"]:
+        variant_goldens()
+        sys.exit(0)
+    variant_goldens()
     block_goldens()
     ftl_goldens()
     model_golden("model_b2_32.npz", (16, 32, 64, 128), (2, 1, 32, 32, 32), seed=42)

@@ -62,7 +62,7 @@ def test_forward_on_cpu_fails_loudly():
 def test_unsupported_configs_raise():
     from light_unet.models.unet3d import Lightweight3DUNet
     with pytest.raises(NotImplementedError):
-        Lightweight3DUNet(use_depthwise_separable=False)
+        Lightweight3DUNet(in_channels=2)
 
 
 def test_loss_factory_and_errors():
@@ -110,3 +110,36 @@ def test_sliding_window_host_pieces(golden):
     with pytest.raises(_native.NativeError):
         sliding_window_inference_3d(np.zeros((48, 48, 48), np.float32), Lightweight3DUNet(),
                                     device=torch.device("cpu"))
+
+
+@pytest.mark.parametrize("fname,kw", [
+    ("model_g_b2_16.npz", dict(use_depthwise_separable=False, use_grouped=True, groups=8)),
+    ("model_d_b1_16.npz", dict(use_depthwise_separable=False, use_grouped=False, groups=8))])
+def test_variant_param_names_and_seed42_init(golden, fname, kw):
+    """use_depthwise_separable=False: GroupedConv3d / dense nn.Conv3d blocks (unet3d.py:26-34,
+    43-60) with the reference's keys, shapes, count and seed-42 initial weights."""
+    from light_unet.models.unet3d import Lightweight3DUNet
+    z = golden(fname)
+    enc = [int(c) for c in z["enc"]]
+    torch.manual_seed(42)
+    m = Lightweight3DUNet(encoder_channels=enc, dropout_p=0.0, **kw)
+    keys = [k[2:] for k in z.files if k.startswith("w/")]
+    sd = m.state_dict()
+    assert list(sd) == keys
+    assert m.count_parameters()["total"] == int(z["n_params"])
+    for k, v in sd.items():
+        assert tuple(v.shape) == z["w/" + k].shape
+        if ".norm" in k or ".shortcut.1." in k:
+            continue
+        assert np.array_equal(v.numpy(), z["w/" + k]), k
+    full = Lightweight3DUNet(use_depthwise_separable=False)
+    assert full.count_parameters()["total"] == 391521          # reference, groups=8
+    dense = Lightweight3DUNet(use_depthwise_separable=False, use_grouped=False)
+    assert dense.count_parameters()["total"] == 2308737
+
+
+def test_variant_group_divisibility_error():
+    """nn.Conv3d raises for channels not divisible by groups; so does the mirror."""
+    from light_unet.models.unet3d import Lightweight3DUNet
+    with pytest.raises(ValueError):
+        Lightweight3DUNet(encoder_channels=[12, 20, 40, 80], use_depthwise_separable=False, groups=8)

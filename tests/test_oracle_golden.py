@@ -64,6 +64,51 @@ def test_oracle_blocks_match_reference(golden):
             assert np.abs(t.grad.numpy() - ref).max() <= 1e-5 * np.abs(ref).max(), (name, j)
 
 
+VARIANTS = {"model_g_b2_16.npz": dict(use_depthwise_separable=False, use_grouped=True, groups=8),
+            "model_d_b1_16.npz": dict(use_depthwise_separable=False, use_grouped=False, groups=8)}
+
+
+@pytest.mark.parametrize("fname", sorted(VARIANTS))
+def test_oracle_variant_models_match_reference(golden, fname):
+    """use_depthwise_separable=False (GroupedConv3d / dense nn.Conv3d, unet3d.py:26-34,43-60)."""
+    z = golden(fname)
+    var = VARIANTS[fname]
+    for k, v in var.items():
+        assert z["variant/" + k].item() == v
+    enc = tuple(int(c) for c in z["enc"])
+    sd = _sd(z)
+    names = U.param_names(enc, **var)
+    assert [k for k in sd] == [n for n, _ in names]
+    for n, shape in names:
+        assert tuple(sd[n].shape) == shape
+    assert sum(v.numel() for v in sd.values()) == int(z["n_params"])
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    out = U.unet_forward(params, torch.from_numpy(z["x"]).double())
+    loss = U.focal_tversky(out, torch.from_numpy(z["target"]).double())
+    loss.backward()
+    assert np.abs(out.detach().numpy() - z["out"]).max() < 1e-6
+    assert abs(loss.item() - float(z["loss"])) < 1e-9
+    for k, p in params.items():
+        g = z["g/" + k]
+        assert np.abs(p.grad.numpy() - g).max() <= 1e-5 * max(np.abs(g).max(), 1e-12) + 1e-12, k
+
+
+def test_oracle_variant_blocks_match_reference(golden):
+    z = golden("blocks_g.npz")
+    cases = {"g_rb": "rb", "g_rb_id": "rb", "g_rb_mixed": "rb", "d_rb": "rb", "g_up": "up"}
+    for name, kind in cases.items():
+        sd = {k[len(name) + 3:]: torch.from_numpy(z[k]).double() for k in z.files
+              if k.startswith(name + "/w/")}
+        ins = [torch.from_numpy(z[f"{name}/in{j}"]).double().requires_grad_(True)
+               for j in range(2 if kind == "up" else 1)]
+        out = U.residual_block(sd, "", ins[0]) if kind == "rb" else U.up_block(sd, "", ins[0], ins[1])
+        out.backward(torch.from_numpy(z[f"{name}/dy"]).double())
+        assert np.abs(out.detach().numpy() - z[f"{name}/out"]).max() < 1e-5, name
+        for j, t in enumerate(ins):
+            ref = z[f"{name}/din{j}"]
+            assert np.abs(t.grad.numpy() - ref).max() <= 1e-5 * np.abs(ref).max(), (name, j)
+
+
 def test_oracle_ftl_and_closed_form(golden):
     z = golden("ftl.npz")
     for case in ("rand", "empty", "full", "sat", "params"):
