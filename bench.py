@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--ftl-mode", default="exact", choices=["exact", "local"])
     ap.add_argument("--no-sliding", action="store_true", help="skip the config-4 inference timing")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (32->256, 64^3) timing")
+    ap.add_argument("--no-grouped", action="store_true",
+                    help="skip the use_depthwise_separable=False (grouped) model timing")
     # multi-rank rehearsal on a one-GPU box: every rank on cuda:0, collectives over gloo
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--one-device", action="store_true")
@@ -264,6 +266,36 @@ def config5_bench(device, steps=20, warmup=5, bs=4, size=64, enc=(32, 64, 128, 2
             "ms_per_step": round(1000 * dt / steps, 4), "final_loss": round(lv, 6)}
 
 
+def grouped_bench(device, steps=10, warmup=3, bs=4, size=48):
+    """The use_depthwise_separable=False network family on this GPU: the
+    grouped model (GroupedConv3d groups 8; the first block dense, unet3d.py:163-167; 391,521
+    parameters) on the config-2 workload (48^3, bs 4, fp32), graph-replayed train step."""
+    from light_unet.models.unet3d import Lightweight3DUNet
+    from light_unet.train_step import TrainStep
+    torch.manual_seed(42)
+    model = Lightweight3DUNet(dropout_p=0.1, use_depthwise_separable=False).to(device).train()
+    step = TrainStep(model, {"alpha": 0.7, "beta": 0.3, "gamma": 0.75}, lr=1e-4, weight_decay=1e-5)
+    rng = np.random.default_rng(42)
+    xs = torch.from_numpy(rng.random((bs, 1, size, size, size), dtype=np.float32)).to(device)
+    ts = torch.from_numpy((rng.random((bs, 1, size, size, size)) > 0.97).astype(np.float32)).to(device)
+    step.capture(xs, ts, warmup=2)
+    for _ in range(warmup):
+        step.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step.replay()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    lv = float(loss.item())
+    if not np.isfinite(lv):
+        raise SystemExit(f"grouped model: non-finite loss {lv}")
+    return {"workload": f"Lightweight3DUNet use_depthwise_separable=False (groups 8) train step, "
+                        f"{size}^3, bs {bs}", "params": int(model.flat_parameters().numel()),
+            "patches_per_s_per_gpu": round(steps * bs / dt, 2),
+            "ms_per_step": round(1000 * dt / steps, 4), "final_loss": round(lv, 6)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -342,6 +374,7 @@ def main():
 
     sliding = sliding_bench(model, device) if (rank == 0 and not args.no_sliding) else None
     cfg5 = config5_bench(device) if (rank == 0 and not args.no_config5) else None
+    grouped = grouped_bench(device) if (rank == 0 and not args.no_grouped) else None
     fwd1 = fwd_ms_per_patch(model, 1, args.size, device) if rank == 0 else None
     fwd4 = fwd_ms_per_patch(model, args.batch, args.size, device) if rank == 0 else None
     out = None
@@ -375,6 +408,7 @@ def main():
             "final_loss": round(final_loss, 6),
             "sliding_window_256": sliding,
             "config5_1gpu": cfg5,
+            "grouped_1gpu": grouped,
             "roofline": {
                 "kernel": f"l3u_dw3_bwd [{N},{cdom},{args.size}^3] (up3.res_block.conv1.depthwise "
                           "backward: one single-pass launch, data and weight gradients from one "

@@ -3,14 +3,14 @@ dispatches of that exact launch shape (kernel name + grid size), so that it can 
 bench.py's HIP-event `roofline.avg_launch_ms`.
 
     python tools/dom_trace.py <run_kernel_trace.csv> [name-substring] [grid_x]
-default: dw3p_bwd_kernel<0, 16> with grid 3840 x 64 = [4, 32, 48^3] (3840 one-wave tiles)
+default: dw3p_bwd_kernel<0, 16, true> with grid 3840 x 64 = [4, 32, 48^3] (3840 one-wave tiles)
 """
 import csv
 import json
 import sys
 
 path = sys.argv[1]
-sub = sys.argv[2] if len(sys.argv) > 2 else "dw3p_bwd_kernel<0, 16>"
+sub = sys.argv[2] if len(sys.argv) > 2 else "dw3p_bwd_kernel<0, 16, true>"
 grid = int(sys.argv[3]) if len(sys.argv) > 3 else 3840 * 64
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
      for r in csv.DictReader(open(path))
