@@ -155,6 +155,13 @@ int l3u_norm_act_bwd_apply(const float* dout, long long dout_nstride, const floa
                            const float* rec_r, const double* part, float* dy2,
                            long long dy2_nstride, float* dr, long long dr_nstride, int N, int C,
                            int S, hipStream_t stream);
+/* reduce + apply as ONE launch when l3u_norm_act_nblocks(S) == 1 (one workgroup per plane: the
+ * small levels); same part layout (nblocks = 1) and bit-identical results                        */
+int l3u_norm_act_bwd(const float* dout, long long dout_nstride, const float* out,
+                     long long out_nstride, const float* y2, long long y2_nstride,
+                     const float* rec2, const float* r, long long r_nstride, const float* rec_r,
+                     double* part, float* dy2, long long dy2_nstride, float* dr,
+                     long long dr_nstride, int N, int C, int S, hipStream_t stream);
 /* inner InstanceNorm backward: dy = rstd*gamma*(dpre - mean(dpre) - xhat*mean(dpre*xhat))     */
 int l3u_in_bwd_apply(const float* dpre, long long dpre_nstride, const float* y, long long y_nstride,
                      const float* rec, const double* in_part, int npart, float* dy,

@@ -231,6 +231,86 @@ __global__ __launch_bounds__(256) void norm_act_bwd_apply_kernel(
   }
 }
 
+// Both phases in one launch for planes that one workgroup covers (l3u_norm_act_nblocks(S) == 1:
+// the 12^3 / 6^3 levels, where a launch costs more than the work): the three plane sums are
+// workgroup sums held by every thread, stored as the single partial, then applied.  Same values,
+// bit for bit, as the reduce + apply pair (the apply's fixed-order merge of one partial is exact).
+template <bool VEC>
+__global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
+    const float* __restrict__ dout, long long dns, const float* __restrict__ out, long long ons,
+    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
+    const float* __restrict__ r, long long rns, const float* __restrict__ recr,
+    double* __restrict__ part, float* __restrict__ dy2, long long dy2ns, float* __restrict__ dr,
+    long long drns, int N, int C, int S) {
+  __shared__ double red[4];
+  const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const float* q2 = rec2 + (long long)nc * kRec;
+  const float m2 = q2[0], rs2 = q2[1], f2 = q2[1] * q2[5];
+  float mr = 0.f, rsr = 1.f, fr = 1.f;
+  if (recr) { const float* qr = recr + (long long)nc * kRec; mr = qr[0]; rsr = qr[1]; fr = qr[1] * qr[5]; }
+  const long long co = (long long)c * S;
+  const float* dp = dout + (long long)n * dns + co;
+  const float* op = out + (long long)n * ons + co;
+  const float* yp = y2 + (long long)n * y2ns + co;
+  const float* rp = r + (long long)n * rns + co;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  if (VEC) {
+    for (int i = threadIdx.x * 4; i < S; i += 1024) {
+      const f4 dv = *reinterpret_cast<const f4*>(dp + i), ov = *reinterpret_cast<const f4*>(op + i);
+      const f4 yv = *reinterpret_cast<const f4*>(yp + i);
+      f4 rv = f4{0.f, 0.f, 0.f, 0.f};
+      if (recr) rv = *reinterpret_cast<const f4*>(rp + i);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float g = dv[q] * lrelu_d(ov[q]);
+        s0 += g;
+        s1 += (double)g * ((yv[q] - m2) * rs2);
+        if (recr) s2 += (double)g * ((rv[q] - mr) * rsr);
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < S; i += 256) {
+      const float g = dp[i] * lrelu_d(op[i]);
+      s0 += g;
+      s1 += (double)g * ((yp[i] - m2) * rs2);
+      if (recr) s2 += (double)g * ((rp[i] - mr) * rsr);
+    }
+  }
+  s0 = block_sum256d(s0, red);
+  s1 = block_sum256d(s1, red);
+  s2 = block_sum256d(s2, red);
+  if (threadIdx.x == 0) {
+    double* o = part + ((long long)c * N + n) * 3;
+    o[0] = s0; o[1] = s1; o[2] = s2;
+  }
+  const float M0 = (float)((0.0 + s0) / S), M1 = (float)((0.0 + s1) / S), M2 = (float)((0.0 + s2) / S);
+  float* d2 = dy2 + (long long)n * dy2ns + co;
+  float* drp = dr + (long long)n * drns + co;
+  if (VEC) {
+    for (int i = threadIdx.x * 4; i < S; i += 1024) {
+      const f4 dv = *reinterpret_cast<const f4*>(dp + i), ov = *reinterpret_cast<const f4*>(op + i);
+      const f4 yv = *reinterpret_cast<const f4*>(yp + i);
+      f4 rv = f4{0.f, 0.f, 0.f, 0.f};
+      if (recr) rv = *reinterpret_cast<const f4*>(rp + i);
+      f4 o2, orr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float g = dv[q] * lrelu_d(ov[q]);
+        o2[q] = f2 * (g - M0 - (yv[q] - m2) * rs2 * M1);
+        orr[q] = recr ? fr * (g - M0 - (rv[q] - mr) * rsr * M2) : g;
+      }
+      *reinterpret_cast<f4*>(d2 + i) = o2;
+      *reinterpret_cast<f4*>(drp + i) = orr;
+    }
+  } else {
+    for (int i = threadIdx.x; i < S; i += 256) {
+      const float g = dp[i] * lrelu_d(op[i]);
+      d2[i] = f2 * (g - M0 - (yp[i] - m2) * rs2 * M1);
+      drp[i] = recr ? fr * (g - M0 - (rp[i] - mr) * rsr * M2) : g;
+    }
+  }
+}
+
 // InstanceNorm backward apply for the inner norm (after dw3_bwd MODE 1 produced dpre + sums):
 // dy = rstd*gamma*(dpre - M1 - xhat*M2); in-place allowed (dy == dpre)
 template <bool VEC>
@@ -364,6 +444,21 @@ int l3u_norm_act_bwd_apply(const float* dout, long long dout_nstride, const floa
   dim3 grid(npart, N * C);
   if (vec) hipLaunchKernelGGL(norm_act_bwd_apply_kernel<true>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, npart, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
   else hipLaunchKernelGGL(norm_act_bwd_apply_kernel<false>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, npart, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_norm_act_bwd(const float* dout, long long dout_nstride, const float* out,
+                     long long out_nstride, const float* y2, long long y2_nstride,
+                     const float* rec2, const float* r, long long r_nstride, const float* rec_r,
+                     double* part, float* dy2, long long dy2_nstride, float* dr,
+                     long long dr_nstride, int N, int C, int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && S > 0 && elem_blocks(S) == 1);
+  const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
+                   y2_nstride % 4 == 0 && r_nstride % 4 == 0 && dy2_nstride % 4 == 0 &&
+                   dr_nstride % 4 == 0;
+  dim3 grid(1, N * C);
+  if (vec) hipLaunchKernelGGL(norm_act_bwd_one_kernel<true>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
+  else hipLaunchKernelGGL(norm_act_bwd_one_kernel<false>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
   L3U_CHECK_LAUNCH();
 }
 

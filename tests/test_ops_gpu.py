@@ -858,3 +858,36 @@ def test_convt_bwd_fused(cuda, case):
     close(dx.view(x.shape), xr.grad, 1e-5, f"convT dX {case}")
     close(wp.view(P, Ci, Co * 8).double().sum(0).view(w.shape), wr.grad, 1e-5, "convT dW")
     close(bp.view(P, Co).double().sum(0), br.grad, 1e-5, "convT db")
+
+
+@pytest.mark.parametrize("shape", [(4, 128, 216), (4, 64, 1728), (2, 8, 250), (1, 4, 27)])
+@pytest.mark.parametrize("shortcut", [False, True])
+def test_norm_act_bwd_one_launch_equals_pair(cuda, shape, shortcut):
+    """l3u_norm_act_bwd (one workgroup per plane) == l3u_norm_act_bwd_reduce + _apply, bitwise."""
+    N, C, S = shape
+    assert nat().query("l3u_norm_act_nblocks", S) == 1
+    gen = torch.Generator().manual_seed(41)
+    t = lambda: torch.randn(N, C, S, generator=gen).to(cuda)  # noqa: E731
+    dout, out, y2, r = t(), t(), t(), t()
+    rec2 = make_rec(N, C, gen).float().to(cuda)
+    recr = make_rec(N, C, gen).float().to(cuda) if shortcut else None
+    rp = recr.data_ptr() if shortcut else None
+
+    def run(one):
+        part = torch.full((C * N * 3,), float("nan"), dtype=torch.float64, device=cuda)
+        dy2 = torch.full((N, C, S), float("nan"), device=cuda)
+        dr = torch.full((N, C, S), float("nan"), device=cuda)
+        a = (dout.data_ptr(), C * S, out.data_ptr(), C * S, y2.data_ptr(), C * S, rec2.data_ptr(),
+             r.data_ptr(), C * S, rp)
+        if one:
+            nat().call("l3u_norm_act_bwd", *a, part.data_ptr(), dy2.data_ptr(), C * S, dr.data_ptr(),
+                       C * S, N, C, S, st())
+        else:
+            nat().call("l3u_norm_act_bwd_reduce", *a, part.data_ptr(), N, C, S, st())
+            nat().call("l3u_norm_act_bwd_apply", *a, part.data_ptr(), dy2.data_ptr(), C * S,
+                       dr.data_ptr(), C * S, N, C, S, st())
+        torch.cuda.synchronize()
+        return part, dy2, dr
+
+    for a, b in zip(run(True), run(False)):
+        assert torch.equal(a, b)
