@@ -22,8 +22,12 @@ using namespace l3u;
 
 namespace {
 
+typedef float f4 __attribute__((ext_vector_type(4)));
+
 constexpr int kGB = 256;      // output voxels per workgroup (one per thread)
 constexpr int kWVPT = 8;      // voxels per thread of the weight-gradient kernel
+constexpr int kKC = 16;       // input channels per LDS weight stage of the stencil kernel
+constexpr int kWCO = 4;       // output channels per workgroup of the weight-gradient kernel
 
 // Y[n][g*JG + j][v] = sum_{k < KG} sum_t Wt(g, j, k, t) * A[n][g*KG + k][v + off(t)]
 //   FLIP = false (forward):        Wt = w[((g*JG + j)*KG + k)*27 + t]       (w: [Cout][Cin/G][27])
@@ -53,30 +57,64 @@ __global__ __launch_bounds__(256) void gconv3_kernel(
 #pragma unroll
   for (int j = 0; j < CT; ++j) acc[j] = 0.f;
   const float* an = a + (long long)n * ans;
-  for (int k = 0; k < KG; ++k) {
-    const int ca = g * KG + k;
-    const float* ap = an + (long long)ca * S + vv;
-    float mu = 0.f, sc = 1.f, sh = 0.f;
-    if (XF) {
-      const float* r = rec_in + ((long long)n * G * KG + ca) * kRec;
-      mu = r[0]; sc = r[2]; sh = r[3];
+  // the workgroup's weights, KC input channels at a time, staged in LDS as [k][t][j] (zero for
+  // j >= JG): the CT weights of one (k, t) are one wave-uniform (broadcast) LDS vector read
+  __shared__ __attribute__((aligned(16))) float wl[kKC * 27 * CT];
+  for (int k0 = 0; k0 < KG; k0 += kKC) {
+    const int kn = min(kKC, KG - k0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kn * 27 * CT; i += kGB) {
+      const int kk = i / (27 * CT), rem = i - kk * 27 * CT, t = rem / CT, j = rem - t * CT;
+      const int jj = j0 + j, k = k0 + kk;
+      wl[i] = jj >= JG ? 0.f
+                       : (FLIP ? w[((long long)(g * KG + k) * JG + jj) * 27 + 26 - t]
+                               : w[((long long)(g * JG + jj) * KG + k) * 27 + t]);
     }
-#pragma unroll
-    for (int t = 0; t < 27; ++t) {
-      const int dz = t / 9, dy = (t / 3) % 3, dx = t % 3;
-      float val = 0.f;
-      if (act && okz[dz] && oky[dy] && okx[dx]) {
-        val = ap[((dz - 1) * H + (dy - 1)) * W + (dx - 1)];
-        if (XF) val = lrelu(fmaf(sc, val - mu, sh));
+    __syncthreads();
+    for (int kk = 0; kk < kn; ++kk) {
+      const int ca = g * KG + k0 + kk;
+      const float* ap = an + (long long)ca * S + vv;
+      float mu = 0.f, sc = 1.f, sh = 0.f;
+      if (XF) {
+        const float* r = rec_in + ((long long)n * G * KG + ca) * kRec;
+        mu = r[0]; sc = r[2]; sh = r[3];
       }
+      const float* wk = wl + kk * 27 * CT;
+      // the 27 neighbourhood loads first (latency), then tap by tap the CT weights from LDS;
+      // the scheduling barrier keeps the weight reads of later taps from being hoisted (they
+      // would hold 27 x CT registers)
+      float val[27];
 #pragma unroll
-      for (int j = 0; j < CT; ++j) {
-        const int jj = j0 + j;
-        if (jj < JG) {
-          const float wv = FLIP ? w[((long long)(g * KG + k) * JG + jj) * 27 + 26 - t]
-                                : w[((long long)(g * JG + jj) * KG + k) * 27 + t];
-          acc[j] = fmaf(wv, val, acc[j]);
+      for (int t = 0; t < 27; ++t) {
+        const int dz = t / 9, dy = (t / 3) % 3, dx = t % 3;
+        val[t] = 0.f;
+        if (act && okz[dz] && oky[dy] && okx[dx]) val[t] = ap[((dz - 1) * H + (dy - 1)) * W + (dx - 1)];
+      }
+      if (XF) {
+#pragma unroll
+        for (int t = 0; t < 27; ++t) {
+          const int dz = t / 9, dy = (t / 3) % 3, dx = t % 3;
+          val[t] = (act && okz[dz] && oky[dy] && okx[dx]) ? lrelu(fmaf(sc, val[t] - mu, sh)) : 0.f;
         }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 27; ++t) {
+        const float v = val[t];
+        if (CT % 4 == 0) {
+#pragma unroll
+          for (int j = 0; j < CT; j += 4) {
+            const f4 w4 = *reinterpret_cast<const f4*>(wk + t * CT + j);
+            acc[j] = fmaf(w4[0], v, acc[j]);
+            acc[j + 1] = fmaf(w4[1], v, acc[j + 1]);
+            acc[j + 2] = fmaf(w4[2], v, acc[j + 2]);
+            acc[j + 3] = fmaf(w4[3], v, acc[j + 3]);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < CT; ++j) acc[j] = fmaf(wk[t * CT + j], v, acc[j]);
+        }
+        asm volatile("" ::: "memory");   // no LDS weight read moves across taps
       }
     }
   }
@@ -122,32 +160,42 @@ __global__ __launch_bounds__(256) void gconv3_kernel(
 
 // part[(n*nbk + bx)][co][k][t] = sum over the chunk's voxels v of dY[n][co][v] * A[n][ci][v+off(t)],
 // ci = (co / JG) * KG + k; A = x (XF 0) or lrelu(scale*(x-mean)+shift) (XF 1).  One workgroup per
-// (chunk, (co, k) pair, n); a fixed-order workgroup reduction of the 27 taps (deterministic).
-template <bool XF>
+// (chunk, (tile of CO output channels of one group, k), n): each A neighbourhood load feeds CO
+// output channels; a fixed-order workgroup reduction of the CO x 27 taps (deterministic).
+template <bool XF, int CO>
 __global__ __launch_bounds__(256) void gconv3_wgrad_kernel(
     const float* __restrict__ dy, long long dyns, const float* __restrict__ a, long long ans,
     const float* __restrict__ rec, float* __restrict__ part, int G, int KG, int JG, int D, int H,
     int W) {
-  __shared__ float red[4][28];
+  __shared__ float red[4][CO * 27];
   const int S = D * H * W;
   const int nbk = gridDim.x, bx = blockIdx.x;
-  const int pair = blockIdx.y, co = pair / KG, k = pair % KG;
-  const int ci = (co / JG) * KG + k;
+  const int ntc = (JG + CO - 1) / CO;
+  const int k = blockIdx.y % KG, tile = blockIdx.y / KG;
+  const int g = tile / ntc, c0 = (tile % ntc) * CO;   // output channels g*JG + c0 .. (< JG)
+  const int ci = g * KG + k;
   const int n = blockIdx.z;
-  const float* dyp = dy + (long long)n * dyns + (long long)co * S;
   const float* ap0 = a + (long long)n * ans + (long long)ci * S;
+  const float* dyp[CO];
+#pragma unroll
+  for (int j = 0; j < CO; ++j)
+    dyp[j] = dy + (long long)n * dyns + (long long)(g * JG + min(c0 + j, JG - 1)) * S;
   float mu = 0.f, sc = 1.f, sh = 0.f;
   if (XF) {
     const float* r = rec + ((long long)n * G * KG + ci) * kRec;
     mu = r[0]; sc = r[2]; sh = r[3];
   }
-  float acc[27];
+  float acc[CO][27];
 #pragma unroll
-  for (int t = 0; t < 27; ++t) acc[t] = 0.f;
+  for (int j = 0; j < CO; ++j)
+#pragma unroll
+    for (int t = 0; t < 27; ++t) acc[j][t] = 0.f;
   for (int i = 0; i < kWVPT; ++i) {
     const int v = (bx * kWVPT + i) * kGB + threadIdx.x;
     if (v >= S) break;
-    const float gv = dyp[v];
+    float gv[CO];
+#pragma unroll
+    for (int j = 0; j < CO; ++j) gv[j] = dyp[j][v];
     const int xx = v % W, t1 = v / W, yy = t1 % H, zz = t1 / H;
     const bool okz[3] = {zz > 0, true, zz < D - 1};
     const bool oky[3] = {yy > 0, true, yy < H - 1};
@@ -156,25 +204,31 @@ __global__ __launch_bounds__(256) void gconv3_wgrad_kernel(
 #pragma unroll
     for (int t = 0; t < 27; ++t) {
       const int dz = t / 9, dyy = (t / 3) % 3, dx = t % 3;
+      float val = 0.f;
       if (okz[dz] && oky[dyy] && okx[dx]) {
-        float val = ap[((dz - 1) * H + (dyy - 1)) * W + (dx - 1)];
+        val = ap[((dz - 1) * H + (dyy - 1)) * W + (dx - 1)];
         if (XF) val = lrelu(fmaf(sc, val - mu, sh));
-        acc[t] = fmaf(gv, val, acc[t]);
       }
+#pragma unroll
+      for (int j = 0; j < CO; ++j) acc[j][t] = fmaf(gv[j], val, acc[j][t]);
     }
   }
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
 #pragma unroll
-  for (int t = 0; t < 27; ++t) {
-    const float r = wave_sum(acc[t]);
-    if (ln == 0) red[wv][t] = r;
-  }
+  for (int j = 0; j < CO; ++j)
+#pragma unroll
+    for (int t = 0; t < 27; ++t) {
+      const float r = wave_sum(acc[j][t]);
+      if (ln == 0) red[wv][j * 27 + t] = r;
+    }
   __syncthreads();
-  if (threadIdx.x < 27) {
-    const float r = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) +
-                    red[3][threadIdx.x];
-    const long long npair = (long long)G * JG * KG;
-    part[(((long long)n * nbk + bx) * npair + pair) * 27 + threadIdx.x] = r;
+  const long long npair = (long long)G * JG * KG;
+  for (int e = threadIdx.x; e < CO * 27; e += kGB) {
+    const int j = e / 27, t = e - j * 27;
+    if (c0 + j >= JG) continue;
+    const float r = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    const long long pair = (long long)(g * JG + c0 + j) * KG + k;
+    part[(((long long)n * nbk + bx) * npair + pair) * 27 + t] = r;
   }
 }
 
@@ -241,11 +295,16 @@ int l3u_gconv3_bwd_weight(const float* dy, long long dy_nstride, const float* x,
                           int Cout, int G, int D, int H, int W, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && G > 0 && D > 0 && H > 0 && W > 0);
   L3U_REQUIRE(Cin % G == 0 && Cout % G == 0);
-  L3U_REQUIRE((long long)D * H * W < (1ll << 31) && Cout * (Cin / G) <= 65535);
   const int S = D * H * W, KG = Cin / G, JG = Cout / G;
-  dim3 grid(l3u_gconv3_wgrad_nparts(1, S), Cout * KG, N), block(kGB);
-  if (rec) hipLaunchKernelGGL((gconv3_wgrad_kernel<true>), grid, block, 0, stream, dy, dy_nstride, x, x_nstride, rec, part, G, KG, JG, D, H, W);
-  else hipLaunchKernelGGL((gconv3_wgrad_kernel<false>), grid, block, 0, stream, dy, dy_nstride, x, x_nstride, rec, part, G, KG, JG, D, H, W);
+  const int co = JG >= kWCO ? kWCO : (JG >= 2 ? 2 : 1);
+  const long long ny = (long long)G * ((JG + co - 1) / co) * KG;
+  L3U_REQUIRE((long long)D * H * W < (1ll << 31) && ny <= 65535);
+  dim3 grid(l3u_gconv3_wgrad_nparts(1, S), (unsigned)ny, N), block(kGB);
+#define GW(X_, C_) hipLaunchKernelGGL((gconv3_wgrad_kernel<X_, C_>), grid, block, 0, stream, dy, \
+      dy_nstride, x, x_nstride, rec, part, G, KG, JG, D, H, W)
+  if (rec) { if (co == kWCO) GW(true, kWCO); else if (co == 2) GW(true, 2); else GW(true, 1); }
+  else { if (co == kWCO) GW(false, kWCO); else if (co == 2) GW(false, 2); else GW(false, 1); }
+#undef GW
   L3U_CHECK_LAUNCH();
 }
 
