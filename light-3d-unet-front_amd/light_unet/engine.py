@@ -15,12 +15,16 @@ layout is fixed by a dry run on first use; one l3u_reduce_segments launch at the
 turns all weight-gradient partials into the flat gradient buffer in a fixed order.
 """
 import math
+import os
 
 import torch
 
 from . import _native as nat
 
 F32 = 4
+# outputs per reduction item by partial-list length (<= 128, <= 384, longer); measured best of
+# 32..256 on the 48^3 step (tools/seg_caps.sh); L3U_SEG_CAPS overrides
+_SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32").split(","))
 
 
 class V:
@@ -172,7 +176,7 @@ class UNetEngine:
         base = self.offsets[dst_name][0] + dst_elem
         # outputs per item (one 256-thread workgroup each): fewer for long partial lists so that
         # every thread's serial share stays short (256 / cap threads share each output's terms)
-        cap = 32 if count <= 128 else (16 if count <= 384 else 8)
+        cap = _SEG_CAPS[0] if count <= 128 else (_SEG_CAPS[1] if count <= 384 else _SEG_CAPS[2])
         t0 = 0
         while t0 < length:
             ln = min(cap, length - t0)
