@@ -10,7 +10,8 @@ timed step).  N > 1: one process per GPU (torch.distributed.run), exact global-b
 scaling); time = max over ranks.
 
 Also reported: eval forward ms/patch (bs 1 and 4), config 5 (32->256, 64^3, step-based mixed
-domains) on one GPU, the config-4 whole-volume sliding-window
+domains) data-parallel over the job's GPUs, the grouped-conv variant on one GPU, the config-4
+whole-volume sliding-window
 inference of a 256^3 synthetic PET volume (seconds, ms/window; light_unet.utils), the roofline of
 the dominant kernel measured with HIP events around back-to-back replays of its C-ABI call, and
 the CPU baseline (the torch-CPU oracle restatement of the same network on this host's cores,
@@ -222,20 +223,23 @@ def sliding_bench(model, device, size=256):
             "note": "includes the host->device upload and the prob-map copy back"}
 
 
-def config5_bench(device, steps=20, warmup=5, bs=4, size=64, enc=(32, 64, 128, 256)):
-    """SURVEY §8d config 5 on this GPU: encoder 32->64->128->256 (812,284 parameters), 64^3
-    patches, bs 4, the reference's step-based mixed-domain epoch (trainer.py:260-347) with
+def config5_bench(device, world, rank, steps=20, warmup=5, bs=4, size=64, enc=(32, 64, 128, 256)):
+    """encoder 32->64->128->256 (812,284 parameters), 64^3 patches, bs 4
+    per GPU, the reference's step-based mixed-domain epoch (trainer.py:260-347) with
     dlbcl_steps_ratio 1.0: the FL stream's steps, then as many DLBCL steps, two synthetic
-    streams seeded 42 and 43 (loader.py:37 seed+1).  Graph-replayed step; per-GPU figure (the
-    8-GPU run of this config is the driver's)."""
+    streams seeded 42 and 43 (loader.py:37 seed+1; rank r adds 1000 r).  Graph-replayed step on
+    EVERY rank (data parallel over the job's GPUs, same exchange as the headline step); time =
+    max over ranks between barrier + synchronize, throughput = all ranks' patches / time."""
     from light_unet.models.unet3d import Lightweight3DUNet
     from light_unet.train_step import TrainStep
     torch.manual_seed(42)
     model = Lightweight3DUNet(encoder_channels=list(enc), dropout_p=0.1).to(device).train()
+    if world > 1:
+        dist.broadcast(model.flat_parameters(), 0)
     step = TrainStep(model, {"alpha": 0.7, "beta": 0.3, "gamma": 0.75}, lr=1e-4, weight_decay=1e-5)
     streams = []
     for seed in (42, 43):   # FL, DLBCL
-        rng = np.random.default_rng(seed)
+        rng = np.random.default_rng(seed + 1000 * rank)
         x = torch.from_numpy(rng.random((bs, 1, size, size, size), dtype=np.float32)).to(device)
         t = torch.from_numpy((rng.random((bs, 1, size, size, size)) > 0.97).astype(np.float32)).to(device)
         streams.append((x, t))
@@ -252,17 +256,29 @@ def config5_bench(device, steps=20, warmup=5, bs=4, size=64, enc=(32, 64, 128, 2
     for i in range(warmup):
         run(i, warmup)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
         loss = run(i, steps)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
     lv = float(loss.item())
     if not np.isfinite(lv):
         raise SystemExit(f"config 5: non-finite loss {lv}")
-    return {"workload": f"Lightweight3DUNet {'->'.join(map(str, enc))} train step, {size}^3, bs {bs}, "
+    return {"workload": f"Lightweight3DUNet {'->'.join(map(str, enc))} train step, {size}^3, bs {bs}/GPU, "
                         f"step-based FL ({half} steps) then DLBCL ({steps - half} steps)",
-            "params": int(model.flat_parameters().numel()), "patches_per_s_per_gpu": round(steps * bs / dt, 2),
+            "params": int(model.flat_parameters().numel()), "n_gpus": world,
+            "patches_per_s": round(world * steps * bs / dt, 2),
+            "patches_per_s_per_gpu": round(steps * bs / dt, 2),
             "ms_per_step": round(1000 * dt / steps, 4), "final_loss": round(lv, 6)}
 
 
@@ -274,7 +290,9 @@ def grouped_bench(device, steps=10, warmup=3, bs=4, size=48):
     from light_unet.train_step import TrainStep
     torch.manual_seed(42)
     model = Lightweight3DUNet(dropout_p=0.1, use_depthwise_separable=False).to(device).train()
-    step = TrainStep(model, {"alpha": 0.7, "beta": 0.3, "gamma": 0.75}, lr=1e-4, weight_decay=1e-5)
+    # rank-local (no exchange): this leg runs on rank 0 only
+    step = TrainStep(model, {"alpha": 0.7, "beta": 0.3, "gamma": 0.75}, lr=1e-4, weight_decay=1e-5,
+                     distributed=False)
     rng = np.random.default_rng(42)
     xs = torch.from_numpy(rng.random((bs, 1, size, size, size), dtype=np.float32)).to(device)
     ts = torch.from_numpy((rng.random((bs, 1, size, size, size)) > 0.97).astype(np.float32)).to(device)
@@ -373,7 +391,8 @@ def main():
         raise SystemExit(f"non-finite loss {final_loss}")
 
     sliding = sliding_bench(model, device) if (rank == 0 and not args.no_sliding) else None
-    cfg5 = config5_bench(device) if (rank == 0 and not args.no_config5) else None
+    cfg5 = config5_bench(device, world, rank) if not args.no_config5 else None   # every rank
+    cfg5 = cfg5 if rank == 0 else None
     grouped = grouped_bench(device) if (rank == 0 and not args.no_grouped) else None
     fwd1 = fwd_ms_per_patch(model, 1, args.size, device) if rank == 0 else None
     fwd4 = fwd_ms_per_patch(model, args.batch, args.size, device) if rank == 0 else None
@@ -407,7 +426,7 @@ def main():
             "fwd_ms_per_patch": {"bs1": round(fwd1, 4), f"bs{args.batch}": round(fwd4, 4)},
             "final_loss": round(final_loss, 6),
             "sliding_window_256": sliding,
-            "config5_1gpu": cfg5,
+            "config5": cfg5,
             "grouped_1gpu": grouped,
             "roofline": {
                 "kernel": f"l3u_dw3_bwd [{N},{cdom},{args.size}^3] (up3.res_block.conv1.depthwise "

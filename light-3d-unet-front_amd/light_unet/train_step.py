@@ -22,7 +22,7 @@ from .optim import FlatAdamW
 
 class TrainStep:
     def __init__(self, model, loss_cfg=None, lr=1e-4, weight_decay=1e-5, betas=(0.9, 0.999),
-                 eps=1e-8, group=None, ftl_mode="exact"):
+                 eps=1e-8, group=None, ftl_mode="exact", distributed=True):
         loss_cfg = loss_cfg or {}
         self.alpha = float(loss_cfg.get("alpha", 0.7))
         self.beta = float(loss_cfg.get("beta", 0.3))
@@ -37,7 +37,8 @@ class TrainStep:
         self.opt = FlatAdamW(self.flat, self.gflat, lr=lr, betas=betas, eps=eps,
                              weight_decay=weight_decay)
         self.group = group
-        self.world = world_size(group)
+        # distributed=False: a rank-local step (no exchange) even inside a process group
+        self.world = world_size(group) if distributed else 1
         self.ftl_mode = ftl_mode
         dev = self.flat.device
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
@@ -65,10 +66,12 @@ class TrainStep:
                                   self.loss))
 
     def _grad_exchange(self):
-        exchange_grads(self.gflat, self.ftl_mode, self.group)
+        if self.world > 1:
+            exchange_grads(self.gflat, self.ftl_mode, self.group)
 
     def _sums_exchange(self, sums):
-        exchange_ftl_sums(sums, self.ftl_mode, self.group)
+        if self.world > 1:
+            exchange_ftl_sums(sums, self.ftl_mode, self.group)
 
     # ----------------------------------------------------------------- eager step
     def __call__(self, x, t):
