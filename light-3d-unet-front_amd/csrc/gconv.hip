@@ -160,75 +160,86 @@ __global__ __launch_bounds__(256) void gconv3_kernel(
 
 // part[(n*nbk + bx)][co][k][t] = sum over the chunk's voxels v of dY[n][co][v] * A[n][ci][v+off(t)],
 // ci = (co / JG) * KG + k; A = x (XF 0) or lrelu(scale*(x-mean)+shift) (XF 1).  One workgroup per
-// (chunk, (tile of CO output channels of one group, k), n): each A neighbourhood load feeds CO
-// output channels; a fixed-order workgroup reduction of the CO x 27 taps (deterministic).
+// (chunk of kGB*kWVPT voxels, (group, k), n).  The chunk of A and its linear halo (one plane + one
+// row + one voxel each side) is staged in LDS ONCE, transformed on the way in; the workgroup then
+// walks the group's output channels CO at a time (each A neighbourhood read from LDS feeds CO
+// channels) with a fixed-order workgroup reduction of CO x 27 taps per tile (deterministic).
 template <bool XF, int CO>
 __global__ __launch_bounds__(256) void gconv3_wgrad_kernel(
     const float* __restrict__ dy, long long dyns, const float* __restrict__ a, long long ans,
     const float* __restrict__ rec, float* __restrict__ part, int G, int KG, int JG, int D, int H,
     int W) {
-  __shared__ float red[4][CO * 27];
-  const int S = D * H * W;
+  extern __shared__ float al[];            // [chunk + 2*halo] staged A, then [4][CO*27] reduction
+  const int S = D * H * W, HW = H * W;
+  const int halo = HW + W + 1, CH = kGB * kWVPT;
   const int nbk = gridDim.x, bx = blockIdx.x;
-  const int ntc = (JG + CO - 1) / CO;
-  const int k = blockIdx.y % KG, tile = blockIdx.y / KG;
-  const int g = tile / ntc, c0 = (tile % ntc) * CO;   // output channels g*JG + c0 .. (< JG)
-  const int ci = g * KG + k;
+  const int g = blockIdx.y / KG, k = blockIdx.y % KG, ci = g * KG + k;
   const int n = blockIdx.z;
+  const int v0 = bx * CH, lo = v0 - halo, len = min(CH, S - v0) + 2 * halo;
   const float* ap0 = a + (long long)n * ans + (long long)ci * S;
-  const float* dyp[CO];
-#pragma unroll
-  for (int j = 0; j < CO; ++j)
-    dyp[j] = dy + (long long)n * dyns + (long long)(g * JG + min(c0 + j, JG - 1)) * S;
   float mu = 0.f, sc = 1.f, sh = 0.f;
   if (XF) {
     const float* r = rec + ((long long)n * G * KG + ci) * kRec;
     mu = r[0]; sc = r[2]; sh = r[3];
   }
-  float acc[CO][27];
-#pragma unroll
-  for (int j = 0; j < CO; ++j)
-#pragma unroll
-    for (int t = 0; t < 27; ++t) acc[j][t] = 0.f;
-  for (int i = 0; i < kWVPT; ++i) {
-    const int v = (bx * kWVPT + i) * kGB + threadIdx.x;
-    if (v >= S) break;
-    float gv[CO];
-#pragma unroll
-    for (int j = 0; j < CO; ++j) gv[j] = dyp[j][v];
-    const int xx = v % W, t1 = v / W, yy = t1 % H, zz = t1 / H;
-    const bool okz[3] = {zz > 0, true, zz < D - 1};
-    const bool oky[3] = {yy > 0, true, yy < H - 1};
-    const bool okx[3] = {xx > 0, true, xx < W - 1};
-    const float* ap = ap0 + v;
-#pragma unroll
-    for (int t = 0; t < 27; ++t) {
-      const int dz = t / 9, dyy = (t / 3) % 3, dx = t % 3;
-      float val = 0.f;
-      if (okz[dz] && oky[dyy] && okx[dx]) {
-        val = ap[((dz - 1) * H + (dyy - 1)) * W + (dx - 1)];
-        if (XF) val = lrelu(fmaf(sc, val - mu, sh));
-      }
-#pragma unroll
-      for (int j = 0; j < CO; ++j) acc[j][t] = fmaf(gv[j], val, acc[j][t]);
+  for (int i = threadIdx.x; i < len; i += kGB) {
+    const int v = lo + i;
+    float val = 0.f;
+    if (v >= 0 && v < S) {
+      val = ap0[v];
+      if (XF) val = lrelu(fmaf(sc, val - mu, sh));
     }
+    al[i] = val;
   }
-  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-#pragma unroll
-  for (int j = 0; j < CO; ++j)
-#pragma unroll
-    for (int t = 0; t < 27; ++t) {
-      const float r = wave_sum(acc[j][t]);
-      if (ln == 0) red[wv][j * 27 + t] = r;
-    }
+  float* red = al + CH + 2 * halo;         // [4][CO*27]
   __syncthreads();
   const long long npair = (long long)G * JG * KG;
-  for (int e = threadIdx.x; e < CO * 27; e += kGB) {
-    const int j = e / 27, t = e - j * 27;
-    if (c0 + j >= JG) continue;
-    const float r = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
-    const long long pair = (long long)(g * JG + c0 + j) * KG + k;
-    part[(((long long)n * nbk + bx) * npair + pair) * 27 + t] = r;
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  for (int c0 = 0; c0 < JG; c0 += CO) {
+    const float* dyp[CO];
+#pragma unroll
+    for (int j = 0; j < CO; ++j)
+      dyp[j] = dy + (long long)n * dyns + (long long)(g * JG + min(c0 + j, JG - 1)) * S;
+    float acc[CO][27];
+#pragma unroll
+    for (int j = 0; j < CO; ++j)
+#pragma unroll
+      for (int t = 0; t < 27; ++t) acc[j][t] = 0.f;
+    for (int i = 0; i < kWVPT; ++i) {
+      const int v = v0 + i * kGB + threadIdx.x;
+      if (v >= S) break;
+      float gv[CO];
+#pragma unroll
+      for (int j = 0; j < CO; ++j) gv[j] = dyp[j][v];
+      const int xx = v % W, t1 = v / W, yy = t1 % H, zz = t1 / H;
+      const bool okz[3] = {zz > 0, true, zz < D - 1};
+      const bool oky[3] = {yy > 0, true, yy < H - 1};
+      const bool okx[3] = {xx > 0, true, xx < W - 1};
+      const float* ap = al + (v - lo);
+#pragma unroll
+      for (int t = 0; t < 27; ++t) {
+        const int dz = t / 9, dyy = (t / 3) % 3, dx = t % 3;
+        const float val = (okz[dz] && oky[dyy] && okx[dx]) ? ap[(dz - 1) * HW + (dyy - 1) * W + (dx - 1)] : 0.f;
+#pragma unroll
+        for (int j = 0; j < CO; ++j) acc[j][t] = fmaf(gv[j], val, acc[j][t]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CO; ++j)
+#pragma unroll
+      for (int t = 0; t < 27; ++t) {
+        const float r = wave_sum(acc[j][t]);
+        if (ln == 0) red[wv * CO * 27 + j * 27 + t] = r;
+      }
+    __syncthreads();
+    for (int e = threadIdx.x; e < CO * 27; e += kGB) {
+      const int j = e / 27, t = e - j * 27;
+      if (c0 + j >= JG) continue;
+      const float r = ((red[e] + red[CO * 27 + e]) + red[2 * CO * 27 + e]) + red[3 * CO * 27 + e];
+      const long long pair = (long long)(g * JG + c0 + j) * KG + k;
+      part[(((long long)n * nbk + bx) * npair + pair) * 27 + t] = r;
+    }
+    __syncthreads();
   }
 }
 
@@ -297,10 +308,12 @@ int l3u_gconv3_bwd_weight(const float* dy, long long dy_nstride, const float* x,
   L3U_REQUIRE(Cin % G == 0 && Cout % G == 0);
   const int S = D * H * W, KG = Cin / G, JG = Cout / G;
   const int co = JG >= kWCO ? kWCO : (JG >= 2 ? 2 : 1);
-  const long long ny = (long long)G * ((JG + co - 1) / co) * KG;
-  L3U_REQUIRE((long long)D * H * W < (1ll << 31) && ny <= 65535);
-  dim3 grid(l3u_gconv3_wgrad_nparts(1, S), (unsigned)ny, N), block(kGB);
-#define GW(X_, C_) hipLaunchKernelGGL((gconv3_wgrad_kernel<X_, C_>), grid, block, 0, stream, dy, \
+  L3U_REQUIRE((long long)D * H * W < (1ll << 31) && (long long)G * KG <= 65535);
+  const int halo = H * W + W + 1;
+  const size_t lds = ((size_t)kGB * kWVPT + 2 * halo + 4 * kWCO * 27) * sizeof(float);
+  L3U_REQUIRE(lds <= 160 * 1024);
+  dim3 grid(l3u_gconv3_wgrad_nparts(1, S), G * KG, N), block(kGB);
+#define GW(X_, C_) hipLaunchKernelGGL((gconv3_wgrad_kernel<X_, C_>), grid, block, lds, stream, dy, \
       dy_nstride, x, x_nstride, rec, part, G, KG, JG, D, H, W)
   if (rec) { if (co == kWCO) GW(true, kWCO); else if (co == 2) GW(true, 2); else GW(true, 1); }
   else { if (co == kWCO) GW(false, kWCO); else if (co == 2) GW(false, 2); else GW(false, 1); }
