@@ -4,8 +4,8 @@ Workload (BASELINE.json configs[1]): 16->32->64->128 U-Net
 batch 4 per GPU, fp32, dropout 0.1, FocalTversky(0.7, 0.3, 0.75), AdamW(lr 1e-4, wd 1e-5).
 A step = forward + loss + backward + optimizer (trainer.py:222-232) over one synthetic batch,
 replayed from a hipGraph; inputs are generated on the host before timing and are resident in HBM
-(a pool of 8 distinct batches, copied device-to-device into the graph's input buffers inside the
-timed step).  N > 1: one process per GPU (torch.distributed.run), exact global-batch FocalTversky
+(a pool of 8 distinct batches, each copied device-to-device into the graph's input buffer inside
+the timed step: one copy of image + target).  N > 1: one process per GPU (torch.distributed.run), exact global-batch FocalTversky
 (3-float all-reduce) + one flat-gradient RCCL all-reduce per step; per-GPU batch fixed (weak
 scaling); time = max over ranks.
 
@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--enc", type=str, default="16,32,64,128")
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--cpu-steps", type=int, default=40)   # ~10-30 s of host work
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--ftl-mode", default="exact", choices=["exact", "local"])
     ap.add_argument("--no-sliding", action="store_true", help="skip the config-4 inference timing")
@@ -60,14 +60,15 @@ def parse():
 
 
 def synthetic_pool(n_pool, bs, size, rank, device):
-    xs, ts = [], []
+    """n_pool batches resident in HBM, each image and target side by side in ONE buffer
+    [2, bs, 1, D, H, W] so that staging a batch into the graph's inputs is one copy."""
+    pool = []
     for i in range(n_pool):
         rng = np.random.default_rng(42 + 1000 * rank + i)
         x = rng.random((bs, 1, size, size, size), dtype=np.float32)
         t = (rng.random((bs, 1, size, size, size)) > 0.97).astype(np.float32)
-        xs.append(torch.from_numpy(x).to(device))
-        ts.append(torch.from_numpy(t).to(device))
-    return xs, ts
+        pool.append(torch.from_numpy(np.stack([x, t])).to(device))
+    return pool
 
 
 def dw_bytes(N, C, S):
@@ -342,8 +343,10 @@ def main():
         dist.broadcast(model.flat_parameters(), 0)
     step = TrainStep(model, {"alpha": 0.7, "beta": 0.3, "gamma": 0.75}, lr=1e-4, weight_decay=1e-5,
                      ftl_mode=args.ftl_mode)
-    xs, ts = synthetic_pool(8, args.batch, args.size, rank, device)
-    x_static, t_static = xs[0].clone(), ts[0].clone()
+    pool = synthetic_pool(8, args.batch, args.size, rank, device)
+    xs, ts = [b[0] for b in pool], [b[1] for b in pool]
+    xt_static = pool[0].clone()
+    x_static, t_static = xt_static[0], xt_static[1]
 
     # roofline leg (eager, instrumented): HIP events around the dominant kernel's launches
     N, S = args.batch, args.size ** 3
@@ -364,8 +367,7 @@ def main():
         step.capture(x_static, t_static, warmup=2)
 
         def run(i):
-            x_static.copy_(xs[i % 8], non_blocking=True)
-            t_static.copy_(ts[i % 8], non_blocking=True)
+            xt_static.copy_(pool[i % 8], non_blocking=True)   # the next batch: one D2D copy
             return step.replay()
 
     for i in range(args.warmup):
