@@ -83,9 +83,17 @@ class _GraphForward:
 def sliding_window_inference_3d(image: np.ndarray, model: torch.nn.Module,
                                 patch_size: Tuple[int, int, int] = (48, 48, 48),
                                 overlap: float = 0.5, device: torch.device = None,
-                                use_gaussian: bool = True, window_batch: int = 16) -> np.ndarray:
+                                use_gaussian: bool = True, window_batch: int = 16,
+                                group=None) -> np.ndarray:
     """utils.py:11-139.  `window_batch` windows run per forward (extra keyword; the result
-    does not depend on it)."""
+    does not depend on it).
+
+    `group` (extra keyword): a torch.distributed process group whose ranks (one
+    per GPU, every rank calling with the same image and weights) split the window batches
+    round-robin.  Each rank blends only its own windows' predictions (the others count as
+    zero; the denominator sum(importance) is the full one everywhere), and one all_reduce(SUM)
+    of the [D, H, W] map (RCCL over xGMI) adds the shares: the result equals the one-GPU map
+    up to the order of the fp32 additions."""
     if device is None:
         device = next(model.parameters()).device
     device = torch.device(device)
@@ -113,9 +121,15 @@ def sliding_window_inference_3d(image: np.ndarray, model: torch.nn.Module,
             vol = torch.from_numpy(np.ascontiguousarray(image, dtype=np.float32)).to(device)
             pos_all = torch.tensor(order + [order[-1]] * ((-nwin) % B), dtype=torch.int32,
                                    device=device)
-            preds = torch.empty(pos_all.shape[0], P, device=device)
+            world, rank = 1, 0
+            if group is not None:
+                import torch.distributed as dist
+                world, rank = dist.get_world_size(group), dist.get_rank(group)
+            preds = (torch.zeros if world > 1 else torch.empty)(pos_all.shape[0], P, device=device)
             fwd = _GraphForward(model, vol, d, h, w, (pd, ph, pw), B, device)
-            for b0 in range(0, nwin, B):
+            for bi, b0 in enumerate(range(0, nwin, B)):
+                if bi % world != rank:   # another rank's batch
+                    continue
                 fwd.pos.copy_(pos_all[b0:b0 + B])
                 out = fwd()
                 if out.dim() != 5 or tuple(out.shape[2:]) != (pd, ph, pw):
@@ -127,6 +141,8 @@ def sliding_window_inference_3d(image: np.ndarray, model: torch.nn.Module,
             nat.call("l3u_window_blend", preds.data_ptr(), zt.data_ptr(), len(zs), yt.data_ptr(),
                      len(ys), xt.data_ptr(), len(xs), impt.data_ptr(), d, h, w, pd, ph, pw,
                      prob.data_ptr(), nat.stream())
+            if world > 1:
+                dist.all_reduce(prob, op=dist.ReduceOp.SUM, group=group)
             return prob.cpu().numpy()
     finally:
         model.train(was_training)
