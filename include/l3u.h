@@ -109,6 +109,17 @@ int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, lon
  * (one workgroup per voxel chunk) or J in {64, 128}, any K (one per 64-voxel tile and 16 columns
  * of K, for the small latency-bound levels).                                                     */
 int l3u_pw_bwd_supported(int J, int K, int S);
+/* the same backward for conv2.pointwise (sel 1: yr = y2, rec = rec2) or the Conv1x1 shortcut
+ * (sel 2: yr = r, rec = rec_r) with the block tail's backward (l3u_norm_act_bwd_apply) formed on
+ * the fly from dout, out, yr and the l3u_norm_act_bwd_reduce partials tail_part[J][N][npart][3]:
+ * dY = rstd*gamma*(g - mean(g) - xhat*mean(g*xhat)), g = dout*lrelu'(out), never written.
+ * Supported: l3u_pw_bwd_supported(J, K, S) with J <= 32 (the 48^3 / 24^3 levels).            */
+int l3u_pw_bwd_tail(const float* dout, long long dout_nstride, const float* out,
+                    long long out_nstride, const float* yr, long long yr_nstride, const float* rec,
+                    const double* tail_part, int npart, int sel, const float* x,
+                    long long x_nstride, const float* w, float* dx, long long dx_nstride,
+                    int accumulate, float* part, int N, int J, int K, int S, hipStream_t stream);
+
 int l3u_pw_bwd_nparts(int N, int J, int K, int S);
 int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long y_nstride,
                const float* rec, const double* in_part, int npart, const float* x,

@@ -549,7 +549,8 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
     const float* __restrict__ x, long long xns, const float* __restrict__ w,
     float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part, int N, int J,
-    int K, int S, int SCH, int nsc) {
+    int K, int S, int SCH, int nsc, const float* __restrict__ oin = nullptr, long long oins = 0,
+    int sel = 1) {
   constexpr int TJ = 16 * NJ, TK = 16 * NK, JR = TJ / 4;
   constexpr int WS = TK + ((16 - TK) % 64 + 64) % 64;   // >= TK, = 16 mod 64
   constexpr int DS = 68;                                // dY tile row stride (floats)
@@ -570,12 +571,21 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   float* dxn = dx + (long long)n * dxns;
 
   // 1. every streamed load of the tile is issued first ...
-  f4 g[JR], yv[PRO ? JR : 1];
+  f4 g[JR], yv[PRO ? JR : 1], ov[PRO == 2 ? JR : 1];
 #pragma unroll
   for (int jr = 0; jr < JR; ++jr) {
     const int j = 4 * jr + lk;
     g[jr] = f4{0.f, 0.f, 0.f, 0.f};
     if (j < J && sd < s_hi) g[jr] = *reinterpret_cast<const f4*>(dyn + (long long)j * S + sd);
+  }
+  if (PRO == 2) {   // the block output (LeakyReLU mask of the tail)
+    const float* on = oin + (long long)n * oins;
+#pragma unroll
+    for (int jr = 0; jr < JR; ++jr) {
+      const int j = 4 * jr + lk;
+      ov[jr] = f4{0.f, 0.f, 0.f, 0.f};
+      if (j < J && sd < s_hi) ov[jr] = *reinterpret_cast<const f4*>(on + (long long)j * S + sd);
+    }
   }
   if (PRO) {
     const float* yn = yin + (long long)n * yns;
@@ -604,8 +614,13 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const int j = tid / PS, sub = tid % PS;
     double t0 = 0.0, t1 = 0.0;
     if (j < J) {
-      const double* pp = in_part + ((long long)j * N + n) * npart * 2;
-      for (int i = sub; i < npart; i += PS) { t0 += pp[i * 2]; t1 += pp[i * 2 + 1]; }
+      if (PRO == 2) {   // block-tail partials [J][N][npart][3]: {sum g, sum g*xhat2, sum g*xhat_r}
+        const double* pp = in_part + ((long long)j * N + n) * npart * 3;
+        for (int i = sub; i < npart; i += PS) { t0 += pp[i * 3]; t1 += pp[i * 3 + sel]; }
+      } else {
+        const double* pp = in_part + ((long long)j * N + n) * npart * 2;
+        for (int i = sub; i < npart; i += PS) { t0 += pp[i * 2]; t1 += pp[i * 2 + 1]; }
+      }
     }
     psum[tid * 2] = t0;
     psum[tid * 2 + 1] = t1;
@@ -636,6 +651,10 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       const float* c = coef + j * 8;
       const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
       const bool ok = j < J && sd < s_hi;
+      if (PRO == 2) {   // g = dout * lrelu'(out), then the tail InstanceNorm backward
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g[jr][q] = g[jr][q] * lrelu_d(ov[jr][q]);
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) g[jr][q] = ok ? f * (g[jr][q] - M1 - (yv[jr][q] - mu) * rs * M2) : 0.f;
     }
@@ -1072,6 +1091,42 @@ int l3u_pw_bwd_supported(int J, int K, int S) {
 int l3u_pw_bwd_nparts(int N, int J, int K, int S) {
   if (!l3u_pw_bwd_supported(J, K, S)) return 0;
   return pw_bwd_wide(J) ? N * ((S + 63) / 64) : l3u_pw_bwd_weight_nparts(N, S);
+}
+
+// the pointwise backward of conv2.pointwise (sel 1: yr = y2, rec = rec2) or of the shortcut conv
+// (sel 2: yr = r, rec = rec_r) with the block tail's backward (l3u_norm_act_bwd_apply) formed in
+// its prologue from dout / out / yr and the tail partials, so dy2 / dr are never written
+int l3u_pw_bwd_tail(const float* dout, long long dout_nstride, const float* out,
+                    long long out_nstride, const float* yr, long long yr_nstride, const float* rec,
+                    const double* tail_part, int npart, int sel, const float* x,
+                    long long x_nstride, const float* w, float* dx, long long dx_nstride,
+                    int accumulate, float* part, int N, int J, int K, int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && l3u_pw_bwd_supported(J, K, S) && !pw_bwd_wide(J));
+  L3U_REQUIRE(dout && out && yr && rec && tail_part && npart > 0 && (sel == 1 || sel == 2));
+  L3U_REQUIRE(x && w && dx && part);
+  const bool al = ((uintptr_t)dout & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                  ((uintptr_t)yr & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
+                  ((uintptr_t)dx & 15) == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
+                  yr_nstride % 4 == 0 && x_nstride % 4 == 0 && dx_nstride % 4 == 0;
+  L3U_REQUIRE(al);
+  const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
+  const int NJ = J <= 16 ? 1 : 2;
+  int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
+  while (NK > 1 && (long long)N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < L3U_PWBF_MIN_BLOCKS) NK >>= 1;
+  const int nwv = SCH / 64;
+  L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
+  dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
+#define PWBT(A_, B_) hipLaunchKernelGGL((pw_bwd_fused_kernel<A_, B_, 2>), grid, block, 0, stream, \
+      dout, dout_nstride, yr, yr_nstride, rec, tail_part, npart, x, x_nstride, w, dx, dx_nstride, \
+      accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel)
+  if (NJ == 1 && NK == 1) PWBT(1, 1);
+  else if (NJ == 1 && NK == 2) PWBT(1, 2);
+  else if (NJ == 1 && NK == 4) PWBT(1, 4);
+  else if (NJ == 2 && NK == 1) PWBT(2, 1);
+  else if (NJ == 2 && NK == 2) PWBT(2, 2);
+  else PWBT(2, 4);
+#undef PWBT
+  L3U_CHECK_LAUNCH();
 }
 
 int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long y_nstride,

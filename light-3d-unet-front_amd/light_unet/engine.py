@@ -24,6 +24,8 @@ from . import _native as nat
 F32 = 4
 # outputs per reduction item by partial-list length (<= 128, <= 384, longer); measured best of
 # 32..256 on the 48^3 step (tools/seg_caps.sh); L3U_SEG_CAPS overrides
+# block-tail backward inside the pointwise backwards (l3u_pw_bwd_tail); L3U_TAIL_FUSE=0 disables
+_TAIL_FUSE = os.environ.get("L3U_TAIL_FUSE", "1") != "0"
 _SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32").split(","))
 
 
@@ -538,10 +540,20 @@ class UNetEngine:
                         st, dev)
         return dx if need_dx else None
 
-    def _tail_bwd(self, pre, sv, dout, dxv, N, cout, S, st, dev):
+    def _tail_fusable(self, sv, cin, cout, S):
+        """The block tail's backward can ride in the prologues of the two pointwise backwards
+        (l3u_pw_bwd_tail) instead of l3u_norm_act_bwd_apply: Conv1x1 shortcut, several
+        workgroups per plane (one-workgroup planes take the one-launch l3u_norm_act_bwd) and
+        the fused-kernel shapes for conv2.pointwise (J = K = cout) and the shortcut (K = cin)."""
+        return (_TAIL_FUSE and sv["shortcut"] and nat.query("l3u_norm_act_nblocks", S) > 1
+                and cout <= 32 and nat.query("l3u_pw_bwd_supported", cout, cout, S)
+                and nat.query("l3u_pw_bwd_supported", cout, cin, S))
+
+    def _tail_bwd(self, pre, sv, dout, dxv, N, cout, S, st, dev, fused=False):
         """Backward of the block tail out = lrelu(IN2(y2) + residual): d y2 and d residual (the
         shortcut-conv output, or dxv itself for the identity shortcut), with the norm2 / shortcut
-        IN parameter-gradient reductions recorded."""
+        IN parameter-gradient reductions recorded.  fused: only the reduce; returns the tail
+        partials' arena offset for l3u_pw_bwd_tail instead."""
         A = self.bwd_arena
         out, recs = sv["out"], sv["recs"]
         rec_r, rec2 = recs[0].data_ptr(), recs[2].data_ptr()
@@ -553,6 +565,12 @@ class UNetEngine:
         pnd = pn // 2
         self._seg(pnd + 1, N * nb, 3, N * nb * 3, cout, pre + "norm2.weight", f64=1)
         self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "norm2.bias", f64=1)
+        if fused:
+            self._seg(pnd + 2, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.weight", f64=1)
+            self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.bias", f64=1)
+            self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(),
+                       cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S, st)
+            return pn, nb
         dy2 = self._empty(N, cout, S, device=dev)
         if shortcut:
             dr = self._empty(N, cout, S, device=dev)
@@ -642,11 +660,20 @@ class UNetEngine:
         rv = sv["r"] if shortcut else x
         y2, z2, y1, z1 = sv["y2"], sv["z2"], sv["y1"], sv["z1"]
         # (1) block tail: out = lrelu(IN2(y2) + residual)
-        dy2, drv = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev)
-        # (2) conv2.pointwise backward
+        fused = self._tail_fusable(sv, cin, cout, S)
         dz2 = e(N, cout, S)
-        self._pw_bwd(flat, V(dy2, 0, cout * S, cout), None, V(z2, 0, cout * S, cout),
-                     pre + "conv2.pointwise.weight", V(dz2, 0, cout * S, cout), 0, N, S, st)
+        if fused:
+            # (1+2) the tail reduce, then conv2.pointwise backward with the tail's apply in its
+            # prologue (dy2 is never written)
+            pn, ntp = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev, fused=True)
+            self._pw_bwd_tail(flat, dout, sv["out"], V(y2, 0, cout * S, cout), rec2, pn, ntp, 1,
+                              V(z2, 0, cout * S, cout), pre + "conv2.pointwise.weight",
+                              V(dz2, 0, cout * S, cout), 0, N, S, st)
+        else:
+            dy2, drv = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev)
+            # (2) conv2.pointwise backward
+            self._pw_bwd(flat, V(dy2, 0, cout * S, cout), None, V(z2, 0, cout * S, cout),
+                         pre + "conv2.pointwise.weight", V(dz2, 0, cout * S, cout), 0, N, S, st)
         # (3) conv2.depthwise backward fused with LeakyReLU/Dropout/IN1 backward partials
         nch = nat.query("l3u_dw3_nchunk", N, cout, d, h, w)
         pd2 = A.alloc(cout * N * nch * 27)
@@ -682,11 +709,15 @@ class UNetEngine:
                    0 if shortcut else 1, A.ptr(pd1), None, N, cin, d, h, w, st)
         self._seg_dw(pd1, N * nch1, cin, pre + "conv1.depthwise.weight")
         # (6) shortcut conv backward accumulates into d(input)
-        if shortcut:
+        if fused:
+            self._pw_bwd_tail(flat, dout, sv["out"], sv["r"], rec_r, pn, ntp, 2, x,
+                              pre + "shortcut.0.weight", dxv, 1, N, S, st)
+        elif shortcut:
             self._pw_bwd(flat, drv, None, x, pre + "shortcut.0.weight", dxv, 1, N, S, st)
         if self.debug is not None and not self._dry:
-            self.debug[pre + "#"] = {"dy2": dy2, "dr": drv, "dz2": dz2, "dy1": dy1, "dz1": dz1,
-                                     "dx": dxv}
+            self.debug[pre + "#"] = {"dz2": dz2, "dy1": dy1, "dz1": dz1, "dx": dxv}
+            if not fused:
+                self.debug[pre + "#"].update(dy2=dy2, dr=drv)
 
     def _pw_bwd(self, flat, dy, pro, x, name, dx, accumulate, N, S, st):
         """Backward of a 1x1 conv y = W x (W = parameter `name`, [J][K]): dx (+)= W^T dy, and the
@@ -709,6 +740,19 @@ class UNetEngine:
             self._call("l3u_pw_fwd", dy.p, dy.ns, w, 1, None, dx.p, dx.ns, accumulate, None, N, J, K,
                        S, st)
             self._call("l3u_pw_bwd_weight", dy.p, dy.ns, x.p, x.ns, A.ptr(part), N, J, K, S, st)
+        self._seg(part, npw, J * K, 1, J * K, name)
+
+    def _pw_bwd_tail(self, flat, dout, out, yr, rec, pn, ntp, sel, x, name, dx, accumulate, N, S,
+                     st):
+        """_pw_bwd of conv2.pointwise (sel 1, yr = y2) or the shortcut (sel 2, yr = r) with the
+        block tail's InstanceNorm/LeakyReLU backward formed in the kernel prologue."""
+        J, K = out.C, x.C
+        A = self.bwd_arena
+        npw = nat.query("l3u_pw_bwd_nparts", N, J, K, S)
+        part = A.alloc(npw * J * K)
+        self._call("l3u_pw_bwd_tail", dout.p, dout.ns, out.p, out.ns, yr.p, yr.ns, rec, A.ptr(pn),
+                   ntp, sel, x.p, x.ns, self._w(flat, name), dx.p, dx.ns, accumulate, A.ptr(part),
+                   N, J, K, S, st)
         self._seg(part, npw, J * K, 1, J * K, name)
 
     def _seg_dw(self, off, count, C, name):

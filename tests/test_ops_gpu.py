@@ -891,3 +891,51 @@ def test_norm_act_bwd_one_launch_equals_pair(cuda, shape, shortcut):
 
     for a, b in zip(run(True), run(False)):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 32, 48 ** 3), (4, 32, 16, 24 ** 3), (2, 16, 8, 1000),
+                                   (1, 8, 3, 7 * 9 * 12)])
+def test_pw_bwd_tail_equals_apply_then_pw_bwd(cuda, shape):
+    """l3u_pw_bwd_tail (the block tail's IN/LeakyReLU backward in the pointwise backward's
+    prologue) == l3u_norm_act_bwd_apply followed by l3u_pw_bwd, for conv2.pointwise (sel 1,
+    K = J) and the Conv1x1 shortcut (sel 2, accumulate), to fp32 rounding (the per-channel
+    means are summed in another order)."""
+    N, J, K, S = shape
+    gen = torch.Generator().manual_seed(43)
+    t = lambda C: torch.randn(N, C, S, generator=gen).to(cuda)  # noqa: E731
+    dout, out, y2, r = t(J), t(J), t(J), t(J)
+    z2, x = t(J), t(K)
+    rec2 = make_rec(N, J, gen).float().to(cuda)
+    recr = make_rec(N, J, gen).float().to(cuda)
+    w2 = torch.randn(J, J, generator=gen).to(cuda)
+    wr = torch.randn(J, K, generator=gen).to(cuda)
+    nb = nat().query("l3u_norm_act_nblocks", S)
+    part = torch.empty(J * N * nb * 3, dtype=torch.float64, device=cuda)
+    a = (dout.data_ptr(), J * S, out.data_ptr(), J * S, y2.data_ptr(), J * S, rec2.data_ptr(),
+         r.data_ptr(), J * S, recr.data_ptr())
+    nat().call("l3u_norm_act_bwd_reduce", *a, part.data_ptr(), N, J, S, st())
+    dy2 = torch.empty(N, J, S, device=cuda)
+    dr = torch.empty(N, J, S, device=cuda)
+    nat().call("l3u_norm_act_bwd_apply", *a, part.data_ptr(), dy2.data_ptr(), J * S, dr.data_ptr(),
+               J * S, N, J, S, st())
+    init = t(K)
+    for sel, yr, rec, dy, xin, w, K_, acc in ((1, y2, rec2, dy2, z2, w2, J, 0),
+                                               (2, r, recr, dr, x, wr, K, 1)):
+        npw = nat().query("l3u_pw_bwd_nparts", N, J, K_, S)
+        outs = []
+        for fused in (False, True):
+            dx = init[:, :K_].contiguous().clone() if acc else torch.empty(N, K_, S, device=cuda)
+            pp = torch.empty(npw * J * K_, device=cuda)
+            if fused:
+                nat().call("l3u_pw_bwd_tail", dout.data_ptr(), J * S, out.data_ptr(), J * S,
+                           yr.data_ptr(), J * S, rec.data_ptr(), part.data_ptr(), nb, sel,
+                           xin.data_ptr(), K_ * S, w.data_ptr(), dx.data_ptr(), K_ * S, acc,
+                           pp.data_ptr(), N, J, K_, S, st())
+            else:
+                nat().call("l3u_pw_bwd", dy.data_ptr(), J * S, None, 0, None, None, 0,
+                           xin.data_ptr(), K_ * S, w.data_ptr(), dx.data_ptr(), K_ * S, acc,
+                           pp.data_ptr(), N, J, K_, S, st())
+            torch.cuda.synchronize()
+            outs.append((dx, pp.view(npw, J * K_).double().sum(0)))
+        close(outs[1][0], outs[0][0], 1e-5, f"dx sel{sel} {shape}")
+        close(outs[1][1], outs[0][1], 1e-5, f"dW sel{sel} {shape}")

@@ -106,6 +106,8 @@ def main(fname="model_b1_48.npz", dtype=torch.float64):
         dd = eng.debug[name + "#"]
         for key, ref in (("dy2", y2.grad), ("dz2", z2.grad), ("dy1", y1.grad), ("dz1", z1.grad),
                          ("dx", X.grad)) + ((("dr", r.grad),) if r is not X else ()):
+            if key not in dd:   # dy2 / dr are never materialised when the tail is fused
+                continue
             v = dd[key]
             if hasattr(v, "ns"):
                 v = v.t.reshape(-1)[v.off:].as_strided((N, v.C, S), (v.ns, S, 1))
