@@ -247,6 +247,17 @@ int l3u_ftl_nblocks(long long numel);
 int l3u_ftl_sums(const float* p, const float* t, long long numel, float* part, double* sums,
                  hipStream_t stream);
 /* second stage only (partials from l3u_outconv_fwd): sums[3] = fixed-order sum of part[nparts][3] */
+/* l3u_outconv_bwd that also writes the first stage of the last decoder block's tail backward
+ * (l3u_norm_act_bwd_reduce of up3.res_block, whose output is h): tail_part[C][N][nb][3] =
+ * {sum g, sum g*xhat2, sum g*xhat_r}, g = dh*lrelu'(h), nb = l3u_outconv_nblocks(S); for the
+ * Conv1x1-shortcut block, C <= 16, S % 4 == 0                                                  */
+int l3u_outconv_bwd_tail(const float* dp, const float* p, const float* t, const double* sums,
+                         double alpha, double beta, double gamma, double smooth,
+                         const float* gscale, const float* h, long long h_nstride, const float* w,
+                         float* dh, long long dh_nstride, double* part, float* loss,
+                         const float* y2, long long y2_nstride, const float* rec2, const float* r,
+                         long long r_nstride, const float* rec_r, double* tail_part, int N, int C,
+                         int S, hipStream_t stream);
 int l3u_ftl_reduce(const float* part, int nparts, double* sums, hipStream_t stream);
 int l3u_ftl_loss(const double* sums, double alpha, double beta, double gamma, double smooth,
                  float* loss, hipStream_t stream);

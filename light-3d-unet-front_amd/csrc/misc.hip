@@ -191,14 +191,20 @@ L3U_DEV FtlCoef ftl_coef(const double* sums, double alpha, double beta, double g
 // dz = dL/dp * p(1-p); dh[c] = w[c] * dz; part[n*nb + blk][0..C-1] = sum dz*h[c], [C] = sum dz.
 // dL/dp comes from dp, or (dp == NULL) from the FocalTversky closed form A t + B (1 - t) of the
 // global sums (losses.py:30-54), fused so the loss gradient is never written out.
-template <bool VEC>
+// TAIL: also the first stage of the last decoder block's tail backward (l3u_norm_act_bwd_reduce
+// of up3, whose output IS h): tpart[c][n][nb][3] = {sum g, sum g*xhat2, sum g*xhat_r} over the
+// workgroup's voxels, g = dh * lrelu'(h), so dh and h are not read again for it.
+template <bool VEC, bool TAIL = false>
 __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     const float* __restrict__ dp, const float* __restrict__ p, const float* __restrict__ t,
     const double* __restrict__ sums, double alpha, double beta, double gamma, double smooth,
     const float* __restrict__ gscale, const float* __restrict__ h, long long hns,
     const float* __restrict__ w, float* __restrict__ dh, long long dhns,
-    double* __restrict__ part, float* __restrict__ loss, int C, int S) {
-  extern __shared__ double redd[];   // [4][C+1]
+    double* __restrict__ part, float* __restrict__ loss, int C, int S,
+    const float* __restrict__ y2 = nullptr, long long y2ns = 0, const float* __restrict__ rec2 = nullptr,
+    const float* __restrict__ r = nullptr, long long rns = 0, const float* __restrict__ recr = nullptr,
+    double* __restrict__ tpart = nullptr, int N = 0) {
+  extern __shared__ double redd[];   // [4][C+1] (TAIL: [4][3C])
   __shared__ float coef[2];
   const int n = blockIdx.y, nb = gridDim.x;
   if (dp == nullptr) {
@@ -228,6 +234,11 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
 #pragma unroll
   for (int c = 0; c < 33; ++c) acc[c] = 0.f;
   acc[32] = (dz[0] + dz[1]) + (dz[2] + dz[3]);
+  float ts[TAIL ? 3 * 16 : 1];
+  if (TAIL) {
+#pragma unroll
+    for (int c = 0; c < 3 * 16; ++c) ts[c] = 0.f;
+  }
 #pragma unroll
   for (int c = 0; c < 32; ++c) {
     if (c < C) {
@@ -235,7 +246,22 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
         if (i0 < S) {
           const f4 hv = *reinterpret_cast<const f4*>(hp + (long long)c * S + i0);
           acc[c] = fmaf(dz[0], hv[0], fmaf(dz[1], hv[1], fmaf(dz[2], hv[2], dz[3] * hv[3])));
-          *reinterpret_cast<f4*>(dhp + (long long)c * S + i0) = w[c] * dz;
+          const f4 dhv = w[c] * dz;
+          *reinterpret_cast<f4*>(dhp + (long long)c * S + i0) = dhv;
+          if (TAIL && c < 16) {   // same float expressions as norm_act_bwd_reduce_kernel
+            const float* q2 = rec2 + ((long long)n * C + c) * kRec;
+            const float* qr = recr + ((long long)n * C + c) * kRec;
+            const float m2 = q2[0], rs2 = q2[1], mr = qr[0], rsr = qr[1];
+            const f4 yv = *reinterpret_cast<const f4*>(y2 + (long long)n * y2ns + (long long)c * S + i0);
+            const f4 rv = *reinterpret_cast<const f4*>(r + (long long)n * rns + (long long)c * S + i0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float g = dhv[q] * lrelu_d(hv[q]);
+              ts[3 * c] += g;
+              ts[3 * c + 1] += g * ((yv[q] - m2) * rs2);
+              ts[3 * c + 2] += g * ((rv[q] - mr) * rsr);
+            }
+          }
         }
       } else {
 #pragma unroll
@@ -260,6 +286,22 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     const int tt = threadIdx.x;
     const double r = (redd[tt] + redd[(C + 1) + tt]) + (redd[2 * (C + 1) + tt] + redd[3 * (C + 1) + tt]);
     part[((long long)n * nb + blockIdx.x) * (C + 1) + tt] = r;
+  }
+  if (TAIL) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 3 * 16; ++e) {
+      if (e < 3 * C) {
+        const double v = wave_sum_d((double)ts[e]);
+        if (l == 0) redd[wv * 3 * C + e] = v;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 * C) {
+      const int e = threadIdx.x, c = e / 3, k = e - 3 * c;
+      const double v = (redd[e] + redd[3 * C + e]) + (redd[6 * C + e] + redd[9 * C + e]);
+      tpart[(((long long)c * N + n) * nb + blockIdx.x) * 3 + k] = v;
+    }
   }
 }
 
@@ -580,8 +622,27 @@ int l3u_outconv_bwd(const float* dp, const float* p, const float* t, const doubl
   const bool vec = S % 4 == 0 && h_nstride % 4 == 0 && dh_nstride % 4 == 0;
   dim3 grid((S + 1023) / 1024, N);
   const size_t lds = 4 * (C + 1) * sizeof(double);
-  if (vec) hipLaunchKernelGGL(outconv_bwd_kernel<true>, grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S);
-  else hipLaunchKernelGGL(outconv_bwd_kernel<false>, grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S);
+  if (vec) hipLaunchKernelGGL((outconv_bwd_kernel<true, false>), grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S);
+  else hipLaunchKernelGGL((outconv_bwd_kernel<false, false>), grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_outconv_bwd_tail(const float* dp, const float* p, const float* t, const double* sums,
+                         double alpha, double beta, double gamma, double smooth,
+                         const float* gscale, const float* h, long long h_nstride, const float* w,
+                         float* dh, long long dh_nstride, double* part, float* loss,
+                         const float* y2, long long y2_nstride, const float* rec2, const float* r,
+                         long long r_nstride, const float* rec_r, double* tail_part, int N, int C,
+                         int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && C <= 16 && S > 0 && S % 4 == 0);
+  L3U_REQUIRE(dp != nullptr || (t != nullptr && sums != nullptr));
+  L3U_REQUIRE(y2 && rec2 && r && rec_r && tail_part);
+  L3U_REQUIRE(h_nstride % 4 == 0 && dh_nstride % 4 == 0 && y2_nstride % 4 == 0 && r_nstride % 4 == 0);
+  dim3 grid((S + 1023) / 1024, N);
+  const size_t lds = 4 * 3 * (C + 1) * sizeof(double);
+  hipLaunchKernelGGL((outconv_bwd_kernel<true, true>), grid, dim3(256), lds, stream, dp, p, t, sums,
+                     alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss,
+                     C, S, y2, y2_nstride, rec2, r, r_nstride, rec_r, tail_part, N);
   L3U_CHECK_LAUNCH();
 }
 

@@ -63,6 +63,8 @@ _SIGS = {
     "l3u_ftl_bwd": [P, P, L, P, D, D, D, D, P, I, P, P],
     "l3u_adamw": [P, P, P, P, L, P, F, F, F, F, P, F, P],
     "l3u_reduce_segments": [P, P, I, P, P],
+    "l3u_outconv_bwd_tail": [P, P, P, P, D, D, D, D, P, P, L, P, P, L, P, P, P, L, P, P, L, P, P,
+                             I, I, I, P],
     "l3u_pw_bwd_tail": [P, L, P, L, P, L, P, P, I, I, P, L, P, P, L, I, P, I, I, I, I, P],
     "l3u_norm_act_bwd": [P, L, P, L, P, L, P, P, L, P, P, P, L, P, L, I, I, I, P],
     "l3u_gconv3_nblocks": [I],

@@ -26,6 +26,8 @@ F32 = 4
 # 32..256 on the 48^3 step (tools/seg_caps.sh); L3U_SEG_CAPS overrides
 # block-tail backward inside the pointwise backwards (l3u_pw_bwd_tail); L3U_TAIL_FUSE=0 disables
 _TAIL_FUSE = os.environ.get("L3U_TAIL_FUSE", "1") != "0"
+# ... and the last decoder block's tail reduce inside the out_conv backward (L3U_OUTCONV_TAIL)
+_OUTCONV_TAIL = os.environ.get("L3U_OUTCONV_TAIL", "0") != "0"   # measured +4 us: off
 _SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32").split(","))
 
 
@@ -476,9 +478,23 @@ class UNetEngine:
             g = (None, t.data_ptr(), sums.data_ptr(), alpha, beta, gamma, smooth, None)
             if len(ftl) > 3 and ftl[3] is not None:   # the loss value, written by the same launch
                 loss_ptr = ftl[3].data_ptr()
-        self._call("l3u_outconv_bwd", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
-                   self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po), loss_ptr,
-                   N, c0, S[0], st)
+        # the last decoder block's tail reduce rides in the out_conv backward (its output is h)
+        b3 = sv["blk"]["up3.res_block."]
+        tail_pre = None
+        if (_TAIL_FUSE and _OUTCONV_TAIL and c0 <= 16 and S[0] % 4 == 0 and b3["out"].C == c0
+                and self.kinds["up3.res_block."][0][0] == "ds"
+                and self._tail_fusable(b3, b3["x"].C, c0, S[0])):
+            ntp = nat.query("l3u_outconv_nblocks", S[0])
+            pt = A.alloc(2 * c0 * N * ntp * 3)            # fp64 partials
+            self._call("l3u_outconv_bwd_tail", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
+                       self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po), loss_ptr,
+                       b3["y2"].data_ptr(), c0 * S[0], b3["recs"][2].data_ptr(), b3["r"].p, b3["r"].ns,
+                       b3["recs"][0].data_ptr(), A.ptr(pt), N, c0, S[0], st)
+            tail_pre = (pt, ntp)
+        else:
+            self._call("l3u_outconv_bwd", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
+                       self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po),
+                       loss_ptr, N, c0, S[0], st)
         self._seg(po // 2, N * nb, c0 + 1, 1, c0, "out_conv.weight", f64=1)
         self._seg(po // 2 + c0, N * nb, c0 + 1, 1, 1, "out_conv.bias", f64=1)
         dcat3, dcat2, dcat1 = e(N, 2 * c0, S[0]), e(N, 2 * c1, S[1]), e(N, 2 * c2, S[2])
@@ -489,7 +505,8 @@ class UNetEngine:
         for up, co, lvl, uidx in up_specs:
             dcat = dcats[lvl]
             self._block_bwd(flat, up + "res_block.", sv["blk"][up + "res_block."], dout,
-                            V(dcat, 0, 2 * co * S[lvl], 2 * co), st, dev)
+                            V(dcat, 0, 2 * co * S[lvl], 2 * co), st, dev,
+                            tail_pre=tail_pre if up == "up3." else None)
             # ConvTranspose3d backward: input = prev (the lower-level output), dOut = dcat[:, :co]
             prev, _ = sv["ups"][uidx]
             ci = prev.C
@@ -549,7 +566,7 @@ class UNetEngine:
                 and cout <= 32 and nat.query("l3u_pw_bwd_supported", cout, cout, S)
                 and nat.query("l3u_pw_bwd_supported", cout, cin, S))
 
-    def _tail_bwd(self, pre, sv, dout, dxv, N, cout, S, st, dev, fused=False):
+    def _tail_bwd(self, pre, sv, dout, dxv, N, cout, S, st, dev, fused=False, tail_pre=None):
         """Backward of the block tail out = lrelu(IN2(y2) + residual): d y2 and d residual (the
         shortcut-conv output, or dxv itself for the identity shortcut), with the norm2 / shortcut
         IN parameter-gradient reductions recorded.  fused: only the reduce; returns the tail
@@ -560,16 +577,20 @@ class UNetEngine:
         shortcut = sv["shortcut"]
         rv = sv["r"] if shortcut else sv["x"]
         y2 = sv["y2"]
-        nb = nat.query("l3u_norm_act_nblocks", S)
-        pn = A.alloc(2 * cout * N * nb * 3)            # fp64 partials
+        if tail_pre is not None:   # partials already written by the producer of dout
+            pn, nb = tail_pre
+        else:
+            nb = nat.query("l3u_norm_act_nblocks", S)
+            pn = A.alloc(2 * cout * N * nb * 3)            # fp64 partials
         pnd = pn // 2
         self._seg(pnd + 1, N * nb, 3, N * nb * 3, cout, pre + "norm2.weight", f64=1)
         self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "norm2.bias", f64=1)
         if fused:
             self._seg(pnd + 2, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.weight", f64=1)
             self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.bias", f64=1)
-            self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(),
-                       cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S, st)
+            if tail_pre is None:
+                self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(),
+                           cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S, st)
             return pn, nb
         dy2 = self._empty(N, cout, S, device=dev)
         if shortcut:
@@ -641,9 +662,10 @@ class UNetEngine:
         if self.debug is not None and not self._dry:
             self.debug[pre + "#"] = {"dy2": dy2, "dr": drv, "dy1": dy1, "dx": dxv}
 
-    def _block_bwd(self, flat, pre, sv, dout, dxv, st, dev):
+    def _block_bwd(self, flat, pre, sv, dout, dxv, st, dev, tail_pre=None):
         """Backward of ResidualBlock.forward (unet3d.py:77-93).  Writes d(block input) into dxv
-        (overwrite) and records the block's weight-gradient reductions."""
+        (overwrite) and records the block's weight-gradient reductions.  tail_pre = (arena
+        offset, blocks per plane): the tail reduce partials were written by dout's producer."""
         if self.kinds[pre][0][0] != "ds":
             return self._block_bwd_g(flat, pre, sv, dout, dxv, st, dev)
         A = self.bwd_arena
@@ -661,11 +683,13 @@ class UNetEngine:
         y2, z2, y1, z1 = sv["y2"], sv["z2"], sv["y1"], sv["z1"]
         # (1) block tail: out = lrelu(IN2(y2) + residual)
         fused = self._tail_fusable(sv, cin, cout, S)
+        assert tail_pre is None or fused
         dz2 = e(N, cout, S)
         if fused:
             # (1+2) the tail reduce, then conv2.pointwise backward with the tail's apply in its
             # prologue (dy2 is never written)
-            pn, ntp = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev, fused=True)
+            pn, ntp = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev, fused=True,
+                                     tail_pre=tail_pre)
             self._pw_bwd_tail(flat, dout, sv["out"], V(y2, 0, cout * S, cout), rec2, pn, ntp, 1,
                               V(z2, 0, cout * S, cout), pre + "conv2.pointwise.weight",
                               V(dz2, 0, cout * S, cout), 0, N, S, st)

@@ -939,3 +939,41 @@ def test_pw_bwd_tail_equals_apply_then_pw_bwd(cuda, shape):
             outs.append((dx, pp.view(npw, J * K_).double().sum(0)))
         close(outs[1][0], outs[0][0], 1e-5, f"dx sel{sel} {shape}")
         close(outs[1][1], outs[0][1], 1e-5, f"dW sel{sel} {shape}")
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 48 ** 3), (2, 8, 1000), (1, 16, 7 * 9 * 12)])
+def test_outconv_bwd_tail_equals_outconv_bwd_then_reduce(cuda, shape):
+    """l3u_outconv_bwd_tail == l3u_outconv_bwd (dh, weight partials: bitwise) followed by
+    l3u_norm_act_bwd_reduce on dh (per-channel sums, to fp rounding: other block sizes)."""
+    N, C, S = shape
+    gen = torch.Generator().manual_seed(44)
+    t = lambda *s: torch.randn(*s, generator=gen).to(cuda)  # noqa: E731
+    dp, p = t(N, S), torch.rand(N, S, generator=gen).to(cuda)
+    h, y2, r = t(N, C, S), t(N, C, S), t(N, C, S)
+    w = t(C)
+    rec2 = make_rec(N, C, gen).float().to(cuda)
+    recr = make_rec(N, C, gen).float().to(cuda)
+    nb = nat().query("l3u_outconv_nblocks", S)
+    outs = []
+    for tail in (False, True):
+        dh = torch.empty(N, C, S, device=cuda)
+        po = torch.empty(N * nb * (C + 1), dtype=torch.float64, device=cuda)
+        tp = torch.empty(C * N * nb * 3, dtype=torch.float64, device=cuda)
+        a = (dp.data_ptr(), p.data_ptr(), None, None, 0.7, 0.3, 0.75, 1e-6, None, h.data_ptr(), C * S,
+             w.data_ptr(), dh.data_ptr(), C * S, po.data_ptr(), None)
+        if tail:
+            nat().call("l3u_outconv_bwd_tail", *a, y2.data_ptr(), C * S, rec2.data_ptr(), r.data_ptr(),
+                       C * S, recr.data_ptr(), tp.data_ptr(), N, C, S, st())
+            sums = tp.view(C, N, nb, 3).sum(2)
+        else:
+            nat().call("l3u_outconv_bwd", *a, N, C, S, st())
+            nr = nat().query("l3u_norm_act_nblocks", S)
+            rp = torch.empty(C * N * nr * 3, dtype=torch.float64, device=cuda)
+            nat().call("l3u_norm_act_bwd_reduce", dh.data_ptr(), C * S, h.data_ptr(), C * S,
+                       y2.data_ptr(), C * S, rec2.data_ptr(), r.data_ptr(), C * S, recr.data_ptr(),
+                       rp.data_ptr(), N, C, S, st())
+            sums = rp.view(C, N, nr, 3).sum(2)
+        torch.cuda.synchronize()
+        outs.append((dh, po, sums))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    close(outs[1][2], outs[0][2], 1e-6, "tail sums")
