@@ -271,6 +271,16 @@ int l3u_adamw(float* p, const float* g, float* m, float* v, long long numel, con
               float beta1, float beta2, float eps, float weight_decay, int* step, float grad_scale,
               hipStream_t stream);
 
+/* ---- the first block's front (in_channels = 1, unet3d.py:163-167) --------------------------
+ * one launch for the Conv1x1 shortcut r[c] = wr[c]*x, conv1.depthwise z1 = dw3(x) (one channel,
+ * w_dw [27]) and conv1.pointwise y1[c] = w1[c]*z1, with the (count, mean, M2) partials of r and y1
+ * ([N][C][l3u_front_nblocks(S)][3], the l3u_pw_fwd format) from the channel's own moments.
+ * Replaces three launches of unet3d.py:70-73,16-18 for the init_conv block.  W % 4 == 0.       */
+int l3u_front_nblocks(int S);
+int l3u_front_fwd(const float* x, long long x_nstride, const float* w_dw, const float* w1,
+                  const float* wr, float* z1, float* y1, float* r, float* stat1, float* statr,
+                  int N, int C, int D, int H, int W, hipStream_t stream);
+
 /* ---- grouped / dense 3x3x3 conv (stride 1, padding 1, no bias): the
  * use_depthwise_separable=False path of ResidualBlock (GroupedConv3d unet3d.py:26-34, chosen at
  * :46-47 / :57-58; nn.Conv3d unet3d.py:49 / :60, G = 1).  w: torch weight [Cout][Cin/G][3][3][3].

@@ -539,6 +539,72 @@ int grid_for(long long n, int per_block, int cap) {
   return b < 1 ? 1 : (int)b;
 }
 
+// ---------------------------------------------------------------- first block front (Cin = 1)
+// The first ResidualBlock of the network has ONE input channel (unet3d.py:163-167), so its
+// Conv1x1 shortcut and conv1.pointwise are rank-1 "GEMMs": r[c] = wr[c] * x and y1[c] = w1[c] * z1
+// with z1 = depthwise3(x) (conv1.depthwise, one channel).  One launch reads x once, writes z1
+// (kept for the backward) and both C-channel tensors, and emits their InstanceNorm statistics
+// partials, derived from the block's single-channel moments: a channel's (count, mean, M2) over
+// the workgroup's voxels is (count, w*mean, w^2*M2) of the input channel, exactly.
+// One workgroup per 1024 voxels (a float4 quad per thread) of one sample.
+__global__ __launch_bounds__(256) void front_fwd_kernel(
+    const float* __restrict__ x, long long xns, const float* __restrict__ wdw,
+    const float* __restrict__ w1, const float* __restrict__ wr, float* __restrict__ z1,
+    float* __restrict__ y1, float* __restrict__ r, float* __restrict__ stat1,
+    float* __restrict__ statr, int C, int D, int H, int W) {
+  __shared__ float red[4];
+  const int S = D * H * W, nb = gridDim.x, b = blockIdx.x, n = blockIdx.y;
+  const int i0 = (b * 256 + threadIdx.x) * 4;
+  const bool act = i0 < S;
+  const float* xp = x + (long long)n * xns;
+  f4 xv = {0.f, 0.f, 0.f, 0.f}, zv = {0.f, 0.f, 0.f, 0.f};
+  if (act) {
+    xv = *reinterpret_cast<const f4*>(xp + i0);
+    const int xx = i0 % W, t1 = i0 / W, yy = t1 % H, zz = t1 / H;   // quad: xx .. xx+3, one row
+#pragma unroll
+    for (int dz = -1; dz <= 1; ++dz) {
+      if (zz + dz < 0 || zz + dz >= D) continue;
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy) {
+        if (yy + dy < 0 || yy + dy >= H) continue;
+        const float* row = xp + ((long long)(zz + dz) * H + (yy + dy)) * W;
+        const f4 m = *reinterpret_cast<const f4*>(row + xx);
+        const float lft = xx > 0 ? row[xx - 1] : 0.f, rgt = xx + 4 < W ? row[xx + 4] : 0.f;
+        const float v[6] = {lft, m[0], m[1], m[2], m[3], rgt};
+        const float* wk = wdw + ((dz + 1) * 3 + (dy + 1)) * 3;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          zv[q] = fmaf(wk[0], v[q], fmaf(wk[1], v[q + 1], fmaf(wk[2], v[q + 2], zv[q])));
+      }
+    }
+    *reinterpret_cast<f4*>(z1 + (long long)n * S + i0) = zv;
+    for (int c = 0; c < C; ++c) {
+      *reinterpret_cast<f4*>(r + ((long long)n * C + c) * S + i0) = wr[c] * xv;
+      *reinterpret_cast<f4*>(y1 + ((long long)n * C + c) * S + i0) = w1[c] * zv;
+    }
+  }
+  // the workgroup's moments of x and z1 (fixed-order sums: deterministic)
+  const int cnt = min(1024, S - b * 1024);
+  const float sx = block_sum256(act ? (xv[0] + xv[1]) + (xv[2] + xv[3]) : 0.f, red);
+  const float sz = block_sum256(act ? (zv[0] + zv[1]) + (zv[2] + zv[3]) : 0.f, red);
+  const float mx = sx / (float)cnt, mz = sz / (float)cnt;
+  float qx = 0.f, qz = 0.f;
+  if (act) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      qx = fmaf(xv[q] - mx, xv[q] - mx, qx);
+      qz = fmaf(zv[q] - mz, zv[q] - mz, qz);
+    }
+  }
+  const float m2x = block_sum256(qx, red), m2z = block_sum256(qz, red);
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float* o1 = stat1 + (((long long)n * C + c) * nb + b) * 3;
+    float* orr = statr + (((long long)n * C + c) * nb + b) * 3;
+    o1[0] = (float)cnt; o1[1] = w1[c] * mz; o1[2] = w1[c] * w1[c] * m2z;
+    orr[0] = (float)cnt; orr[1] = wr[c] * mx; orr[2] = wr[c] * wr[c] * m2x;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -686,6 +752,21 @@ int l3u_adamw(float* p, const float* g, float* m, float* v, long long numel, con
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(numel, 1024, 1024)), dim3(256), 0, stream, p, g, m,
                      v, numel, lr, beta1, beta2, eps, weight_decay, step, grad_scale);
   hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, stream, step);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_front_nblocks(int S) { return (S + 1023) / 1024; }
+
+int l3u_front_fwd(const float* x, long long x_nstride, const float* w_dw, const float* w1,
+                  const float* wr, float* z1, float* y1, float* r, float* stat1, float* statr,
+                  int N, int C, int D, int H, int W, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && C > 0 && D > 0 && H > 0 && W > 0 && W % 4 == 0 && x_nstride % 4 == 0);
+  L3U_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)z1 & 15) == 0 && ((uintptr_t)y1 & 15) == 0 &&
+              ((uintptr_t)r & 15) == 0);
+  const int S = D * H * W;
+  dim3 grid(l3u_front_nblocks(S), N);
+  hipLaunchKernelGGL(front_fwd_kernel, grid, dim3(256), 0, stream, x, x_nstride, w_dw, w1, wr, z1,
+                     y1, r, stat1, statr, C, D, H, W);
   L3U_CHECK_LAUNCH();
 }
 

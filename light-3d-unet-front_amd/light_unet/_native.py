@@ -63,6 +63,8 @@ _SIGS = {
     "l3u_ftl_bwd": [P, P, L, P, D, D, D, D, P, I, P, P],
     "l3u_adamw": [P, P, P, P, L, P, F, F, F, F, P, F, P],
     "l3u_reduce_segments": [P, P, I, P, P],
+    "l3u_front_nblocks": [I],
+    "l3u_front_fwd": [P, L, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "l3u_outconv_bwd_tail": [P, P, P, P, D, D, D, D, P, P, L, P, P, L, P, P, P, L, P, P, L, P, P,
                              I, I, I, P],
     "l3u_pw_bwd_tail": [P, L, P, L, P, L, P, P, I, I, P, L, P, P, L, I, P, I, I, I, I, P],
@@ -78,7 +80,7 @@ _SIGS = {
 _QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_weight_nparts",
             "l3u_pw_bwd_supported", "l3u_pw_bwd_nparts", "l3u_convt_bwd_fused_nparts",
             "l3u_norm_act_nblocks", "l3u_chan_sum_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks",
-            "l3u_gconv3_nblocks", "l3u_gconv3_wgrad_nparts"}
+            "l3u_gconv3_nblocks", "l3u_gconv3_wgrad_nparts", "l3u_front_nblocks"}
 
 _lib = None
 

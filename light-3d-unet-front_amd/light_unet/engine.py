@@ -22,6 +22,8 @@ import torch
 from . import _native as nat
 
 F32 = 4
+# the one-input-channel first block's front in one launch (l3u_front_fwd); L3U_FRONT=0 disables
+_FRONT = os.environ.get("L3U_FRONT", "1") != "0"
 # outputs per reduction item by partial-list length (<= 128, <= 384, longer); measured best of
 # 32..256 on the 48^3 step (tools/seg_caps.sh); L3U_SEG_CAPS overrides
 # block-tail backward inside the pointwise backwards (l3u_pw_bwd_tail); L3U_TAIL_FUSE=0 disables
@@ -328,25 +330,44 @@ class UNetEngine:
         # InstanceNorm records are finalized inside their consumer kernels from the GEMM
         # partials (l3u_norm_src); `recs` receives them for the backward pass.
         src_r = src2 = None
-        if shortcut:
-            r = e(N, cout, S)
-            so = self.fwd_arena.alloc(N * cout * nsb * 3)
-            self._call("l3u_pw_fwd", x.p, x.ns, self._w(flat, pre + "shortcut.0.weight"), 0, None,
-                       r.data_ptr(), cout * S, 0, self.fwd_arena.ptr(so), N, cin, cout, S, st)
-            src_r = self._src(flat, pre + "shortcut.1.", so, nsb, rec_r, 0.0, cptr, 0)
+        if _FRONT and shortcut and cin == 1 and w % 4 == 0 and x.ns % 4 == 0:
+            # the one-input-channel block: shortcut, conv1.depthwise and conv1.pointwise (both
+            # rank-1 channel maps) and their IN statistics in one launch
+            nbf = nat.query("l3u_front_nblocks", S)
+            r, z1, y1 = e(N, cout, S), e(N, cin, S), e(N, cout, S)
+            so = self.fwd_arena.alloc(N * cout * nbf * 3)
+            s1 = self.fwd_arena.alloc(N * cout * nbf * 3)
+            self._call("l3u_front_fwd", x.p, x.ns, self._w(flat, pre + "conv1.depthwise.weight"),
+                       self._w(flat, pre + "conv1.pointwise.weight"),
+                       self._w(flat, pre + "shortcut.0.weight"), z1.data_ptr(), y1.data_ptr(),
+                       r.data_ptr(), self.fwd_arena.ptr(s1), self.fwd_arena.ptr(so), N, cout, d, h,
+                       w, st)
+            src_r = self._src(flat, pre + "shortcut.1.", so, nbf, rec_r, 0.0, cptr, 0)
             rv = V(r, 0, cout * S, cout)
             sv["r"] = rv
+            src1 = self._src(flat, pre + "norm1.", s1, nbf, rec1, drop, cptr, 1 + layer)
         else:
-            rv = x
-            sv["r"] = None
-        z1 = e(N, cin, S)
-        self._call("l3u_dw3_fwd", x.p, x.ns, self._w(flat, pre + "conv1.depthwise.weight"), None,
-                   None, z1.data_ptr(), cin * S, N, cin, d, h, w, st)
-        y1 = e(N, cout, S)
-        s1 = self.fwd_arena.alloc(N * cout * nsb * 3)
-        self._call("l3u_pw_fwd", z1.data_ptr(), cin * S, self._w(flat, pre + "conv1.pointwise.weight"),
-                   0, None, y1.data_ptr(), cout * S, 0, self.fwd_arena.ptr(s1), N, cin, cout, S, st)
-        src1 = self._src(flat, pre + "norm1.", s1, nsb, rec1, drop, cptr, 1 + layer)
+            if shortcut:
+                r = e(N, cout, S)
+                so = self.fwd_arena.alloc(N * cout * nsb * 3)
+                self._call("l3u_pw_fwd", x.p, x.ns, self._w(flat, pre + "shortcut.0.weight"), 0,
+                           None, r.data_ptr(), cout * S, 0, self.fwd_arena.ptr(so), N, cin, cout, S,
+                           st)
+                src_r = self._src(flat, pre + "shortcut.1.", so, nsb, rec_r, 0.0, cptr, 0)
+                rv = V(r, 0, cout * S, cout)
+                sv["r"] = rv
+            else:
+                rv = x
+                sv["r"] = None
+            z1 = e(N, cin, S)
+            self._call("l3u_dw3_fwd", x.p, x.ns, self._w(flat, pre + "conv1.depthwise.weight"), None,
+                       None, z1.data_ptr(), cin * S, N, cin, d, h, w, st)
+            y1 = e(N, cout, S)
+            s1 = self.fwd_arena.alloc(N * cout * nsb * 3)
+            self._call("l3u_pw_fwd", z1.data_ptr(), cin * S,
+                       self._w(flat, pre + "conv1.pointwise.weight"), 0, None, y1.data_ptr(),
+                       cout * S, 0, self.fwd_arena.ptr(s1), N, cin, cout, S, st)
+            src1 = self._src(flat, pre + "norm1.", s1, nsb, rec1, drop, cptr, 1 + layer)
         z2 = e(N, cout, S)
         self._call("l3u_dw3_fwd", y1.data_ptr(), cout * S, self._w(flat, pre + "conv2.depthwise.weight"),
                    None, nat.norm_src_ptr(src1), z2.data_ptr(), cout * S, N, cout, d, h, w, st)

@@ -977,3 +977,44 @@ def test_outconv_bwd_tail_equals_outconv_bwd_then_reduce(cuda, shape):
         outs.append((dh, po, sums))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     close(outs[1][2], outs[0][2], 1e-6, "tail sums")
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 48, 48, 48), (2, 8, 5, 6, 8), (1, 16, 7, 3, 12)])
+def test_front_fwd(cuda, shape):
+    """l3u_front_fwd (first block, one input channel): shortcut r = wr*x, z1 = depthwise3(x),
+    y1 = w1*z1 and their (count, mean, M2) partials vs fp64 torch."""
+    N, C, D, H, W = shape
+    S = D * H * W
+    gen = torch.Generator().manual_seed(45)
+    x = torch.randn(N, 1, D, H, W, generator=gen, dtype=torch.float64)
+    wdw = torch.randn(1, 1, 3, 3, 3, generator=gen, dtype=torch.float64)
+    w1 = torch.randn(C, generator=gen, dtype=torch.float64)
+    wr = torch.randn(C, generator=gen, dtype=torch.float64)
+    z1 = F.conv3d(x, wdw, padding=1).reshape(N, 1, S)
+    y1 = w1[None, :, None] * z1
+    r = wr[None, :, None] * x.reshape(N, 1, S)
+    nb = nat().query("l3u_front_nblocks", S)
+    dev = [t.float().to(cuda).contiguous() for t in (x, wdw, w1, wr)]
+    z1d = torch.empty(N, 1, S, device=cuda)
+    y1d = torch.empty(N, C, S, device=cuda)
+    rd = torch.empty(N, C, S, device=cuda)
+    s1 = torch.empty(N * C * nb * 3, device=cuda)
+    sr = torch.empty(N * C * nb * 3, device=cuda)
+    nat().call("l3u_front_fwd", dev[0].data_ptr(), S, dev[1].data_ptr(), dev[2].data_ptr(),
+               dev[3].data_ptr(), z1d.data_ptr(), y1d.data_ptr(), rd.data_ptr(), s1.data_ptr(),
+               sr.data_ptr(), N, C, D, H, W, st())
+    torch.cuda.synchronize()
+    close(z1d, z1, 1e-6, "z1")
+    close(y1d, y1, 1e-6, "y1")
+    close(rd, r, 1e-6, "r")
+    for part, ref in ((s1, y1), (sr, r)):
+        p = part.view(N, C, nb, 3).double().cpu()
+        pad = torch.full((N, C, nb * 1024 - S), float("nan"), dtype=torch.float64)
+        blocks = torch.cat([ref, pad], 2).view(N, C, nb, 1024)
+        valid = ~torch.isnan(blocks)
+        cnt = valid.sum(-1).double()
+        mean = torch.where(valid, blocks, 0.0).sum(-1) / cnt
+        m2 = torch.where(valid, (blocks - mean[..., None]) ** 2, 0.0).sum(-1)
+        assert torch.equal(p[..., 0], cnt)
+        close(p[..., 1], mean, 1e-5, "block mean")
+        close(p[..., 2], m2, 1e-5, "block M2")
