@@ -305,6 +305,13 @@ int l3u_gconv3_bwd_weight(const float* dy, long long dy_nstride, const float* x,
                           long long x_nstride, const float* rec, float* part, int N, int Cin,
                           int Cout, int G, int D, int H, int W, hipStream_t stream);
 
+/* the same AdamW update in ONE launch: the last workgroup to finish (ticket order; *ticket
+ * starts at 0 and is reset) advances *step and, when counter2 != NULL, *counter2 (the model's
+ * Dropout3d stream counter, so a captured training step needs no separate counter launches)  */
+int l3u_adamw_tick(float* p, const float* g, float* m, float* v, long long numel, const float* lr,
+                   float beta1, float beta2, float eps, float weight_decay, int* step,
+                   float grad_scale, int* ticket, int* counter2, hipStream_t stream);
+
 /* ---- deterministic second-stage reduction --------------------------------------------------
  * items[nitems][8] int64 = {src_off, count, istride, tstride, len<=256, dst_off, accumulate, f64}:
  * dst[dst_off+t] (+)= sum_{i<count} src[src_off + i*istride + t*tstride], summed in fp64;

@@ -398,6 +398,41 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   }
 }
 
+// The same update with the step counter(s) advanced by the LAST workgroup to finish (ticket
+// order): every workgroup has read *step by the time it takes its ticket, so the increment
+// cannot race a read, and the separate one-thread launch disappears.  The ticket is reset.
+__global__ __launch_bounds__(256) void adamw_tick_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v,
+                                                         long long numel, const float* __restrict__ lr,
+                                                         float beta1, float beta2, float eps, float wd,
+                                                         int* step, float gscale, int* ticket,
+                                                         int* counter2) {
+  const float lrv = lr[0];
+  const int t = step[0] + 1;
+  const float bc1 = 1.f - powf(beta1, (float)t);
+  const float bc2s = sqrtf(1.f - powf(beta2, (float)t));
+  const float step_size = lrv / bc1;
+  const float decay = 1.f - lrv * wd;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < numel; i += (long long)gridDim.x * 256) {
+    const float gv = g[i] * gscale;
+    float pv = p[i] * decay;
+    float mv = m[i];
+    mv = mv + (1.f - beta1) * (gv - mv);                 // exp_avg.lerp_(grad, 1 - beta1)
+    const float vv = v[i] * beta2 + (1.f - beta2) * gv * gv;
+    const float denom = sqrtf(vv) / bc2s + eps;
+    pv = pv - step_size * (mv / denom);
+    p[i] = pv;
+    m[i] = mv;
+    v[i] = vv;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(ticket, 1) == (int)gridDim.x - 1) {
+    step[0] = t;
+    if (counter2) counter2[0] += 1;
+    ticket[0] = 0;
+  }
+}
+
 __global__ void step_inc_kernel(int* step) { step[0] += 1; }
 __global__ void counter_add_kernel(int* c, int v) { c[0] += v; }
 
@@ -767,6 +802,16 @@ int l3u_front_fwd(const float* x, long long x_nstride, const float* w_dw, const 
   dim3 grid(l3u_front_nblocks(S), N);
   hipLaunchKernelGGL(front_fwd_kernel, grid, dim3(256), 0, stream, x, x_nstride, w_dw, w1, wr, z1,
                      y1, r, stat1, statr, C, D, H, W);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_adamw_tick(float* p, const float* g, float* m, float* v, long long numel, const float* lr,
+                   float beta1, float beta2, float eps, float weight_decay, int* step,
+                   float grad_scale, int* ticket, int* counter2, hipStream_t stream) {
+  L3U_REQUIRE(numel > 0 && step && ticket);
+  hipLaunchKernelGGL(adamw_tick_kernel, dim3(grid_for(numel, 1024, 1024)), dim3(256), 0, stream, p, g,
+                     m, v, numel, lr, beta1, beta2, eps, weight_decay, step, grad_scale, ticket,
+                     counter2);
   L3U_CHECK_LAUNCH();
 }
 

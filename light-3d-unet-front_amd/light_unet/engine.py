@@ -204,7 +204,7 @@ class UNetEngine:
 
     # ------------------------------------------------------------------ forward
     def forward(self, flat, x, training=False, dropout_p=0.0, counter=None, save=True, target=None,
-                ftl_part=None):
+                ftl_part=None, bump_counter=True):
         """x: [N,1,D,H,W] fp32 on device -> probabilities [N,1,D,H,W] (+ saved state).  With a
         target (same shape) the out_conv launch also writes the FocalTversky partials into
         ftl_part [N * l3u_outconv_nblocks(S)][3]."""
@@ -217,16 +217,18 @@ class UNetEngine:
             self._dry = True
             self.fwd_arena.reset(None)
             try:
-                self._forward_impl(flat, x, training, dropout_p, counter, save, dev, target, ftl_part)
+                self._forward_impl(flat, x, training, dropout_p, counter, save, dev, target, ftl_part,
+                                   bump_counter)
             finally:
                 self._dry = False
             self._arenas[key] = torch.empty(max(self.fwd_arena.top, 64), dtype=torch.float32,
                                             device=dev)
         self.fwd_arena.reset(self._arenas[key])
-        return self._forward_impl(flat, x, training, dropout_p, counter, save, dev, target, ftl_part)
+        return self._forward_impl(flat, x, training, dropout_p, counter, save, dev, target, ftl_part,
+                                  bump_counter)
 
     def _forward_impl(self, flat, x, training, dropout_p, counter, save, dev, target=None,
-                      ftl_part=None):
+                      ftl_part=None, bump_counter=True):
         N, _, D, H, W = x.shape
         c0, c1, c2, c3 = self.enc
         dims = [(D >> k, H >> k, W >> k) for k in range(4)]
@@ -235,7 +237,7 @@ class UNetEngine:
         drop = dropout_p if training else 0.0
         st = nat.stream()
         sv = {"N": N, "dims": dims, "S": S, "x": x, "drop": drop}
-        if drop > 0.0 and counter is not None:
+        if drop > 0.0 and counter is not None and bump_counter:
             self._call("l3u_counter_add", counter.data_ptr(), 1, st)
         cptr = counter.data_ptr() if counter is not None else None
         # concatenation buffers [up | skip]

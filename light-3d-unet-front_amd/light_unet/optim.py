@@ -15,7 +15,9 @@ from . import _native as nat
 
 class FlatAdamW:
     def __init__(self, flat_params, flat_grads, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=1e-2, grad_scale=1.0):
+                 weight_decay=1e-2, grad_scale=1.0, tick_counter=None):
+        """tick_counter: an int32 device counter (the model's Dropout3d stream counter) that the
+        update launch advances together with its own step count (l3u_adamw_tick: one launch)."""
         nat.require_device(flat_params, flat_grads)
         if flat_params.shape != flat_grads.shape or flat_params.dtype != torch.float32:
             raise ValueError("flat params/grads must be matching fp32 buffers")
@@ -28,12 +30,16 @@ class FlatAdamW:
         self.eps = float(eps)
         self.wd = float(weight_decay)
         self.grad_scale = float(grad_scale)
+        self.tick_counter = tick_counter
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=flat_params.device)
 
     def set_lr(self, lr):
         self.lr_t.fill_(float(lr))
 
     def step(self):
-        nat.call("l3u_adamw", self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(),
+        nat.call("l3u_adamw_tick", self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(),
                  self.v.data_ptr(), self.p.numel(), self.lr_t.data_ptr(), self.betas[0],
                  self.betas[1], self.eps, self.wd, self.step_t.data_ptr(), self.grad_scale,
+                 self.ticket.data_ptr(),
+                 self.tick_counter.data_ptr() if self.tick_counter is not None else None,
                  nat.stream())

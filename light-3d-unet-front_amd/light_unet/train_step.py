@@ -34,8 +34,9 @@ class TrainStep:
         self.engine = model.engine
         self.flat = model.flat_parameters()
         self.gflat = torch.zeros_like(self.flat)
+        # the update launch also advances the Dropout3d counter (no counter launch per step)
         self.opt = FlatAdamW(self.flat, self.gflat, lr=lr, betas=betas, eps=eps,
-                             weight_decay=weight_decay)
+                             weight_decay=weight_decay, tick_counter=model._rng_counter)
         self.group = group
         # distributed=False: a rank-local step (no exchange) even inside a process group
         self.world = world_size(group) if distributed else 1
@@ -52,7 +53,8 @@ class TrainStep:
         part = torch.empty(nparts * 3, dtype=torch.float32, device=x.device)
         p, sv = self.engine.forward(self.flat, x, training=self.model.training,
                                     dropout_p=self.model.dropout_p,
-                                    counter=self.model._rng_counter, save=True, target=t,
+                                    counter=self.model._rng_counter, bump_counter=False,
+                                    save=True, target=t,
                                     ftl_part=part)
         sums = torch.empty(3, dtype=torch.float64, device=p.device)
         nat.call("l3u_ftl_reduce", part.data_ptr(), nparts, sums.data_ptr(), nat.stream())

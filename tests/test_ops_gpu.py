@@ -1018,3 +1018,28 @@ def test_front_fwd(cuda, shape):
         assert torch.equal(p[..., 0], cnt)
         close(p[..., 1], mean, 1e-5, "block mean")
         close(p[..., 2], m2, 1e-5, "block M2")
+
+
+def test_adamw_tick_equals_adamw(cuda):
+    """l3u_adamw_tick (one launch; the last workgroup advances the counters) == l3u_adamw +
+    its step increment, bitwise; the extra counter advances once per call, the ticket resets."""
+    gen = torch.Generator().manual_seed(12)
+    n = 217228
+    p0 = torch.randn(n, generator=gen).to(cuda)
+    pa, pb = p0.clone(), p0.clone()
+    ma, va, mb, vb = (torch.zeros(n, device=cuda) for _ in range(4))
+    sa = torch.zeros(1, dtype=torch.int32, device=cuda)
+    sb = torch.zeros(1, dtype=torch.int32, device=cuda)
+    ticket = torch.zeros(1, dtype=torch.int32, device=cuda)
+    ctr = torch.full((1,), 7, dtype=torch.int32, device=cuda)
+    lr = torch.tensor([1e-3], device=cuda)
+    for _ in range(5):
+        g = torch.randn(n, generator=gen).to(cuda)
+        nat().call("l3u_adamw", pa.data_ptr(), g.data_ptr(), ma.data_ptr(), va.data_ptr(), n,
+                   lr.data_ptr(), 0.9, 0.999, 1e-8, 1e-2, sa.data_ptr(), 1.0, st())
+        nat().call("l3u_adamw_tick", pb.data_ptr(), g.data_ptr(), mb.data_ptr(), vb.data_ptr(), n,
+                   lr.data_ptr(), 0.9, 0.999, 1e-8, 1e-2, sb.data_ptr(), 1.0, ticket.data_ptr(),
+                   ctr.data_ptr(), st())
+    torch.cuda.synchronize()
+    assert sa.item() == sb.item() == 5 and ctr.item() == 12 and ticket.item() == 0
+    assert torch.equal(pa, pb) and torch.equal(ma, mb) and torch.equal(va, vb)
