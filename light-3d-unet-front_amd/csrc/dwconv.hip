@@ -1324,6 +1324,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
 #define L3U_VOL_MAX 600   // measured: the 6^3 level gains, at 12^3 the plane kernels are faster
 #endif
 bool use_volume(int D, int H, int W) { return (long long)(D + 2) * (H + 2) * (W + 2) <= L3U_VOL_MAX; }
+#ifndef L3U_DWV_FUSED
+#define L3U_DWV_FUSED 1   // whole-volume backward as one launch (data + weight gradient)
+#endif
 
 // load volume `src` (transformed if XF) into the padded LDS image; the halo is zero
 template <bool XF>
@@ -1460,6 +1463,101 @@ __global__ __launch_bounds__(256) void dwv_dw_kernel(
   }
 }
 
+// Both backward halves of the whole-volume form in ONE launch (6^3 level, where each launch is
+// latency): the (n, c) volumes of dZ and of A (= x, or lrelu(IN(x)) in MODE 1) sit in LDS side
+// by side; each thread forms the flipped-tap data gradient of its voxels (MODE 1: the IN-fused
+// dpre epilogue and IN sums; 2: accumulate; 0: overwrite) and the 27 weight-gradient products.
+// Same per-voxel arithmetic as dwv_fwd_kernel<0, EPI> + dwv_dw_kernel<XF>.
+template <int MODE>
+__global__ __launch_bounds__(256) void dwv_bwd_kernel(
+    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
+    const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
+    long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part, int N, int C, int D,
+    int H, int W) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int nc = blockIdx.x, c = nc % C, n = nc / C;
+  const long long HW = (long long)H * W, S = D * HW, cofs = (long long)c * S;
+  const int PW = W + 2, PHW = (H + 2) * PW, PV = (D + 2) * PHW;
+  float wk[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t) wk[t] = w[c * 27 + 26 - t];
+  float sc = 1.f, sh = 0.f, mu = 0.f, rstd = 1.f, kk = 1.f;
+  if (MODE == 1) {
+    const float* r = rec + (long long)nc * kRec;
+    mu = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];
+  }
+  float* dzl = lds;
+  float* al = lds + PV;
+  v_load<false>(dzl, dz + (long long)n * dzns + cofs, D, H, W, 1.f, 0.f, 0.f);
+  v_load<MODE == 1>(al, x + (long long)n * xns + cofs, D, H, W, sc, mu, sh);
+  __syncthreads();
+  const float* xp = x + (long long)n * xns + cofs;
+  float* dxp = dx + (long long)n * dxns + cofs;
+  float gw[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t) gw[t] = 0.f;
+  float s1 = 0.f, s2 = 0.f;
+  for (int v = threadIdx.x; v < S; v += blockDim.x) {
+    const int xx = v % W, t1 = v / W, yy = t1 % H, zz = t1 / H;
+    const int corner = zz * PHW + yy * PW + xx;
+    const float* bz = dzl + corner;
+    const float* ba = al + corner;
+    float o = 0.f;
+#pragma unroll
+    for (int dzz = 0; dzz < 3; ++dzz)
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dxx = 0; dxx < 3; ++dxx)
+          o = fmaf(wk[dzz * 9 + dy * 3 + dxx], bz[dzz * PHW + dy * PW + dxx], o);
+    const float g = bz[PHW + PW + 1];   // dZ(v)
+#pragma unroll
+    for (int dzz = 0; dzz < 3; ++dzz)
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dxx = 0; dxx < 3; ++dxx) {
+          const int tp = dzz * 9 + dy * 3 + dxx;
+          gw[tp] = fmaf(g, ba[dzz * PHW + dy * PW + dxx], gw[tp]);
+        }
+    if (MODE == 1) {
+      const float e = xp[v];
+      const float pre = fmaf(sc, e - mu, sh);
+      o = o * kk * lrelu_d(pre);
+      s1 += o;
+      s2 += o * ((e - mu) * rstd);
+    } else if (MODE == 2) {
+      o += dxp[v];
+    }
+    dxp[v] = o;
+  }
+  __syncthreads();
+  float* red = lds;                                        // [4 waves][32]
+  double* redd = reinterpret_cast<double*>(lds + 4 * 32);  // [4 waves][2]
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int t = 0; t < 27; ++t) {
+    const float r = wave_sum(gw[t]);
+    if (ln == 0) red[wv * 32 + t] = r;
+  }
+  if (MODE == 1) {
+    const double r1 = wave_sum_d((double)s1), r2 = wave_sum_d((double)s2);
+    if (ln == 0) { redd[wv * 2] = r1; redd[wv * 2 + 1] = r2; }
+  }
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    float r = 0.f;
+    for (int k = 0; k < nw; ++k) r += red[k * 32 + threadIdx.x];
+    dw_part[((long long)c * N + n) * 27 + threadIdx.x] = r;
+  }
+  if (MODE == 1 && threadIdx.x >= 32 && threadIdx.x < 34) {
+    const int j = threadIdx.x - 32;
+    double r = 0.0;
+    for (int k = 0; k < nw; ++k) r += redd[k * 2 + j];
+    in_part[((long long)c * N + n) * 2 + j] = r;
+  }
+}
+
 }  // namespace
 
 #define DW_DISPATCH_P(KERNEL, MODE, ...)                                               \
@@ -1540,6 +1638,17 @@ int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long l
   if (use_volume(D, H, W)) {
     size_t lds = (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
     if (lds < 128 * sizeof(float)) lds = 128 * sizeof(float);
+    if (parts == 3 && L3U_DWV_FUSED) {   // both halves in one launch
+      size_t lds2 = 2 * (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
+      if (lds2 < 160 * sizeof(float)) lds2 = 160 * sizeof(float);
+#define DWVB(M_) hipLaunchKernelGGL((dwv_bwd_kernel<M_>), dim3(N * C), dim3(256), lds2, stream, dz, \
+      dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W)
+      if (rec) DWVB(1);
+      else if (accumulate) DWVB(2);
+      else DWVB(0);
+#undef DWVB
+      L3U_CHECK_LAUNCH();
+    }
     if (parts & 1) {
       const l3u_norm_src z{};
 #define DWVX(E_) hipLaunchKernelGGL((dwv_fwd_kernel<0, E_>), dim3(N * C), dim3(256), lds, stream, dz, \
