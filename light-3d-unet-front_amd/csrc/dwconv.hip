@@ -895,6 +895,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ?
 #ifndef L3U_DWP_PD
 #define L3U_DWP_PD 2
 #endif
+#ifndef L3U_DWP_NT
+#define L3U_DWP_NT 1   // non-temporal dX stores in the LDS-DMA backward (kbench [4,32,48^3] 36.4 -> 35.6 us; step neutral)
+#endif
 #ifndef L3U_DWP_PIN
 #define L3U_DWP_PIN 1
 #endif
@@ -1259,7 +1262,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
       } else if (MODE == 2) {
         o += epi;
       }
-      if (st) *reinterpret_cast<f4*>(dxp + (long long)zf * HW + qofs) = o;
+      if (st) {
+        f4* dst = reinterpret_cast<f4*>(dxp + (long long)zf * HW + qofs);
+        if (GL && L3U_DWP_NT) __builtin_nontemporal_store(o, dst);   // streamed out, not re-read
+        else *dst = o;
+      }
     }
 #if L3U_DWP_PIN
     // keep each step's accumulation inside the step (no sinking of FMAs past later barriers)
