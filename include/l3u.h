@@ -113,7 +113,9 @@ int l3u_pw_bwd_supported(int J, int K, int S);
  * (sel 2: yr = r, rec = rec_r) with the block tail's backward (l3u_norm_act_bwd_apply) formed on
  * the fly from dout, out, yr and the l3u_norm_act_bwd_reduce partials tail_part[J][N][npart][3]:
  * dY = rstd*gamma*(g - mean(g) - xhat*mean(g*xhat)), g = dout*lrelu'(out), never written.
- * Supported: l3u_pw_bwd_supported(J, K, S) with J <= 32 (the 48^3 / 24^3 levels).            */
+ * Supported: l3u_pw_bwd_supported(J, K, S) with J <= 32 (the 48^3 / 24^3 levels).
+ * Replaces the autograd backward of norm2 / relu2 / the residual add (unet3d.py:62-63,87-91)
+ * fused with that of conv2.pointwise (:18) or the shortcut (:70-73).                            */
 int l3u_pw_bwd_tail(const float* dout, long long dout_nstride, const float* out,
                     long long out_nstride, const float* yr, long long yr_nstride, const float* rec,
                     const double* tail_part, int npart, int sel, const float* x,
@@ -167,7 +169,7 @@ int l3u_norm_act_bwd_apply(const float* dout, long long dout_nstride, const floa
                            long long dy2_nstride, float* dr, long long dr_nstride, int N, int C,
                            int S, hipStream_t stream);
 /* reduce + apply as ONE launch when l3u_norm_act_nblocks(S) == 1 (one workgroup per plane: the
- * small levels); same part layout (nblocks = 1) and bit-identical results                        */
+ * small levels); same part layout (nblocks = 1) and bit-identical results (unet3d.py:87-91)      */
 int l3u_norm_act_bwd(const float* dout, long long dout_nstride, const float* out,
                      long long out_nstride, const float* y2, long long y2_nstride,
                      const float* rec2, const float* r, long long r_nstride, const float* rec_r,
@@ -246,7 +248,6 @@ int l3u_outconv_bwd(const float* dp, const float* p, const float* t, const doubl
 int l3u_ftl_nblocks(long long numel);
 int l3u_ftl_sums(const float* p, const float* t, long long numel, float* part, double* sums,
                  hipStream_t stream);
-/* second stage only (partials from l3u_outconv_fwd): sums[3] = fixed-order sum of part[nparts][3] */
 /* l3u_outconv_bwd that also writes the first stage of the last decoder block's tail backward
  * (l3u_norm_act_bwd_reduce of up3.res_block, whose output is h): tail_part[C][N][nb][3] =
  * {sum g, sum g*xhat2, sum g*xhat_r}, g = dh*lrelu'(h), nb = l3u_outconv_nblocks(S); for the
@@ -258,6 +259,7 @@ int l3u_outconv_bwd_tail(const float* dp, const float* p, const float* t, const 
                          const float* y2, long long y2_nstride, const float* rec2, const float* r,
                          long long r_nstride, const float* rec_r, double* tail_part, int N, int C,
                          int S, hipStream_t stream);
+/* second stage only (partials from l3u_outconv_fwd): sums[3] = fixed-order sum of part[nparts][3] */
 int l3u_ftl_reduce(const float* part, int nparts, double* sums, hipStream_t stream);
 int l3u_ftl_loss(const double* sums, double alpha, double beta, double gamma, double smooth,
                  float* loss, hipStream_t stream);
@@ -305,9 +307,10 @@ int l3u_gconv3_bwd_weight(const float* dy, long long dy_nstride, const float* x,
                           long long x_nstride, const float* rec, float* part, int N, int Cin,
                           int Cout, int G, int D, int H, int W, hipStream_t stream);
 
-/* the same AdamW update in ONE launch: the last workgroup to finish (ticket order; *ticket
- * starts at 0 and is reset) advances *step and, when counter2 != NULL, *counter2 (the model's
- * Dropout3d stream counter, so a captured training step needs no separate counter launches)  */
+/* the same AdamW update (torch.optim.AdamW, trainer.py:75-79) in ONE launch: the last workgroup
+ * to finish (ticket order; *ticket starts at 0 and is reset) advances *step and, when
+ * counter2 != NULL, *counter2 (the model's Dropout3d stream counter, unet3d.py:66, so a
+ * captured training step needs no separate counter launches)                                   */
 int l3u_adamw_tick(float* p, const float* g, float* m, float* v, long long numel, const float* lr,
                    float beta1, float beta2, float eps, float weight_decay, int* step,
                    float grad_scale, int* ticket, int* counter2, hipStream_t stream);
