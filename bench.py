@@ -129,6 +129,39 @@ class KernelTimer:
         return e0.elapsed_time(e1) / reps
 
 
+def dw_bwd_cache_exceeding(device, N=8, C=32, L=48, reps=30):
+    """The dominant call's kernel (single-pass depthwise backward, mode 0) at a batch whose
+    working set (dZ + X + dX = 340 MB at [8, 32, 48^3]) exceeds the 256 MB MALL, as SURVEY §8d
+    asks: HIP events around back-to-back launches on the launch stream."""
+    from light_unet import _native as nat
+    S = L ** 3
+    g = torch.Generator(device=device).manual_seed(3)
+    dz = torch.randn(N, C, S, device=device, generator=g)
+    x = torch.randn(N, C, S, device=device, generator=g)
+    dx = torch.empty(N, C, S, device=device)
+    w = torch.randn(C, 27, device=device, generator=g)
+    nch = nat.query("l3u_dw3_nchunk", N, C, L, L, L)
+    part = torch.empty(C * N * nch * 27, device=device)
+    st = torch.cuda.current_stream()
+
+    def call():
+        nat.call("l3u_dw3_bwd", dz.data_ptr(), C * S, x.data_ptr(), C * S, w.data_ptr(), None,
+                 dx.data_ptr(), C * S, 0, part.data_ptr(), None, N, C, L, L, L, st.cuda_stream)
+    for _ in range(3):
+        call()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        call()
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    b = dw_bytes(N, C, S)
+    return {"call": f"l3u_dw3_bwd [{N},{C},{L}^3]", "working_set_MB": round(3 * 4 * N * C * S / 1e6, 1),
+            "algorithmic_bytes": b, "avg_launch_ms": round(ms, 5),
+            "achieved": round(b / (ms * 1e-3) / 1e9, 1), "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def cpu_baseline(args, enc):
     """The oracle (torch-CPU restatement of the same network, fp32) on the host cores."""
     from oracle import unet_oracle as U
@@ -443,6 +476,7 @@ def main():
                 "traffic_source": traffic_src,
                 "algorithmic_bytes": dbytes,
                 "avg_launch_ms": round(dom_ms, 5) if dom_ms else None,
+                "cache_exceeding": dw_bwd_cache_exceeding(device),
             },
         }
         if world == 1 and not args.no_cpu_baseline:
