@@ -111,6 +111,8 @@ class KernelTimer:
         return orig
 
     def mean_ms(self, nat_call, reps=50):
+        """Mean over `reps` back-to-back calls between two HIP events on the launch stream (one
+        continuous batch: syncs between shorter batches let the clocks drop and read ~15% slow)."""
         if set(self.args) != set(self.names):
             return None
         s = torch.cuda.current_stream()
