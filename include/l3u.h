@@ -92,6 +92,14 @@ int l3u_pw_stat_nsb(int K, int Nout, int S);
 int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout,
                const float* bias, float* y, long long y_nstride, int accumulate,
                float* stat_part, int N, int K, int Nout, int S, hipStream_t stream);
+/* two independent 1x1 convs of the same shape (no bias, no accumulate, w [Nout][K]) in ONE launch
+ * (a ResidualBlock's Conv1x1 shortcut, unet3d.py:70-73, and its conv1.pointwise, :18: both
+ * K = Cin -> Nout = Cout over the same volume); statistics partials as l3u_pw_fwd, both or none.
+ * S and every batch stride % 4 == 0.                                                           */
+int l3u_pw_fwd2(const float* xa, long long xa_nstride, const float* wa, float* ya,
+                long long ya_nstride, float* stat_a, const float* xb, long long xb_nstride,
+                const float* wb, float* yb, long long yb_nstride, float* stat_b, int N, int K,
+                int Nout, int S, hipStream_t stream);
 /* weight gradient partials: part[N*nsc][J][K] = sum_s dY[n][j][s] X[n][k][s] per voxel chunk   */
 int l3u_pw_bwd_weight_nparts(int N, int S);
 int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, long long x_nstride,

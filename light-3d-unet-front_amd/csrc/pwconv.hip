@@ -106,14 +106,21 @@ template <int NC, int NSW, bool VEC, int XM, int KS>   // XM: 0 plain, 1 scatter
 __global__ __launch_bounds__(256) void pw_fwd_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
     const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
-    float* __restrict__ stat_part, int K, int Nout, int S, int nsb, int Dq, int Hq, int Wq) {
+    float* __restrict__ stat_part, int K, int Nout, int S, int nsb, int Dq, int Hq, int Wq,
+    const float* __restrict__ x2 = nullptr, long long xns2 = 0, const float* __restrict__ w2 = nullptr,
+    float* __restrict__ y2 = nullptr, long long yns2 = 0, float* __restrict__ stat2 = nullptr,
+    int N1 = 0) {
   constexpr int CO_BLK = 16 * NC;
   constexpr int TSB = 256 * NSW;
   constexpr int WS = (CO_BLK % 32 == 16) ? CO_BLK : CO_BLK + 16;
   constexpr int KCH = 128;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
-  const int sb = blockIdx.x, co0 = blockIdx.y * CO_BLK, n = blockIdx.z;
+  const int sb = blockIdx.x, co0 = blockIdx.y * CO_BLK;
+  int n = blockIdx.z;
+  if (x2 != nullptr && n >= N1) {   // the second problem of a paired launch (l3u_pw_fwd2)
+    n -= N1; x = x2; xns = xns2; w = w2; y = y2; yns = yns2; stat_part = stat2;
+  }
   const int Kp = (K + 3) & ~3;
   const int wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const float* xn = x + (long long)n * xns;
@@ -305,12 +312,19 @@ template <int NC, bool VEC, int XM>
 __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
     const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
-    float* __restrict__ stat_part, int K, int Nout, int S, int nsb, int Dq, int Hq, int Wq) {
+    float* __restrict__ stat_part, int K, int Nout, int S, int nsb, int Dq, int Hq, int Wq,
+    const float* __restrict__ x2 = nullptr, long long xns2 = 0, const float* __restrict__ w2 = nullptr,
+    float* __restrict__ y2 = nullptr, long long yns2 = 0, float* __restrict__ stat2 = nullptr,
+    int N1 = 0) {
   constexpr int CO_BLK = 16 * NC;
   constexpr int T = NC * 16;   // accumulator floats per lane
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [4 waves][T][64 lanes]
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
-  const int sb = blockIdx.x, co0 = blockIdx.y * CO_BLK, n = blockIdx.z;
+  const int sb = blockIdx.x, co0 = blockIdx.y * CO_BLK;
+  int n = blockIdx.z;
+  if (x2 != nullptr && n >= N1) {   // the second problem of a paired launch (l3u_pw_fwd2)
+    n -= N1; x = x2; xns = xns2; w = w2; y = y2; yns = yns2; stat_part = stat2;
+  }
   const float* xn = x + (long long)n * xns;
   const int s = sb * 64 + 4 * lr;
   const int ksteps = (K + 3) >> 2;
@@ -941,9 +955,17 @@ extern "C" {
 
 namespace {
 
+struct PwSecond {   // the second problem of a paired launch: same K, Nout, S, N and options
+  const float* x; long long xns; const float* w; float* y; long long yns; float* stat;
+};
+
 int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout, const float* bias,
               float* y, long long y_nstride, int accumulate, float* stat_part, int N, int K,
-              int Nout, int S, int xm, int Dq, int Hq, int Wq, hipStream_t stream) {
+              int Nout, int S, int xm, int Dq, int Hq, int Wq, hipStream_t stream,
+              const PwSecond* sec = nullptr) {
+  const PwSecond z2{nullptr, 0, nullptr, nullptr, 0, nullptr};
+  const PwSecond& p2 = sec ? *sec : z2;
+  const int NZ = sec ? 2 * N : N;
   // xm: 0 plain GEMM, 1 ConvTranspose3d scatter epilogue, 2 X gathered from the up-sampled
   // ConvTranspose3d gradient; (Dq, Hq, Wq) = the low-resolution volume for xm != 0
   L3U_REQUIRE(N > 0 && K > 0 && Nout > 0 && S > 0);
@@ -955,9 +977,10 @@ int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout,
     int NC = Nout <= 16 ? 1 : (Nout <= 32 ? 2 : 4);
     while (NC > 1 && (long long)nsb * ((Nout + 16 * NC - 1) / (16 * NC)) * N < 256) NC >>= 1;
     const size_t lds = 4 * 64 * (size_t)NC * 16 * sizeof(float);
-    dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), N), block(256);
+    dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), NZ), block(256);
 #define PWK(NC_, V_, X_) hipLaunchKernelGGL((pw_fwd_ks_kernel<NC_, V_, X_>), grid, block, lds, stream, \
-      x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq)
+      x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq, \
+      p2.x, p2.xns, p2.w, p2.y, p2.yns, p2.stat, N)
 #define PWK_X(NC_, V_) do { if (xm == 1) PWK(NC_, V_, 1); else if (xm == 2) PWK(NC_, V_, 2); else PWK(NC_, V_, 0); } while (0)
 #define PWK_V(NC_) do { if (vec) PWK_X(NC_, true); else PWK_X(NC_, false); } while (0)
     if (NC == 1) PWK_V(1);
@@ -976,12 +999,12 @@ int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout,
   size_t lds = (size_t)(Kp < 128 ? Kp : 128) * WS * sizeof(float);
   if (lds < 4 * CO_BLK * sizeof(float)) lds = 4 * CO_BLK * sizeof(float);
   L3U_REQUIRE(lds <= 160 * 1024);
-  dim3 grid(nsb, (Nout + CO_BLK - 1) / CO_BLK, N), block(256);
+  dim3 grid(nsb, (Nout + CO_BLK - 1) / CO_BLK, NZ), block(256);
   L3U_REQUIRE(NSW == 1);
   const int KSn = K <= 16 ? 4 : (K <= 32 ? 8 : (K <= 64 ? 16 : 0));
 #define PWF(NC_, V_, X_, KS_) hipLaunchKernelGGL((pw_fwd_kernel<NC_, 1, V_, X_, KS_>), grid, block, lds, \
       stream, x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, \
-      Dq, Hq, Wq)
+      Dq, Hq, Wq, p2.x, p2.xns, p2.w, p2.y, p2.yns, p2.stat, N)
 #define PWF_K(NC_, V_, X_) do { if (KSn == 4) PWF(NC_, V_, X_, 4); else if (KSn == 8) PWF(NC_, V_, X_, 8); \
                                 else if (KSn == 16) PWF(NC_, V_, X_, 16); else PWF(NC_, V_, X_, 0); } while (0)
 #define PWF_X(NC_, V_) do { if (xm == 1) PWF_K(NC_, V_, 1); else if (xm == 2) PWF_K(NC_, V_, 2); else PWF_K(NC_, V_, 0); } while (0)
@@ -1042,6 +1065,18 @@ int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout
                float* stat_part, int N, int K, int Nout, int S, hipStream_t stream) {
   return pw_launch(x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, N, K,
                    Nout, S, 0, 0, 0, 0, stream);
+}
+
+int l3u_pw_fwd2(const float* xa, long long xa_nstride, const float* wa, float* ya,
+                long long ya_nstride, float* stat_a, const float* xb, long long xb_nstride,
+                const float* wb, float* yb, long long yb_nstride, float* stat_b, int N, int K,
+                int Nout, int S, hipStream_t stream) {
+  L3U_REQUIRE(xa && wa && ya && xb && wb && yb && (stat_a == nullptr) == (stat_b == nullptr));
+  L3U_REQUIRE(S % 4 == 0 && xa_nstride % 4 == 0 && ya_nstride % 4 == 0 && xb_nstride % 4 == 0 &&
+              yb_nstride % 4 == 0);   // both problems on the vector path
+  const PwSecond b{xb, xb_nstride, wb, yb, yb_nstride, stat_b};
+  return pw_launch(xa, xa_nstride, wa, 0, nullptr, ya, ya_nstride, 0, stat_a, N, K, Nout, S, 0, 0,
+                   0, 0, stream, &b);
 }
 
 int l3u_convt_fwd(const float* x, long long x_nstride, const float* w, const float* bias,

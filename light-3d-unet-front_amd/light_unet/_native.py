@@ -63,6 +63,7 @@ _SIGS = {
     "l3u_ftl_bwd": [P, P, L, P, D, D, D, D, P, I, P, P],
     "l3u_adamw": [P, P, P, P, L, P, F, F, F, F, P, F, P],
     "l3u_reduce_segments": [P, P, I, P, P],
+    "l3u_pw_fwd2": [P, L, P, P, L, P, P, L, P, P, L, P, I, I, I, I, P],
     "l3u_adamw_tick": [P, P, P, P, L, P, F, F, F, F, P, F, P, P, P],
     "l3u_front_nblocks": [I],
     "l3u_front_fwd": [P, L, P, P, P, P, P, P, P, P, I, I, I, I, I, P],

@@ -24,6 +24,8 @@ from . import _native as nat
 F32 = 4
 # the one-input-channel first block's front in one launch (l3u_front_fwd); L3U_FRONT=0 disables
 _FRONT = os.environ.get("L3U_FRONT", "1") != "0"
+# a block's shortcut and conv1.pointwise GEMMs as one paired launch; L3U_PAIR_PW=0 disables
+_PAIR_PW = os.environ.get("L3U_PAIR_PW", "1") != "0"
 # outputs per reduction item by partial-list length (<= 128, <= 384, longer); measured best of
 # 32..256 on the 48^3 step (tools/seg_caps.sh); L3U_SEG_CAPS overrides
 # block-tail backward inside the pointwise backwards (l3u_pw_bwd_tail); L3U_TAIL_FUSE=0 disables
@@ -348,6 +350,23 @@ class UNetEngine:
             rv = V(r, 0, cout * S, cout)
             sv["r"] = rv
             src1 = self._src(flat, pre + "norm1.", s1, nbf, rec1, drop, cptr, 1 + layer)
+        elif _PAIR_PW and shortcut and S % 4 == 0 and x.ns % 4 == 0:
+            # conv1.depthwise, then the shortcut and conv1.pointwise (same K -> Nout over the
+            # same volume) as one paired GEMM launch
+            z1 = e(N, cin, S)
+            self._call("l3u_dw3_fwd", x.p, x.ns, self._w(flat, pre + "conv1.depthwise.weight"), None,
+                       None, z1.data_ptr(), cin * S, N, cin, d, h, w, st)
+            r, y1 = e(N, cout, S), e(N, cout, S)
+            so = self.fwd_arena.alloc(N * cout * nsb * 3)
+            s1 = self.fwd_arena.alloc(N * cout * nsb * 3)
+            self._call("l3u_pw_fwd2", x.p, x.ns, self._w(flat, pre + "shortcut.0.weight"), r.data_ptr(),
+                       cout * S, self.fwd_arena.ptr(so), z1.data_ptr(), cin * S,
+                       self._w(flat, pre + "conv1.pointwise.weight"), y1.data_ptr(), cout * S,
+                       self.fwd_arena.ptr(s1), N, cin, cout, S, st)
+            src_r = self._src(flat, pre + "shortcut.1.", so, nsb, rec_r, 0.0, cptr, 0)
+            rv = V(r, 0, cout * S, cout)
+            sv["r"] = rv
+            src1 = self._src(flat, pre + "norm1.", s1, nsb, rec1, drop, cptr, 1 + layer)
         else:
             if shortcut:
                 r = e(N, cout, S)

@@ -1043,3 +1043,34 @@ def test_adamw_tick_equals_adamw(cuda):
     torch.cuda.synchronize()
     assert sa.item() == sb.item() == 5 and ctr.item() == 12 and ticket.item() == 0
     assert torch.equal(pa, pb) and torch.equal(ma, mb) and torch.equal(va, vb)
+
+
+@pytest.mark.parametrize("shape", [(4, 32, 16, 48 ** 3), (4, 64, 32, 24 ** 3), (4, 128, 64, 12 ** 3),
+                                   (4, 64, 128, 6 ** 3), (2, 8, 16, 1000)])
+def test_pw_fwd2_equals_two_pw_fwd(cuda, shape):
+    """l3u_pw_fwd2 (a block's shortcut and conv1.pointwise in one launch) == two l3u_pw_fwd
+    calls, bitwise (outputs and statistics partials), with strided (concat-view) inputs."""
+    N, K, J, S = shape
+    gen = torch.Generator().manual_seed(46)
+    xa_full = torch.randn(N, 2 * K, S, generator=gen).to(cuda)   # input as the upper half of a concat
+    xa = xa_full[:, K:]
+    xb = torch.randn(N, K, S, generator=gen).to(cuda)
+    wa = torch.randn(J, K, generator=gen).to(cuda)
+    wb = torch.randn(J, K, generator=gen).to(cuda)
+    nsb = nat().query("l3u_pw_stat_nsb", K, J, S)
+
+    def bufs():
+        return (torch.full((N, J, S), float("nan"), device=cuda),
+                torch.full((N * J * nsb * 3,), float("nan"), device=cuda))
+    (ya, sa), (yb, sb) = bufs(), bufs()
+    nat().call("l3u_pw_fwd", xa.data_ptr(), 2 * K * S, wa.data_ptr(), 0, None, ya.data_ptr(), J * S,
+               0, sa.data_ptr(), N, K, J, S, st())
+    nat().call("l3u_pw_fwd", xb.data_ptr(), K * S, wb.data_ptr(), 0, None, yb.data_ptr(), J * S, 0,
+               sb.data_ptr(), N, K, J, S, st())
+    (ya2, sa2), (yb2, sb2) = bufs(), bufs()
+    nat().call("l3u_pw_fwd2", xa.data_ptr(), 2 * K * S, wa.data_ptr(), ya2.data_ptr(), J * S,
+               sa2.data_ptr(), xb.data_ptr(), K * S, wb.data_ptr(), yb2.data_ptr(), J * S,
+               sb2.data_ptr(), N, K, J, S, st())
+    torch.cuda.synchronize()
+    for a, b in ((ya, ya2), (sa, sa2), (yb, yb2), (sb, sb2)):
+        assert torch.equal(a, b)
