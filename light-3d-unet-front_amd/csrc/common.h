@@ -222,7 +222,20 @@ L3U_DEV void block_record2(const l3u_norm_src& a, const l3u_norm_src& b, bool ha
                            int C, bool store, float* sh8) {
   const int wv = threadIdx.x >> 6;
   if (wv == 0 || (wv == 1 && has_b)) {
-    const l3u_norm_src& s = wv == 0 ? a : b;
+    // field-wise selects: a reference picked at run time between the two by-value kernel
+    // arguments made the compiler copy both to scratch in every thread (120 B of private
+    // memory per thread, ~25 MB of HBM writes per 48^3 launch, profiles/r1i_pmc_step.json)
+    const bool q = wv == 0;
+    l3u_norm_src s;
+    s.stat_part = q ? a.stat_part : b.stat_part;
+    s.nsb = q ? a.nsb : b.nsb;
+    s.layer = q ? a.layer : b.layer;
+    s.gamma = q ? a.gamma : b.gamma;
+    s.beta = q ? a.beta : b.beta;
+    s.drop_p = q ? a.drop_p : b.drop_p;
+    s.seed = q ? a.seed : b.seed;
+    s.step = q ? a.step : b.step;
+    s.rec_out = q ? a.rec_out : b.rec_out;
     float r[kRec];
     finalize_record(s, n, c, C, r);
     if ((threadIdx.x & 63) == 0) {

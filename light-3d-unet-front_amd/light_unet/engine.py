@@ -97,6 +97,19 @@ def param_layout(enc, in_channels=1, out_channels=1, use_depthwise_separable=Tru
     return out
 
 
+def _splitmix64(z):
+    z = (z + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return z ^ (z >> 31)
+
+
+def stream_seed(base, rank):
+    """The Dropout3d seed of data-parallel rank `rank` (rank 0 keeps `base`)."""
+    rank = int(rank)
+    return int(base) if rank == 0 else _splitmix64((int(base) ^ _splitmix64(rank)) & 0xFFFFFFFFFFFFFFFF)
+
+
 class _Arena:
     """Bump allocator over one float32 tensor; sized by a dry run on first use of a shape."""
 
@@ -154,7 +167,8 @@ class UNetEngine:
             self.offsets[name] = (off, n, shape)
             off += n
         self.numel = off
-        self.seed = seed
+        self.base_seed = int(seed)
+        self.stream_id = None   # None: the torch.distributed rank at call time (0 without a group)
         self._arenas = {}
         self._items = {}
         self._dry = False
@@ -164,6 +178,19 @@ class UNetEngine:
         self.bwd_arena = _Arena()
 
     # ------------------------------------------------------------------ helpers
+    @property
+    def seed(self):
+        """Dropout3d stream seed of this process.  The channel-mask hash is (seed, device step,
+        layer, n, c) with n the LOCAL sample index, so data-parallel ranks must not share a seed
+        (else local sample n draws the same mask on every rank).  Rank 0 (and a single process)
+        keeps base_seed, so single-process masks are unchanged; rank r > 0 uses a splitmix of
+        (base_seed, r).  stream_id overrides the rank (e.g. a caller-managed stream)."""
+        r = self.stream_id
+        if r is None:
+            import torch.distributed as dist
+            r = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        return stream_seed(self.base_seed, r)
+
     def _call(self, name, *args):
         if not self._dry:
             nat.call(name, *args)

@@ -30,7 +30,7 @@ def _ftl_sums(pred, target):
 
 class _FTLFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pred, target, alpha, beta, gamma, smooth, reduce_hook):
+    def forward(ctx, pred, target, alpha, beta, gamma, smooth, reduce_hook, grad_scale=1.0):
         sums = _ftl_sums(pred, target)
         if reduce_hook is not None:            # data-parallel: all-reduce the 3 global sums
             reduce_hook(sums)
@@ -39,6 +39,7 @@ class _FTLFunction(torch.autograd.Function):
                  nat.stream())
         ctx.save_for_backward(pred, target, sums)
         ctx.abgs = (alpha, beta, gamma, smooth)
+        ctx.grad_scale = grad_scale
         return loss
 
     @staticmethod
@@ -46,10 +47,12 @@ class _FTLFunction(torch.autograd.Function):
         pred, target, sums = ctx.saved_tensors
         a, b, g, s = ctx.abgs
         gout = gout.contiguous().float()
+        if ctx.grad_scale != 1.0:
+            gout = gout * ctx.grad_scale
         dp = torch.empty_like(pred)
         nat.call("l3u_ftl_bwd", pred.data_ptr(), target.data_ptr(), pred.numel(), sums.data_ptr(),
                  a, b, g, s, gout.data_ptr(), 0, dp.data_ptr(), nat.stream())
-        return dp, None, None, None, None, None, None
+        return dp, None, None, None, None, None, None, None
 
 
 def _check_inputs(pred, target):
@@ -81,68 +84,70 @@ class FocalTverskyLoss(nn.Module):
         self.beta = beta
         self.gamma = gamma
         self.smooth = smooth
-        # data-parallel hook: callable(sums_fp64[3]) that all-reduces the global sums in place
+        # data-parallel hook: callable(sums_fp64[3]) that all-reduces the sums in place, so every
+        # rank forms the loss of the GLOBAL batch (losses.py:40-46 sums over every voxel).  Each
+        # rank's backward is then its share of the global loss's gradient: the parameter
+        # gradients must be SUMMED over ranks (exchange.exchange_grads(..., "exact")).  Under a
+        # reduction that AVERAGES them (torch DDP), set hook_grad_scale = world size.
         self.reduce_hook = None
+        self.hook_grad_scale = 1.0
         assert abs(alpha + beta - 1.0) < 1e-6, f"alpha + beta must equal 1.0, got {alpha + beta}"
 
     def forward(self, pred, target):
         _check_inputs(pred, target)
         target = target.float() if target.dtype != torch.float32 else target
         return _FTLFunction.apply(pred, target, float(self.alpha), float(self.beta),
-                                  float(self.gamma), float(self.smooth), self.reduce_hook)
+                                  float(self.gamma), float(self.smooth), self.reduce_hook,
+                                  float(self.hook_grad_scale) if self.reduce_hook else 1.0)
 
 
 class CombinedLoss(nn.Module):
-    """losses.py:57-87 — FTL + BCE (out of hot-path scope; not enabled by any shipped config)."""
+    """losses.py:57-87: w_ftl * FocalTversky + w_bce * BCE over the flattened batch.  Out of the
+    hot-path scope (no shipped config enables it); composed from the FTL kernel and torch's BCE."""
 
     def __init__(self, ftl_weight=0.8, bce_weight=0.2, alpha=0.7, beta=0.3, gamma=0.75):
         super().__init__()
-        self.ftl_weight = ftl_weight
-        self.bce_weight = bce_weight
+        if abs(ftl_weight + bce_weight - 1.0) >= 1e-6:
+            raise AssertionError(f"Weights must sum to 1.0, got {ftl_weight + bce_weight}")
+        self.ftl_weight, self.bce_weight = ftl_weight, bce_weight
         self.focal_tversky = FocalTverskyLoss(alpha=alpha, beta=beta, gamma=gamma)
         self.bce = nn.BCELoss()
-        assert abs(ftl_weight + bce_weight - 1.0) < 1e-6, \
-            f"Weights must sum to 1.0, got {ftl_weight + bce_weight}"
 
     def forward(self, pred, target):
-        ftl = self.focal_tversky(pred, target)
-        bce = self.bce(pred.view(-1), target.view(-1))
-        return self.ftl_weight * ftl + self.bce_weight * bce
+        terms = (self.focal_tversky(pred, target), self.bce(pred.view(-1), target.view(-1)))
+        return self.ftl_weight * terms[0] + self.bce_weight * terms[1]
 
 
 class DiceLoss(nn.Module):
-    """losses.py:90-113 (out of hot-path scope)."""
+    """losses.py:90-113: 1 - (2 sum(p t) + s) / (sum p + sum t + s) over the flattened batch.
+    Out of the hot-path scope; plain device tensor ops."""
 
     def __init__(self, smooth=1e-6):
         super().__init__()
         self.smooth = smooth
 
     def forward(self, pred, target):
-        pred = pred.view(-1)
-        target = target.view(-1)
-        intersection = (pred * target).sum()
-        union = pred.sum() + target.sum()
-        dice = (2.0 * intersection + self.smooth) / (union + self.smooth)
-        return 1.0 - dice
+        p, t = pred.view(-1), target.view(-1)
+        num = 2.0 * torch.dot(p, t) + self.smooth
+        return 1.0 - num / (p.sum() + t.sum() + self.smooth)
+
+
+_LOSSES = {
+    "FocalTverskyLoss": lambda c: FocalTverskyLoss(alpha=c.get("alpha", 0.7), beta=c.get("beta", 0.3),
+                                                   gamma=c.get("gamma", 0.75)),
+    "DiceLoss": lambda c: DiceLoss(),
+}
 
 
 def get_loss_function(config):
-    """losses.py:116-147 — factory from the config["loss"] dict."""
-    loss_name = config.get("name", "FocalTverskyLoss")
+    """losses.py:116-147: build the loss named by config["loss"] (a combined FTL + BCE loss when
+    use_combined_loss is set); ValueError for an unknown name."""
     if config.get("use_combined_loss", False):
-        weights = config.get("combined_loss_weights", {"focal_tversky": 0.8, "bce": 0.2})
-        return CombinedLoss(
-            ftl_weight=weights["focal_tversky"],
-            bce_weight=weights["bce"],
-            alpha=config.get("alpha", 0.7),
-            beta=config.get("beta", 0.3),
-            gamma=config.get("gamma", 0.75))
-    elif loss_name == "FocalTverskyLoss":
-        return FocalTverskyLoss(
-            alpha=config.get("alpha", 0.7),
-            beta=config.get("beta", 0.3),
-            gamma=config.get("gamma", 0.75))
-    elif loss_name == "DiceLoss":
-        return DiceLoss()
-    else:
-        raise ValueError(f"Unknown loss function: {loss_name}")
+        w = config.get("combined_loss_weights", {"focal_tversky": 0.8, "bce": 0.2})
+        return CombinedLoss(ftl_weight=w["focal_tversky"], bce_weight=w["bce"],
+                            alpha=config.get("alpha", 0.7), beta=config.get("beta", 0.3),
+                            gamma=config.get("gamma", 0.75))
+    name = config.get("name", "FocalTverskyLoss")
+    if name not in _LOSSES:
+        raise ValueError(f"Unknown loss function: {name}")
+    return _LOSSES[name](config)

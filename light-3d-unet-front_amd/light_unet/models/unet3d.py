@@ -180,17 +180,26 @@ class Lightweight3DUNet(nn.Module):
 
     # -------------------------------------------------------------- flat parameter storage
     def _flatten(self):
-        """Re-home every parameter as a view of one contiguous buffer (after init or .to())."""
+        """Re-home every parameter as a view of one contiguous buffer (after init or .to()).
+        When the existing buffer already has the parameters' device and dtype (a no-op .to(),
+        or a parameter replaced in place), it is refilled in place and keeps its identity and
+        the Dropout3d counter, so a TrainStep / FlatAdamW built on it stays attached."""
         params = list(self.parameters())
         dev = params[0].device
         dt = params[0].dtype
-        flat = torch.empty(self.engine.numel, device=dev, dtype=dt)
+        old = getattr(self, "_flat", None)
+        reuse = old is not None and old.device == dev and old.dtype == dt
+        flat = old if reuse else torch.empty(self.engine.numel, device=dev, dtype=dt)
         with torch.no_grad():
             for p, (off, n, shape) in zip(params, self._slices):
-                flat[off:off + n].copy_(p.detach().reshape(-1))
-                p.data = flat[off:off + n].view(shape)
+                dst = flat[off:off + n]
+                if p.data_ptr() != dst.data_ptr():
+                    dst.copy_(p.detach().reshape(-1))
+                p.data = dst.view(shape)
         self._flat = flat
-        self._rng_counter = torch.zeros(1, dtype=torch.int32, device=dev)
+        cnt = getattr(self, "_rng_counter", None)
+        if cnt is None or cnt.device != dev:
+            self._rng_counter = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def _is_flat(self):
         base = self._flat.data_ptr()

@@ -75,9 +75,15 @@ class TrainStep:
         if self.world > 1:
             exchange_ftl_sums(sums, self.ftl_mode, self.group)
 
+    def _check_flat(self):
+        if self.model._flat is not self.flat:
+            raise RuntimeError("the model's parameters were re-homed (e.g. .to() to another "
+                               "device/dtype) after this TrainStep was built; build a new one")
+
     # ----------------------------------------------------------------- eager step
     def __call__(self, x, t):
         """One step on device tensors x, t [N,1,D,H,W]; returns the device loss (no sync)."""
+        self._check_flat()
         p, sv, sums = self._fwd(x, t)
         self._sums_exchange(sums)
         self._bwd(p, sv, t, sums)
@@ -91,12 +97,23 @@ class TrainStep:
         between graph segments: [fwd+sums] -> allreduce(sums) -> [loss+bwd] -> allreduce(grads)
         -> [adamw].  On one GPU the three segments are one graph."""
         self.xs, self.ts = x_static, t_static
+        # warm-up runs full steps (arena sizing, kernel loading); they must leave no trace: the
+        # parameters, the AdamW state and counters and the Dropout3d counter are restored, so
+        # capture() is side-effect free even on unfilled static buffers
+        self._check_flat()
+        state = [self.flat, self.opt.m, self.opt.v, self.opt.step_t, self.opt.ticket,
+                 self.model._rng_counter, self.loss]
+        saved = [t.clone() for t in state]
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 self(self.xs, self.ts)
         torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            for t, c in zip(state, saved):
+                t.copy_(c)
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
         if self.world == 1:
@@ -118,6 +135,7 @@ class TrainStep:
     def replay(self):
         if self._graphs is None:
             raise RuntimeError("call capture() first")
+        self._check_flat()
         if len(self._graphs) == 1:
             self._graphs[0].replay()
         else:

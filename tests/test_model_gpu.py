@@ -179,16 +179,22 @@ def test_trainstep_eager_graph_and_autograd_agree(cuda, golden):
     m_b = fresh()
     ts = TrainStep(m_b, lr=1e-4, weight_decay=1e-5)
     lb = [ts(x, t).item() for _ in range(steps)]
-    # (c) TrainStep captured in a hipGraph (2 warmup steps are part of the trajectory)
+    # (c) TrainStep captured in a hipGraph; capture() is side-effect free (its warm-up steps
+    # run on garbage static buffers here and are rolled back), so replays start at step 1
     m_c = fresh()
     tc = TrainStep(m_c, lr=1e-4, weight_decay=1e-5)
-    xs, tsb = x.clone(), t.clone()
+    p0 = m_c.flat_parameters().detach().clone()
+    xs, tsb = torch.full_like(x, float("nan")), torch.empty_like(t)
     tc.capture(xs, tsb, warmup=2)
+    assert torch.equal(m_c.flat_parameters().detach(), p0), "capture() moved the parameters"
+    assert int(m_c._rng_counter.item()) == 0 and int(tc.opt.step_t.item()) == 0
+    xs.copy_(x)
+    tsb.copy_(t)
     lc = []
-    for _ in range(steps - 2):
+    for _ in range(steps):
         lc.append(tc.replay().item())
     np.testing.assert_allclose(la, lb, rtol=1e-5)
-    np.testing.assert_allclose(lb[2:], lc, rtol=1e-6)
+    np.testing.assert_allclose(lb, lc, rtol=1e-6)
     pa = m_a.flat_parameters().detach()
     pb = m_b.flat_parameters().detach()
     pc = m_c.flat_parameters().detach()
@@ -222,3 +228,77 @@ def test_full_size_batch_independence(cuda):
     torch.cuda.synchronize()
     assert torch.isfinite(p4).all()
     assert (p4 - p1).abs().max().item() <= 1e-6
+
+
+def test_trainstep_data_parallel_two_ranks(cuda, tmp_path):
+    """The product data-parallel step (TrainStep: 3-segment graph with eager collectives, in-kernel
+    FTL gradient from all-reduced sums) on 2 ranks x bs 2 (gloo here, both ranks on this GPU;
+    RCCL on a node) against the single-process bs-4 step:
+      exact mode == single process on the concatenated batch (loss, flat gradient, parameters
+      after an eager step and a graph replay), to fp32 summation-order rounding;
+      local mode == the mean of the two half-batch single-process gradients (plain DDP);
+      Dropout3d: the ranks draw different channel masks; rank 0 draws the single-process masks
+      of samples 0-1 (the seed is mixed with the rank, engine.stream_seed)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    from light_unet.train_step import TrainStep
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import _trainstep_dist_worker as W
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "tests", "_trainstep_dist_worker.py"), str(tmp_path)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rk = [np.load(tmp_path / f"rank{i}.npz") for i in range(2)]
+    bt = W.batches(2)
+    dx = [torch.from_numpy(x).to(cuda) for x, _ in bt]
+    dt = [torch.from_numpy(t).to(cuda) for _, t in bt]
+
+    def rel(a, b):
+        return float(np.linalg.norm(a.astype(np.float64) - b) / np.linalg.norm(b))
+
+    # single process, bs 4: eager step, then a second eager step
+    m = W.fresh_model(cuda, 0.0)
+    ts = TrainStep(m)
+    l1 = ts(dx[0], dt[0]).item()
+    g1 = ts.gflat.cpu().numpy().astype(np.float64)
+    p1 = ts.flat.cpu().numpy().astype(np.float64)
+    l2 = ts(dx[1], dt[1]).item()
+    p2 = ts.flat.cpu().numpy().astype(np.float64)
+    for z in rk:
+        assert abs(float(z["A_loss1"]) - l1) <= 1e-5 * abs(l1)
+        assert abs(float(z["A_loss2"]) - l2) <= 1e-5 * abs(l2)
+        assert rel(z["A_g1"], g1) <= 1e-4, rel(z["A_g1"], g1)
+        # AdamW's first steps move a parameter by ~lr * g / (|g| + eps): gradients near eps
+        # (1e-8) carry the fp32 summation-order differences into the update; bound them by lr
+        assert np.abs(z["A_p1"] - p1).max() <= 0.05 * 1e-4
+        assert np.abs(z["A_p2"] - p2).max() <= 0.1 * 1e-4
+        assert np.median(np.abs(z["A_p2"] - p2)) <= 1e-9
+    assert np.array_equal(rk[0]["A_p2"], rk[1]["A_p2"]), "ranks diverged"
+    # local mode: mean of the half-batch gradients
+    gh = []
+    for h in range(2):
+        mh = W.fresh_model(cuda, 0.0)
+        th = TrainStep(mh)
+        th(dx[0][2 * h:2 * h + 2].contiguous(), dt[0][2 * h:2 * h + 2].contiguous())
+        gh.append(th.gflat.cpu().numpy().astype(np.float64))
+    gmean = 0.5 * (gh[0] + gh[1])
+    for z in rk:
+        assert rel(z["B_g1"], gmean) <= 1e-4, rel(z["B_g1"], gmean)
+    # dropout masks: distinct per rank, rank 0 == single-process samples 0-1
+    ms = W.fresh_model(cuda, 0.1)
+    _, sv = ms.engine.forward(ms.flat_parameters(), dx[0], training=True, dropout_p=0.1,
+                              counter=ms._rng_counter, save=True)
+    differ = False
+    for i, pre in enumerate(ms.engine.BLOCKS):
+        k0, k1 = rk[0][f"C_keep{i}"], rk[1][f"C_keep{i}"]
+        differ |= not np.array_equal(k0, k1)
+        ks = sv["blk"][pre]["recs"][1][:, 4].cpu().numpy()
+        np.testing.assert_array_equal(k0, ks[:k0.size])
+    assert differ, "both ranks drew the same Dropout3d masks"
