@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--size", type=int, default=48)
     ap.add_argument("--enc", type=str, default="16,32,64,128")
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="activation storage of the headline step (bf16: BASELINE config 3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=40)   # ~10-30 s of host work
     ap.add_argument("--no-graph", action="store_true")
@@ -377,7 +379,8 @@ def main():
     if world > 1:   # identical initial weights on every rank (DDP semantics)
         dist.broadcast(model.flat_parameters(), 0)
     step = TrainStep(model, {"alpha": 0.7, "beta": 0.3, "gamma": 0.75}, lr=1e-4, weight_decay=1e-5,
-                     ftl_mode=args.ftl_mode)
+                     ftl_mode=args.ftl_mode,
+                     dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     pool = synthetic_pool(8, args.batch, args.size, rank, device)
     xs, ts = [b[0] for b in pool], [b[1] for b in pool]
     xt_static = pool[0].clone()
@@ -387,7 +390,8 @@ def main():
     N, S = args.batch, args.size ** 3
     cdom = 2 * enc[0]      # up3.res_block conv1.depthwise: [N, 2*c0, D^3] backward
     # l3u_dw3_bwd args end with (..., N, C, D, H, W, stream)
-    timer = KernelTimer(("l3u_dw3_bwd",), lambda a: a[-5] == cdom and a[-4] == args.size)
+    dom_name = "l3u_dw3_bwd" + ("_bf16" if args.dtype == "bf16" else "")
+    timer = KernelTimer((dom_name,), lambda a: a[-5] == cdom and a[-4] == args.size)
     orig = timer.wrap(nat)
     for i in range(3):
         step(xs[i % 8], ts[i % 8])

@@ -10,7 +10,10 @@
  *   - the last argument is the hipStream_t to enqueue on; calls are asynchronous;
  *   - the return value is a hipError_t as int (0 = hipSuccess; hipErrorInvalidValue for a shape
  *     the kernels do not support, e.g. an H*W plane above 4096 voxels for the stencil);
- *   - activations are fp32 NCDHW with the spatial volume S = D*H*W contiguous per (n, c); a tensor
+ *   - activations are NCDHW with the spatial volume S = D*H*W contiguous per (n, c), stored as fp32
+ *     or — entry points with the suffix _bf16, same arguments otherwise — as bf16 (l3u_bf16, the
+ *     raw 16-bit pattern); kernels compute in fp32 either way (bf16 loads widen, stores round to
+ *     nearest even), weights / records / partial sums are always fp32 (fp64 where marked); a tensor
  *     is (pointer, batch stride in elements) — channel stride is always S.  A batch stride larger
  *     than C*S addresses one channel range of a concatenation buffer (zero-copy torch.cat);
  *   - "rec" is the per-(n,c) InstanceNorm record of 8 floats:
@@ -32,6 +35,8 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+typedef unsigned short l3u_bf16;   /* bfloat16 bit pattern (torch.bfloat16 storage) */
 
 int l3u_abi_version(void);
 
@@ -68,15 +73,6 @@ int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long
                 const float* w, const float* rec, float* dx, long long dx_nstride, int accumulate,
                 float* dw_part, double* in_part, int N, int C, int D, int H, int W,
                 hipStream_t stream);
-/* the two halves of l3u_dw3_bwd as separate calls (same arguments and partial layouts), so the
- * weight gradient can run on another stream off the data-gradient critical path             */
-int l3u_dw3_bwd_data(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
-                     const float* w, const float* rec, float* dx, long long dx_nstride,
-                     int accumulate, double* in_part, int N, int C, int D, int H, int W,
-                     hipStream_t stream);
-int l3u_dw3_bwd_weight(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
-                       const float* w, const float* rec, float* dw_part, int N, int C, int D,
-                       int H, int W, hipStream_t stream);
 
 /* ---- channel-contraction GEMM on MFMA (v_mfma_f32_16x16x4_f32) ------------------------------
  * Y[n][j][s] = sum_k Wm[j][k] X[n][k][s] (+ bias[j]) (+ Y if accumulate)
@@ -197,13 +193,8 @@ int l3u_maxpool2_bwd(const float* dy, long long dy_nstride, const unsigned char*
                      const float* add, long long add_nstride, float* dx, long long dx_nstride,
                      int N, int C, int D, int H, int W, hipStream_t stream);
 
-/* ---- ConvTranspose3d(Ci, Co, 2, 2) scatter halves (UpBlock.up, unet3d.py:119, forward :127) -
- * GEMM half = l3u_pw_fwd(w_layout=1, Nout=Co*8) into yp[N][Co*8][S_in];
- * d2s: out[n][co][2z+a][2y+b][2x+c] = yp[n][co*8+4a+2b+c][z][y][x] + bias[co]  (D,H,W = input dims)
- * s2d: the inverse permutation (backward)                                                     */
-int l3u_convt_d2s(const float* yp, const float* bias, float* out, long long out_nstride, int N,
-                  int Co, int D, int H, int W, hipStream_t stream);
-/* the whole forward in one launch: the [Co*8 x Ci] GEMM on MFMA with the scatter (and bias) in
+/* ---- ConvTranspose3d(Ci, Co, 2, 2) (UpBlock.up, unet3d.py:119, forward :127) ---------------
+ * the whole forward in one launch: the [Co*8 x Ci] GEMM on MFMA with the scatter (and bias) in
  * its epilogue (x: [N][Ci][D*H*W], w: torch ConvTranspose3d weight [Ci][Co][2][2][2])        */
 int l3u_convt_fwd(const float* x, long long x_nstride, const float* w, const float* bias,
                   float* out, long long out_nstride, int N, int Ci, int Co, int D, int H, int W,
@@ -225,13 +216,6 @@ int l3u_convt_bwd_fused_nparts(int N, int Ci, int Co, int D, int H, int W);
 int l3u_convt_bwd_fused(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
                         const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
                         int N, int Ci, int Co, int D, int H, int W, hipStream_t stream);
-int l3u_convt_s2d(const float* dy, long long dy_nstride, float* dyp, int N, int Co, int D, int H,
-                  int W, hipStream_t stream);
-/* per-channel sums part[C][N][nblocks] (fp64; bias gradients)                                */
-int l3u_chan_sum_nblocks(long long S);
-int l3u_chan_sum(const float* x, long long x_nstride, double* part, int N, int C, long long S,
-                 hipStream_t stream);
-
 /* ---- out_conv (1x1x1, C->1, bias) + Sigmoid (unet3d.py:201-202, forward :220-221) ----------
  * fwd: p = sigmoid(b + w.h); t != NULL also emits the FocalTversky first-stage partials
  *      ftl_part[N*nblocks][3] = {sum p*t, sum p, sum t} (reduce them with l3u_ftl_reduce)
@@ -256,17 +240,6 @@ int l3u_outconv_bwd(const float* dp, const float* p, const float* t, const doubl
 int l3u_ftl_nblocks(long long numel);
 int l3u_ftl_sums(const float* p, const float* t, long long numel, float* part, double* sums,
                  hipStream_t stream);
-/* l3u_outconv_bwd that also writes the first stage of the last decoder block's tail backward
- * (l3u_norm_act_bwd_reduce of up3.res_block, whose output is h): tail_part[C][N][nb][3] =
- * {sum g, sum g*xhat2, sum g*xhat_r}, g = dh*lrelu'(h), nb = l3u_outconv_nblocks(S); for the
- * Conv1x1-shortcut block, C <= 16, S % 4 == 0                                                  */
-int l3u_outconv_bwd_tail(const float* dp, const float* p, const float* t, const double* sums,
-                         double alpha, double beta, double gamma, double smooth,
-                         const float* gscale, const float* h, long long h_nstride, const float* w,
-                         float* dh, long long dh_nstride, double* part, float* loss,
-                         const float* y2, long long y2_nstride, const float* rec2, const float* r,
-                         long long r_nstride, const float* rec_r, double* tail_part, int N, int C,
-                         int S, hipStream_t stream);
 /* second stage only (partials from l3u_outconv_fwd): sums[3] = fixed-order sum of part[nparts][3] */
 int l3u_ftl_reduce(const float* part, int nparts, double* sums, hipStream_t stream);
 int l3u_ftl_loss(const double* sums, double alpha, double beta, double gamma, double smooth,
@@ -275,21 +248,17 @@ int l3u_ftl_bwd(const float* p, const float* t, long long numel, const double* s
                 double beta, double gamma, double smooth, const float* gscale,
                 int through_sigmoid, float* g, hipStream_t stream);
 
-/* ---- AdamW on the flat parameter buffer (torch.optim.AdamW, trainer.py:75-79) -------------
- * lr and step live on the device (graph-replay safe); the call increments *step.             */
-int l3u_adamw(float* p, const float* g, float* m, float* v, long long numel, const float* lr,
-              float beta1, float beta2, float eps, float weight_decay, int* step, float grad_scale,
-              hipStream_t stream);
-
 /* ---- the first block's front (in_channels = 1, unet3d.py:163-167) --------------------------
  * one launch for the Conv1x1 shortcut r[c] = wr[c]*x, conv1.depthwise z1 = dw3(x) (one channel,
  * w_dw [27]) and conv1.pointwise y1[c] = w1[c]*z1, with the (count, mean, M2) partials of r and y1
  * ([N][C][l3u_front_nblocks(S)][3], the l3u_pw_fwd format) from the channel's own moments.
- * Replaces three launches of unet3d.py:70-73,16-18 for the init_conv block.  W % 4 == 0.       */
+ * Replaces three launches of unet3d.py:70-73,16-18 for the init_conv block.  W % 4 == 0.
+ * x is the caller's fp32 input; x_copy != NULL also receives x in the storage type (the bf16
+ * network's backward reads its input in bf16).                                                  */
 int l3u_front_nblocks(int S);
 int l3u_front_fwd(const float* x, long long x_nstride, const float* w_dw, const float* w1,
                   const float* wr, float* z1, float* y1, float* r, float* stat1, float* statr,
-                  int N, int C, int D, int H, int W, hipStream_t stream);
+                  float* x_copy, int N, int C, int D, int H, int W, hipStream_t stream);
 
 /* ---- grouped / dense 3x3x3 conv (stride 1, padding 1, no bias): the
  * use_depthwise_separable=False path of ResidualBlock (GroupedConv3d unet3d.py:26-34, chosen at
@@ -315,7 +284,8 @@ int l3u_gconv3_bwd_weight(const float* dy, long long dy_nstride, const float* x,
                           long long x_nstride, const float* rec, float* part, int N, int Cin,
                           int Cout, int G, int D, int H, int W, hipStream_t stream);
 
-/* the same AdamW update (torch.optim.AdamW, trainer.py:75-79) in ONE launch: the last workgroup
+/* ---- AdamW on the flat parameter buffer (torch.optim.AdamW, trainer.py:75-79) -------------
+ * lr and step live on the device (graph-replay safe).  ONE launch: the last workgroup
  * to finish (ticket order; *ticket starts at 0 and is reset) advances *step and, when
  * counter2 != NULL, *counter2 (the model's Dropout3d stream counter, unet3d.py:66, so a
  * captured training step needs no separate counter launches)                                   */
@@ -342,8 +312,105 @@ int l3u_window_blend(const float* preds, const int* zpos, int nz, const int* ypo
                      const int* xpos, int nx, const float* imp, int D, int H, int W, int pd, int ph,
                      int pw, float* prob, hipStream_t stream);
 
+/* storage casts (the bf16 network's input / input gradient); n elements                      */
+int l3u_cast_f32_bf16(const float* x, l3u_bf16* y, long long n, hipStream_t stream);
+int l3u_cast_bf16_f32(const l3u_bf16* x, float* y, long long n, hipStream_t stream);
+
 /* device counter += value (Dropout3d RNG stream position, advanced once per training forward) */
 int l3u_counter_add(int* counter, int value, hipStream_t stream);
+
+/* ---- bf16 twins (BASELINE config 3) --------------------------------------------------------
+ * The same calls with the saved activations (forward inputs and outputs: what the backward
+ * re-reads) stored as bf16; argument order and meaning are those of the fp32 entry point without
+ * the suffix.  Gradients (every backward input/output gradient), weights, biases, InstanceNorm
+ * records and the statistics / weight-gradient partials stay fp32 (fp64 where marked), and every
+ * kernel computes in fp32 (bf16 loads widen exactly, stores round to nearest even).
+ * l3u_outconv_* keep p / dp / t fp32 (the loss runs on fp32 probabilities); l3u_front_fwd reads
+ * the caller's fp32 x and can write its bf16 copy (x_copy) for the backward.  l3u_maxpool2_bwd
+ * has no bf16 twin: it reads no saved activation.                                          */
+int l3u_dw3_fwd_bf16(const l3u_bf16* x, long long x_nstride, const float* w, const float* rec,
+                     const l3u_norm_src* src, l3u_bf16* y, long long y_nstride, int N, int C, int D,
+                     int H, int W, hipStream_t stream);
+int l3u_dw3_bwd_bf16(const float* dz, long long dz_nstride, const l3u_bf16* x, long long x_nstride,
+                     const float* w, const float* rec, float* dx, long long dx_nstride,
+                     int accumulate, float* dw_part, double* in_part, int N, int C, int D, int H,
+                     int W, hipStream_t stream);
+int l3u_maxpool2_fwd_bf16(const l3u_bf16* x, long long x_nstride, l3u_bf16* y, long long y_nstride,
+                          unsigned char* idx, int N, int C, int D, int H, int W,
+                          hipStream_t stream);
+int l3u_outconv_fwd_bf16(const l3u_bf16* h, long long h_nstride, const float* w, const float* b,
+                         float* p, const float* t, float* ftl_part, int N, int C, int S,
+                         hipStream_t stream);
+int l3u_outconv_bwd_bf16(const float* dp, const float* p, const float* t, const double* sums,
+                         double alpha, double beta, double gamma, double smooth,
+                         const float* gscale, const l3u_bf16* h, long long h_nstride,
+                         const float* w, float* dh, long long dh_nstride, double* part, float* loss,
+                         int N, int C, int S, hipStream_t stream);
+int l3u_front_fwd_bf16(const float* x, long long x_nstride, const float* w_dw, const float* w1,
+                       const float* wr, l3u_bf16* z1, l3u_bf16* y1, l3u_bf16* r, float* stat1,
+                       float* statr, l3u_bf16* x_copy, int N, int C, int D, int H, int W,
+                       hipStream_t stream);
+int l3u_norm_act_fwd_bf16(const l3u_bf16* y2, long long y2_nstride, const float* rec2,
+                          const l3u_norm_src* src2, const l3u_bf16* r, long long r_nstride,
+                          const float* rec_r, const l3u_norm_src* src_r, int shortcut,
+                          l3u_bf16* out, long long out_nstride, int N, int C, int S,
+                          hipStream_t stream);
+int l3u_norm_act_pool_fwd_bf16(const l3u_bf16* y2, long long y2_nstride, const float* rec2,
+                               const l3u_norm_src* src2, const l3u_bf16* r, long long r_nstride,
+                               const float* rec_r, const l3u_norm_src* src_r, int shortcut,
+                               l3u_bf16* out, long long out_nstride, l3u_bf16* pooled,
+                               long long pooled_nstride, unsigned char* idx, int N, int C, int D,
+                               int H, int W, hipStream_t stream);
+int l3u_norm_act_bwd_reduce_bf16(const float* dout, long long dout_nstride, const l3u_bf16* out,
+                                 long long out_nstride, const l3u_bf16* y2, long long y2_nstride,
+                                 const float* rec2, const l3u_bf16* r, long long r_nstride,
+                                 const float* rec_r, double* part, int N, int C, int S,
+                                 hipStream_t stream);
+int l3u_norm_act_bwd_apply_bf16(const float* dout, long long dout_nstride, const l3u_bf16* out,
+                                long long out_nstride, const l3u_bf16* y2, long long y2_nstride,
+                                const float* rec2, const l3u_bf16* r, long long r_nstride,
+                                const float* rec_r, const double* part, float* dy2,
+                                long long dy2_nstride, float* dr, long long dr_nstride, int N,
+                                int C, int S, hipStream_t stream);
+int l3u_norm_act_bwd_bf16(const float* dout, long long dout_nstride, const l3u_bf16* out,
+                          long long out_nstride, const l3u_bf16* y2, long long y2_nstride,
+                          const float* rec2, const l3u_bf16* r, long long r_nstride,
+                          const float* rec_r, double* part, float* dy2, long long dy2_nstride,
+                          float* dr, long long dr_nstride, int N, int C, int S, hipStream_t stream);
+int l3u_in_bwd_apply_bf16(const float* dpre, long long dpre_nstride, const l3u_bf16* y,
+                          long long y_nstride, const float* rec, const double* in_part, int npart,
+                          float* dy, long long dy_nstride, int N, int C, int S, hipStream_t stream);
+int l3u_pw_fwd_bf16(const l3u_bf16* x, long long x_nstride, const float* w, int w_layout,
+                    const float* bias, l3u_bf16* y, long long y_nstride, int accumulate,
+                    float* stat_part, int N, int K, int Nout, int S, hipStream_t stream);
+int l3u_pw_fwd2_bf16(const l3u_bf16* xa, long long xa_nstride, const float* wa, l3u_bf16* ya,
+                     long long ya_nstride, float* stat_a, const l3u_bf16* xb, long long xb_nstride,
+                     const float* wb, l3u_bf16* yb, long long yb_nstride, float* stat_b, int N,
+                     int K, int Nout, int S, hipStream_t stream);
+int l3u_convt_fwd_bf16(const l3u_bf16* x, long long x_nstride, const float* w, const float* bias,
+                       l3u_bf16* out, long long out_nstride, int N, int Ci, int Co, int D, int H,
+                       int W, hipStream_t stream);
+int l3u_pw_bwd_weight_bf16(const float* dy, long long dy_nstride, const l3u_bf16* x,
+                           long long x_nstride, float* part, int N, int J, int K, int S,
+                           hipStream_t stream);
+int l3u_pw_bwd_tail_bf16(const float* dout, long long dout_nstride, const l3u_bf16* out,
+                         long long out_nstride, const l3u_bf16* yr, long long yr_nstride,
+                         const float* rec, const double* tail_part, int npart, int sel,
+                         const l3u_bf16* x, long long x_nstride, const float* w, float* dx,
+                         long long dx_nstride, int accumulate, float* part, int N, int J, int K,
+                         int S, hipStream_t stream);
+int l3u_pw_bwd_bf16(const float* dy, long long dy_nstride, const l3u_bf16* y, long long y_nstride,
+                    const float* rec, const double* in_part, int npart, const l3u_bf16* x,
+                    long long x_nstride, const float* w, float* dx, long long dx_nstride,
+                    int accumulate, float* part, int N, int J, int K, int S, hipStream_t stream);
+int l3u_convt_bwd_fused_bf16(const float* dy, long long dy_nstride, const l3u_bf16* x,
+                             long long x_nstride, const float* w, float* dx, long long dx_nstride,
+                             float* wpart, float* bpart, int N, int Ci, int Co, int D, int H, int W,
+                             hipStream_t stream);
+int l3u_convt_bwd_bf16(const float* dy, long long dy_nstride, const l3u_bf16* x,
+                       long long x_nstride, const float* w, float* dx, long long dx_nstride,
+                       float* wpart, float* bpart, int N, int Ci, int Co, int D, int H, int W,
+                       hipStream_t stream);
 
 #ifdef __cplusplus
 }

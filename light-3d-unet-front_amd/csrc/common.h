@@ -10,6 +10,7 @@
 #include "l3u.h"
 
 #define L3U_DEV __device__ __forceinline__
+#define L3U_INLINE_HOST static inline
 
 namespace l3u {
 
@@ -23,6 +24,37 @@ constexpr float kEps = 1e-5f;     // InstanceNorm3d eps (torch default)  unet3d.
 // valid because lrelu(k*v) = k*lrelu(v) for k >= 0.  (y - mean) is formed first: folding the mean
 // into the shift cancels catastrophically when |mean| >> std and costs ~1e-5 relative accuracy.
 constexpr int kRec = 8;
+
+// ---- activation storage types -----------------------------------------------------------------
+// Activations (and their gradients) are stored as T = float or bf16; every kernel computes in fp32
+// (loads widen, stores round to nearest even with v_cvt_pk_bf16_f32), statistics in fp32 / fp64,
+// weights and partial sums stay fp32.  Overloads on the pointer type, so the same kernel text
+// serves LDS (float) and global (T) operands.
+typedef __bf16 bf16;
+typedef float f4_t __attribute__((ext_vector_type(4)));
+typedef float f2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 b4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+
+L3U_DEV f4_t ldv4(const float* p) { return *reinterpret_cast<const f4_t*>(p); }
+L3U_DEV f4_t ldv4(const bf16* p) { return __builtin_convertvector(*reinterpret_cast<const b4_t*>(p), f4_t); }
+L3U_DEV void stv4(float* p, f4_t v) { *reinterpret_cast<f4_t*>(p) = v; }
+L3U_DEV void stv4(bf16* p, f4_t v) { *reinterpret_cast<b4_t*>(p) = __builtin_convertvector(v, b4_t); }
+L3U_DEV void stv4_nt(float* p, f4_t v) { __builtin_nontemporal_store(v, reinterpret_cast<f4_t*>(p)); }
+L3U_DEV void stv4_nt(bf16* p, f4_t v) {
+  __builtin_nontemporal_store(__builtin_convertvector(v, b4_t), reinterpret_cast<b4_t*>(p));
+}
+L3U_DEV f2_t ldv2(const float* p) { return *reinterpret_cast<const f2_t*>(p); }
+L3U_DEV f2_t ldv2(const bf16* p) { return __builtin_convertvector(*reinterpret_cast<const b2_t*>(p), f2_t); }
+L3U_DEV void stv2(float* p, f2_t v) { *reinterpret_cast<f2_t*>(p) = v; }
+L3U_DEV void stv2(bf16* p, f2_t v) { *reinterpret_cast<b2_t*>(p) = __builtin_convertvector(v, b2_t); }
+// v rounded to the storage precision of T (the value a store + reload would give)
+L3U_DEV f4_t round_to(f4_t v, const float*) { return v; }
+L3U_DEV f4_t round_to(f4_t v, const bf16*) { return __builtin_convertvector(__builtin_convertvector(v, b4_t), f4_t); }
+L3U_DEV float ld1(const float* p) { return *p; }
+L3U_DEV float ld1(const bf16* p) { return (float)*p; }
+L3U_DEV void st1(float* p, float v) { *p = v; }
+L3U_DEV void st1(bf16* p, float v) { *p = (bf16)v; }
 
 L3U_DEV float lrelu(float v) { return v > 0.f ? v : v * kSlope; }
 L3U_DEV float lrelu_d(float pre) { return pre > 0.f ? 1.f : kSlope; }   // torch: x > 0 ? 1 : slope
@@ -261,6 +293,17 @@ L3U_DEV int xcd_remap(int bid, int nblocks) {
 }
 
 }  // namespace l3u
+
+// C-ABI twins: every activation entry point exists for fp32 and, with the suffix _bf16, for bf16
+// storage (l3u_bf16 = the raw 16-bit pattern in the header).  bp() maps an ABI pointer to the
+// kernel element type (identity for float), so both twins share one argument list.
+L3U_INLINE_HOST const float* bp(const float* p) { return p; }
+L3U_INLINE_HOST float* bp(float* p) { return p; }
+L3U_INLINE_HOST const l3u::bf16* bp(const l3u_bf16* p) { return reinterpret_cast<const l3u::bf16*>(p); }
+L3U_INLINE_HOST l3u::bf16* bp(l3u_bf16* p) { return reinterpret_cast<l3u::bf16*>(p); }
+#define L3U_TWIN(NAME, PARAMS, ...)                               \
+  extern "C" int NAME PARAMS(float) { return __VA_ARGS__; }        \
+  extern "C" int NAME##_bf16 PARAMS(l3u_bf16) { return __VA_ARGS__; }
 
 // Error plumbing for the C-ABI: every entry point returns a hipError_t as int.
 #define L3U_CHECK_LAUNCH() return (int)hipGetLastError()

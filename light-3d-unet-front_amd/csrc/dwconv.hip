@@ -21,10 +21,10 @@ using namespace l3u;
 
 namespace {
 
-template <int MODE, int P>
+template <typename T, int MODE, int P>
 __global__ __launch_bounds__(256) void dw3_fwd_kernel(
-    const float* __restrict__ x, long long xns, const float* __restrict__ w,
-    const float* __restrict__ rec, l3u_norm_src src, int has_src, float* __restrict__ y,
+    const T* __restrict__ x, long long xns, const float* __restrict__ w,
+    const float* __restrict__ rec, l3u_norm_src src, int has_src, T* __restrict__ y,
     long long yns, int C, int D, int H, int W, int TZ, int nchunk) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int HW = H * W, PW = W + 2, PP = (H + 2) * PW;
@@ -33,8 +33,8 @@ __global__ __launch_bounds__(256) void dw3_fwd_kernel(
   const int nc = lb / nchunk;
   const int c = nc % C, n = nc / C;
   const int z0 = chunk * TZ, z1 = min(z0 + TZ, D);
-  const float* xp = x + (long long)n * xns + (long long)c * D * HW;
-  float* yp = y + (long long)n * yns + (long long)c * D * HW;
+  const T* xp = x + (long long)n * xns + (long long)c * D * HW;
+  T* yp = y + (long long)n * yns + (long long)c * D * HW;
   const int tid = threadIdx.x;
 
   float wk[27];
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void dw3_fwd_kernel(
     if (zi >= 0) {
 #pragma unroll
       for (int k = 0; k < P; ++k)
-        if (own[k]) nxt[k] = xp[(long long)zi * HW + tid + k * 256];
+        if (own[k]) nxt[k] = ld1(xp + (long long)zi * HW + tid + k * 256);
     }
   }
   __syncthreads();
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void dw3_fwd_kernel(
     if (zn <= z1 && zn < D) {
 #pragma unroll
       for (int k = 0; k < P; ++k)
-        if (own[k]) nxt[k] = xp[(long long)zn * HW + tid + k * 256];
+        if (own[k]) nxt[k] = ld1(xp + (long long)zn * HW + tid + k * 256);
     }
     __syncthreads();
 #pragma unroll
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void dw3_fwd_kernel(
     if (zo >= z0 && zo < z1) {
 #pragma unroll
       for (int k = 0; k < P; ++k)
-        if (own[k]) yp[(long long)zo * HW + tid + k * 256] = a0[k];
+        if (own[k]) st1(yp + (long long)zo * HW + tid + k * 256, a0[k]);
     }
 #pragma unroll
     for (int k = 0; k < P; ++k) { a0[k] = a1[k]; a1[k] = a2[k]; a2[k] = 0.f; }
@@ -133,9 +133,9 @@ __global__ __launch_bounds__(256) void dw3_fwd_kernel(
 // MODE 1: A = lrelu(scale*y + shift) recomputed from y; the kernel emits
 // dpre = dA * k * lrelu'(pre) (gradient at the InstanceNorm output before the activation) and the
 // per-(n,c) partial sums  sum(dpre), sum(dpre * xhat)  for the InstanceNorm backward.
-template <int MODE, int P>
+template <typename T, int MODE, int P>
 __global__ __launch_bounds__(256) void dw3_bwd_kernel(
-    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
+    const float* __restrict__ dz, long long dzns, const T* __restrict__ x, long long xns,
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
     long long dxns, int accumulate, float* __restrict__ dw_part, double* __restrict__ in_part,
     int N, int C, int D, int H, int W, int TZ, int nchunk) {
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void dw3_bwd_kernel(
   const int z0 = chunk * TZ, z1 = min(z0 + TZ, D);
   const long long cofs = (long long)c * D * HW;
   const float* dzp = dz + (long long)n * dzns + cofs;
-  const float* xp = x + (long long)n * xns + cofs;
+  const T* xp = x + (long long)n * xns + cofs;
   float* dxp = dx + (long long)n * dxns + cofs;
   const int tid = threadIdx.x;
   float* dzb = lds;            // 2 planes
@@ -195,10 +195,10 @@ __global__ __launch_bounds__(256) void dw3_bwd_kernel(
     for (int k = 0; k < P; ++k) {
       if (own[k]) {
         const long long off = tid + k * 256;
-        dbuf[lbase[k]] = ldz ? dzp[(long long)zd * HW + off] : 0.f;
+        dbuf[lbase[k]] = ldz ? ld1(dzp + (long long)zd * HW + off) : 0.f;
         float v = 0.f;
         if (la) {
-          v = xp[(long long)za * HW + off];
+          v = ld1(xp + (long long)za * HW + off);
           if (MODE == 1) v = lrelu(fmaf(sc, v - mean, sh));
         }
         abuf[lbase[k]] = v;
@@ -246,15 +246,15 @@ __global__ __launch_bounds__(256) void dw3_bwd_kernel(
         if (!own[k]) continue;
         const long long idx = (long long)zf * HW + tid + k * 256;
         if (MODE == 1) {
-          const float yv = xp[idx];
+          const float yv = ld1(xp + idx);
           const float pre = fmaf(sc, yv - mean, sh);
           const float dp = d0[k] * kk * lrelu_d(pre);
           const float xh = (yv - mean) * rstd;
-          dxp[idx] = dp;
+          st1(dxp + idx, dp);
           s1 += dp;
           s2 += (double)dp * xh;
         } else {
-          dxp[idx] = accumulate ? dxp[idx] + d0[k] : d0[k];
+          st1(dxp + idx, accumulate ? ld1(dxp + idx) + d0[k] : d0[k]);
         }
       }
     }
@@ -427,9 +427,15 @@ L3U_DEV void q_nbr(const float* plane, int row, int W, int ox, bool el, bool er,
   v[5] = er ? 0.f : r;
 }
 
-// Register-staged plane loads (issued early, committed to LDS when their step comes up).
+// Register-staged plane loads (issued early, committed to LDS when their step comes up); held
+// in the storage type (bf16 staging costs half the VGPRs) and widened at commit.
+template <typename T> struct Raw4 { typedef f4 type; };
+template <> struct Raw4<bf16> { typedef b4_t type; };
+L3U_DEV f4 widen(f4 v) { return v; }
+L3U_DEV f4 widen(b4_t v) { return __builtin_convertvector(v, f4); }
+template <typename T>
 struct QPre {
-  f4 v[2];
+  typename Raw4<T>::type v[2];
 };
 
 // Per-thread staging map, computed once: global offset (within a plane) and LDS offset of the
@@ -458,14 +464,15 @@ L3U_DEV QMap q_map(int y0, int rows, int H, int W, int WQ, int lpitch = 0, int l
   return m;
 }
 
-L3U_DEV void q_fetch(QPre& p, const float* plane, const QMap& m) {
+template <typename T>
+L3U_DEV void q_fetch(QPre<T>& p, const T* plane, const QMap& m) {
 #pragma unroll
-  for (int k = 0; k < 2; ++k) p.v[k] = *reinterpret_cast<const f4*>(plane + m.goff[k]);
+  for (int k = 0; k < 2; ++k) p.v[k] = *reinterpret_cast<const typename Raw4<T>::type*>(plane + m.goff[k]);
 }
 
 // commit a staged plane to LDS (zeros for a plane outside the needed z range)
-template <bool XF>
-L3U_DEV void q_commit(const QPre& p, float* lplane, const QMap& m, bool in, float sc, float mu,
+template <bool XF, typename T>
+L3U_DEV void q_commit(const QPre<T>& p, float* lplane, const QMap& m, bool in, float sc, float mu,
                       float sh) {
   // out of range: XF folds the zero into the transform (lrelu(0*(v-mu) + 0) = 0), plain
   // planes multiply by 0 (two v_pk_mul per quad instead of four selects)
@@ -474,7 +481,7 @@ L3U_DEV void q_commit(const QPre& p, float* lplane, const QMap& m, bool in, floa
   sh *= keep;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    f4 v = p.v[k];
+    f4 v = widen(p.v[k]);
     if (XF) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(sc, v[i] - mu, sh));
@@ -498,20 +505,20 @@ L3U_DEV void pin(T& v) { asm volatile("" : "+v"(v)); }
 //            + shift (ep = the saved pre-IN activation), plus the fp64 IN-backward sums
 //            in_part[c][n][chunk] = {sum dpre, sum dpre*xhat}
 //   EPI = 2: backward data, y += conv^T(x)      EPI = 3: backward data, y = conv^T(x)
-template <int XF, int EPI, int TZC>
+template <typename T, typename TE, int XF, int EPI, int TZC>
 __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
-    const float* __restrict__ x, long long xns, const float* __restrict__ w,
-    const float* __restrict__ rec, l3u_norm_src src, int has_src, float* __restrict__ y,
-    long long yns, const float* __restrict__ ep, long long epns, double* __restrict__ in_part,
+    const T* __restrict__ x, long long xns, const float* __restrict__ w,
+    const float* __restrict__ rec, l3u_norm_src src, int has_src, T* __restrict__ y,
+    long long yns, const TE* __restrict__ ep, long long epns, double* __restrict__ in_part,
     int N, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
   constexpr bool FLIP = EPI != 0;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int WQ = W >> 2, PP = (RB + 2) * W, HW = H * W;
   const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
   const long long cofs = (long long)b.c * D * HW;
-  const float* xp = x + (long long)b.n * xns + cofs;
-  float* yp = y + (long long)b.n * yns + cofs;
-  const float* epp = (EPI == 1 || EPI == 2) ? ep + (long long)b.n * epns + cofs : nullptr;
+  const T* xp = x + (long long)b.n * xns + cofs;
+  T* yp = y + (long long)b.n * yns + cofs;
+  const TE* epp = (EPI == 1 || EPI == 2) ? ep + (long long)b.n * epns + cofs : nullptr;
   float wk[27];
 #pragma unroll
   for (int t = 0; t < 27; ++t) wk[t] = w[b.c * 27 + (FLIP ? 26 - t : t)];
@@ -537,17 +544,17 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
   // step t consumes input plane zi = z0-1+t; the step count is a compile-time constant and the
   // loop is fully unrolled, so the two staged registers never move (no back-edge copies that
   // would force a vmcnt(0) drain of the pipeline)
-  QPre p0, p1;
+  QPre<T> p0, p1;
   q_fetch(p0, xp + zc(b.z0 - 1), qm);
   q_fetch(p1, xp + zc(b.z0), qm);
-  auto step = [&](int t, QPre& pre) {
+  auto step = [&](int t, QPre<T>& pre) {
     const int zi = b.z0 - 1 + t;
     float* buf = lds + (t & 1) * PP;
     q_commit<XF == 1>(pre, buf, qm, zi >= zlo && zi <= zhi, sc, mu, sh);
     q_fetch(pre, xp + zc(zi + 2), qm);
     const int zo = zi - 1;   // output plane zo has all three input planes after this step
     f4 e = {0.f, 0.f, 0.f, 0.f};
-    if (EPI == 1 || EPI == 2) e = *reinterpret_cast<const f4*>(epp + (long long)min(max(zo, 0), D - 1) * HW + qofs);
+    if (EPI == 1 || EPI == 2) e = ldv4(epp + (long long)min(max(zo, 0), D - 1) * HW + qofs);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -580,7 +587,7 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
     } else if (EPI == 2) {
       o += e;
     }
-    if (fin) *reinterpret_cast<f4*>(yp + (long long)zo * HW + qofs) = o;
+    if (fin) stv4(yp + (long long)zo * HW + qofs, o);
     a0 = a1;
     a1 = a2;
     a2 = f4{0.f, 0.f, 0.f, 0.f};
@@ -610,9 +617,9 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
 // through LDS (x-neighbours by DPP); each thread's own dZ quad comes straight from global memory,
 // three planes kept in registers.  Split from the data gradient (which is the forward kernel with
 // flipped taps) so that each pass keeps few registers and a short VALU chain per byte.
-template <int XF, int TZC>
+template <typename T, int XF, int TZC>
 __global__ __launch_bounds__(256) void dw3q_dw_kernel(
-    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
+    const float* __restrict__ dz, long long dzns, const T* __restrict__ x, long long xns,
     const float* __restrict__ rec, float* __restrict__ dw_part, int N, int C, int D, int H, int W,
     int RB, int RPW, int ny, int TZ, int nz) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -620,7 +627,7 @@ __global__ __launch_bounds__(256) void dw3q_dw_kernel(
   const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
   const long long cofs = (long long)b.c * D * HW;
   const float* dzp = dz + (long long)b.n * dzns + cofs;
-  const float* xp = x + (long long)b.n * xns + cofs;
+  const T* xp = x + (long long)b.n * xns + cofs;
   float sc = 1.f, sh = 0.f, mu = 0.f;
   if (XF) {
     const float* r = rec + (long long)b.nc * kRec;
@@ -638,13 +645,13 @@ __global__ __launch_bounds__(256) void dw3q_dw_kernel(
   auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };
   const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
   auto dzq = [&](int z) {   // own dZ quad of plane z (clamped address, always issued)
-    return *reinterpret_cast<const f4*>(dzp + (long long)min(max(z, 0), D - 1) * HW + qofs);
+    return ldv4(dzp + (long long)min(max(z, 0), D - 1) * HW + qofs);
   };
-  QPre p0, p1;
+  QPre<T> p0, p1;
   q_fetch(p0, xp + zc(b.z0 - 1), qm);
   q_fetch(p1, xp + zc(b.z0), qm);
   f4 q0 = dzq(b.z0), q1 = dzq(b.z0 + 1);
-  auto step = [&](int t, QPre& pre, f4& q) {
+  auto step = [&](int t, QPre<T>& pre, f4& q) {
     const int za = b.z0 - 1 + t;   // A plane of this step
     float* buf = lds + (t & 1) * PP;
     q_commit<XF == 1>(pre, buf, qm, za >= zlo && za <= zhi, sc, mu, sh);
@@ -692,183 +699,6 @@ __global__ __launch_bounds__(256) void dw3q_dw_kernel(
     float r = 0.f;
     for (int k = 0; k < nw; ++k) r += red[k * 32 + threadIdx.x];
     dw_part[((long long)b.c * N * nchunk + (long long)b.n * nchunk + b.ck) * 27 + threadIdx.x] = r;
-  }
-}
-
-// MODE 0: dx = conv^T(dz);  MODE 1: fused IN/LeakyReLU/Dropout backward (dx = dpre, IN sums);
-// MODE 2: dx += conv^T(dz).  PD: register prefetch depth in planes (1 or 2).
-template <int MODE, int TZC, int PD = L3U_DWB_PD>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 2 : L3U_DWB_WAVES))) void dw3q_bwd_kernel(
-    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
-    const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
-    long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part,
-    int N, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int WQ = W >> 2, PP = (RB + 2) * W, HW = H * W;
-  const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
-  const long long cofs = (long long)b.c * D * HW;
-  const float* dzp = dz + (long long)b.n * dzns + cofs;
-  const float* xp = x + (long long)b.n * xns + cofs;
-  float* dxp = dx + (long long)b.n * dxns + cofs;
-  float* dzb = lds;             // 2 planes
-  float* ab = lds + 2 * PP;     // 2 planes
-  float wk[27];
-#pragma unroll
-  for (int t = 0; t < 27; ++t) wk[t] = w[b.c * 27 + t];
-  float sc = 1.f, sh = 0.f, kk = 1.f, mean = 0.f, rstd = 1.f;
-  if (MODE == 1) {
-    const float* r = rec + (long long)b.nc * kRec;
-    mean = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];
-  }
-  for (int i = threadIdx.x; i < 4 * PP; i += blockDim.x) lds[i] = 0.f;
-  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  f4 d0 = zero4, d1 = zero4, d2 = zero4;      // dA planes zd-1, zd, zd+1
-  f4 g0 = zero4, g1 = zero4, g2 = zero4;      // own dZ of planes zd-2, zd-1, zd (owned only)
-  f2 gw[27];   // dW taps as x-pair partial sums (.x + .y at the end)
-#pragma unroll
-  for (int t = 0; t < 27; ++t) gw[t] = f2{0.f, 0.f};
-  double s1 = 0.0, s2 = 0.0;
-  const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
-  const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
-  constexpr int nsteps = TZC + 3;   // compile-time step count: the step loop fully unrolls
-  QPre pz0, pa0, pz1, pa1;
-  const QMap qm = q_map(b.y0, b.rows, H, W, WQ);
-  auto in_rng = [&](int z) { return z >= zlo && z <= zhi; };
-  auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };  // clamped plane offset
-  {
-    const int zd = b.z0 - 1, za = zd - 1;
-    q_fetch(pz0, dzp + zc(zd), qm);
-    q_fetch(pa0, xp + zc(za), qm);
-    if (PD == 2) {
-      q_fetch(pz1, dzp + zc(zd + 1), qm);
-      q_fetch(pa1, xp + zc(za + 1), qm);
-    }
-  }
-  __syncthreads();
-  auto step = [&](int s, QPre& pz, QPre& pa) {
-    const int zd = b.z0 - 1 + s, za = zd - 1;
-    float* dbuf = dzb + (s & 1) * PP;
-    float* abuf = ab + (s & 1) * PP;
-    q_commit<false>(pz, dbuf, qm, in_rng(zd), 1.f, 0.f, 0.f);
-    q_commit<MODE == 1>(pa, abuf, qm, in_rng(za), sc, mean, sh);
-    // issue the loads of step s+PD and this step's epilogue load before the barrier; all loads
-    // are unconditional (clamped addresses) so the waits stay counted, never vmcnt(0)
-    q_fetch(pz, dzp + zc(zd + PD), qm);
-    q_fetch(pa, xp + zc(za + PD), qm);
-    const int zf = zd - 1;   // dA plane zf completes in this step
-    const bool fin = b.own && zf >= b.z0 && zf < b.z1;
-    f4 epi = zero4;
-    if (MODE != 0)
-      epi = *reinterpret_cast<const f4*>((MODE == 1 ? xp : dxp) + (long long)min(max(zf, 0), D - 1) * HW + qofs);
-    __syncthreads();
-    const bool zd_owned = b.own && zd >= b.z0 && zd < b.z1;
-    g0 = g1;
-    g1 = g2;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      float v[6];
-      q_nbr(dbuf, b.oy + r, W, b.ox, b.el, b.er, v);
-      if (r == 1) g2 = zd_owned ? f4{v[1], v[2], v[3], v[4]} : zero4;
-#pragma unroll
-      for (int dxi = 0; dxi < 3; ++dxi) {
-        const int tf = (2 - r) * 3 + (2 - dxi);   // flipped in-plane tap
-        const float w0 = wk[tf], w1 = wk[9 + tf], w2 = wk[18 + tf];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          d0[i] = fmaf(w0, v[i + dxi], d0[i]);
-          d1[i] = fmaf(w1, v[i + dxi], d1[i]);
-          d2[i] = fmaf(w2, v[i + dxi], d2[i]);
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      float u[6];
-      q_nbr(abuf, b.oy + r, W, b.ox, b.el, b.er, u);
-#pragma unroll
-      for (int dxi = 0; dxi < 3; ++dxi) {
-#if L3U_GW_SCALAR
-        float a = gw[r * 3 + dxi].x, bb = gw[9 + r * 3 + dxi].x, cc = gw[18 + r * 3 + dxi].x;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          a = fmaf(g2[i], u[i + dxi], a);     // dZ plane za+1 (kd=0)
-          bb = fmaf(g1[i], u[i + dxi], bb);   // dZ plane za   (kd=1)
-          cc = fmaf(g0[i], u[i + dxi], cc);   // dZ plane za-1 (kd=2)
-        }
-        gw[r * 3 + dxi].x = a;
-        gw[9 + r * 3 + dxi].x = bb;
-        gw[18 + r * 3 + dxi].x = cc;
-        continue;
-#endif
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {   // x-pairs (2h, 2h+1): one v_pk_fma_f32 per tap and kd
-          const f2 uu = {u[2 * h + dxi], u[2 * h + 1 + dxi]};
-          gw[r * 3 + dxi] = pfma(f2{g2[2 * h], g2[2 * h + 1]}, uu, gw[r * 3 + dxi]);            // kd=0
-          gw[9 + r * 3 + dxi] = pfma(f2{g1[2 * h], g1[2 * h + 1]}, uu, gw[9 + r * 3 + dxi]);    // kd=1
-          gw[18 + r * 3 + dxi] = pfma(f2{g0[2 * h], g0[2 * h + 1]}, uu, gw[18 + r * 3 + dxi]);  // kd=2
-        }
-      }
-    }
-    // pin the accumulators at the end of the step: without a use here the compiler sinks the
-    // dW FMAs (whose only use is the final reduction) past later barriers, keeping every
-    // step's LDS operands live at once
-#pragma unroll
-    for (int t = 0; t < 27; ++t) pin(gw[t]);
-    pin(d1);
-    pin(d2);
-    f4 o = d0;
-    if (MODE == 1) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float pre = fmaf(sc, epi[i] - mean, sh);
-        const float dp = o[i] * kk * lrelu_d(pre);
-        o[i] = dp;
-        s1 += fin ? (double)dp : 0.0;
-        s2 += fin ? (double)dp * ((epi[i] - mean) * rstd) : 0.0;
-      }
-    } else if (MODE == 2) {
-      o += epi;
-    }
-    if (fin) *reinterpret_cast<f4*>(dxp + (long long)zf * HW + qofs) = o;
-    d0 = d1;
-    d1 = d2;
-    d2 = zero4;
-  };
-#pragma unroll
-  for (int s = 0; s < nsteps; s += 2) {
-    step(s, pz0, pa0);
-    if (s + 1 < nsteps) {
-      if (PD == 2) step(s + 1, pz1, pa1);
-      else step(s + 1, pz0, pa0);
-    }
-  }
-  // workgroup reduction (fixed order) of the 27 taps and the 2 fp64 IN sums
-  __syncthreads();
-  float* red = lds;                                        // [nwaves][27]
-  double* redd = reinterpret_cast<double*>(lds + 4 * 32);  // [nwaves][2], after [4][32] floats
-  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, nw = blockDim.x >> 6;
-#pragma unroll
-  for (int t = 0; t < 27; ++t) {
-    const float r = wave_sum(gw[t].x + gw[t].y);
-    if (ln == 0) red[wv * 32 + t] = r;
-  }
-  if (MODE == 1) {
-    const double r1 = wave_sum_d(s1), r2 = wave_sum_d(s2);
-    if (ln == 0) { redd[wv * 2] = r1; redd[wv * 2 + 1] = r2; }
-  }
-  __syncthreads();
-  const int ck = b.ck;   // (zb, yb) chunk within (n, c)
-  const int nchunk = nz * ny;
-  if (threadIdx.x < 27) {
-    float r = 0.f;
-    for (int k = 0; k < nw; ++k) r += red[k * 32 + threadIdx.x];
-    dw_part[((long long)b.c * N * nchunk + (long long)b.n * nchunk + ck) * 27 + threadIdx.x] = r;
-  }
-  if (MODE == 1 && threadIdx.x >= 32 && threadIdx.x < 34) {
-    const int j = threadIdx.x - 32;
-    double r = 0.0;
-    for (int k = 0; k < nw; ++k) r += redd[k * 2 + j];
-    in_part[(((long long)b.c * N + b.n) * nchunk + ck) * 2 + j] = r;
   }
 }
 
@@ -941,7 +771,8 @@ L3U_DEV void q_row3(const float* plane, int row, int lp, int ox, bool el, bool e
 }
 
 // the same from an already-read quad m0 (neighbours by DPP, or from LDS in the padded layout)
-L3U_DEV void q_nbr3(const f4& m0, const float* plane, int row, int lp, int ox, bool el, bool er,
+template <typename LT>
+L3U_DEV void q_nbr3(const f4& m0, const LT* plane, int row, int lp, int ox, bool el, bool er,
                     f2& n2, f4& m, f2& p2) {
   m = m0;
 #if L3U_DWP_LDSNB
@@ -1016,19 +847,20 @@ L3U_DEV f2 pk_bc_s(f2 acc, f2 a, f2 b) {   // a wave-uniform (SGPR pair)
 #endif
 __device__ __attribute__((aligned(16))) float g_l3u_zero_page[256];   // 1 KiB of zeros (64 lanes x 16 B)
 
-L3U_DEV void glds16(const float* gsrc, unsigned lds_dst) {
+L3U_DEV void glds16(const void* gsrc, unsigned lds_dst) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
-// DMAs issued for plane step t (2 slots per loaded tensor; see gissue)
-template <int TZC>
-constexpr int gl_n(int t) { return 2 * ((t < TZC + 2 ? 1 : 0) + (t > 0 ? 1 : 0)); }
+// DMAs issued for plane step t (slots per loaded tensor: 2 for fp32, 1 for bf16 — NSD for dZ,
+// NSA for A; see gissue)
+template <int TZC, int NSD, int NSA>
+constexpr int gl_n(int t) { return NSD * (t < TZC + 2 ? 1 : 0) + NSA * (t > 0 ? 1 : 0); }
 // DMAs younger than plane step s's when step s waits for it (planes s+1 .. s+PD, if issued)
-template <int TZC, int PD>
+template <int TZC, int PD, int NSD, int NSA>
 constexpr int gl_younger(int s) {
   int n = 0;
-  for (int t = s + 1; t <= s + PD && t < TZC + 3; ++t) n += gl_n<TZC>(t);
+  for (int t = s + 1; t <= s + PD && t < TZC + 3; ++t) n += gl_n<TZC, NSD, NSA>(t);
   return n;
 }
 template <int NOUT>
@@ -1036,23 +868,31 @@ L3U_DEV void dw_wait_vm() {   // at most NOUT vector-memory operations still out
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NOUT) : "memory");
 }
 
-template <int MODE, int TZC, bool GL = false>
+// Gradients (dZ, dX) are fp32; the saved activation A is T (fp32, or bf16 in the bf16 network).
+// bf16 A on the LDS-DMA path: the DMA moves raw bf16, 8 elements (two quads) per lane, so one
+// slot per plane covers the 128-quad tile (needs an even quad count per row, W % 8 == 0, so a
+// lane's pair never straddles a row); that LDS image is bf16 and its rows widen at the read.
+template <typename T, int MODE, int TZC, bool GL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE == 1 ? L3U_DWG_WAVES1 : L3U_DWG_WAVES) : L3U_DWP_WAVES))) void dw3p_bwd_kernel(
-    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
+    const float* __restrict__ dz, long long dzns, const T* __restrict__ x, long long xns,
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
     long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part,
     int N, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  using LTA = std::conditional_t<GL, T, float>;        // LDS element type of the A image
+  constexpr bool BH = GL && sizeof(T) == 2;
+  constexpr int NSA = BH ? 1 : 2;                      // DMA slots per A plane (dZ: 2)
   const int WQ = W >> 2, LP = W + kLPad, PP = (RB + 2) * LP, HW = H * W;
   const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
   const long long cofs = (long long)b.c * D * HW;
   const float* dzp = dz + (long long)b.n * dzns + cofs;
-  const float* xp = x + (long long)b.n * xns + cofs;
+  const T* xp = x + (long long)b.n * xns + cofs;
   float* dxp = dx + (long long)b.n * dxns + cofs;
-  float* dzb = lds;             // 2 planes
-  float* ab = lds + 2 * PP;     // 2 planes
   constexpr int GNB = L3U_DWG_PD + 1;                  // DMA ring buffers per tensor
-  const int GPS = (RB + 2) * W;                        // floats per ring buffer (nq quads)
+  const int GPSD = (RB + 2) * W;                       // dZ elements per ring buffer (nq quads)
+  const int GPSA = BH ? 512 : (RB + 2) * W;            // A elements per ring buffer
+  float* const dzl = lds;                              // dZ planes
+  LTA* const al = reinterpret_cast<LTA*>(lds + (GL ? GNB * GPSD : 2 * PP));   // A planes
   // flipped data-gradient taps: pair (kd 0, kd 1) and kd 2 per in-plane tap (r, dx)
   f2 wp[9];
   float w2[9];
@@ -1084,7 +924,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
   const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
   // register staging PD planes ahead (sets alternate by step parity when PD = 2)
   constexpr int PD = GL ? 1 : L3U_DWP_PD;
-  QPre pzs[PD], pas[PD];
+  QPre<float> pzs[PD];
+  QPre<T> pas[PD];
   const QMap qm = q_map(b.y0, b.rows, H, W, WQ, LP, kLOfs);
   auto in_rng = [&](int z) { return z >= zlo && z <= zhi; };
   auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };
@@ -1093,24 +934,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
 #pragma unroll
   for (int r = 0; r < 3; ++r) rv[r] = (unsigned)(b.y0 + b.oy + r - 1) < (unsigned)H ? 1.f : 0.f;
   const float* zpage = g_l3u_zero_page + 4 * (threadIdx.x & 63);
+  // bf16: lane l moves quads 2l, 2l+1 of the tile (same row: W % 8 == 0)
+  int goff2 = 0;
+  bool ok2 = false;
+  if (BH) {
+    const int qp = 2 * (int)(threadIdx.x & 63), lr2 = qp / WQ, y2 = b.y0 - 1 + lr2;
+    ok2 = qp < (RB + 2) * WQ && y2 >= 0 && y2 < H;
+    goff2 = min(max(y2, 0), H - 1) * W + (qp - lr2 * WQ) * 4;
+  }
   // DMA of plane step t (dZ plane z0-1+t, A plane z0-2+t) into ring buffer t % GNB.  Step 0's A
   // plane and the last step's dZ plane are never used: not loaded (gl_n gives the DMA count).
   // Slot 1 is issued by the lanes of its nq - 64 quads only (nq > 64 for one-wave tiles, so the
   // instruction always issues and the count stays static).
   const int nq = (RB + 2) * WQ;
-  auto gissue = [&](auto T) {
-    constexpr int t = decltype(T)::value;
+  auto gissue = [&](auto TI) {
+    constexpr int t = decltype(TI)::value;
     const int z_d = b.z0 - 1 + t, z_a = z_d - 1;
     const bool ind = in_rng(z_d), ina = in_rng(z_a);
-    const unsigned bz = lbase + (unsigned)((t % GNB) * GPS) * 4u;
-    const unsigned ba = lbase + (unsigned)((GNB + t % GNB) * GPS) * 4u;
+    const unsigned bz = lbase + (unsigned)((t % GNB) * GPSD) * 4u;
+    const unsigned ba = (unsigned)(size_t)al + (unsigned)((t % GNB) * GPSA) * (unsigned)sizeof(T);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       if (k == 1 && (int)threadIdx.x >= nq - 64) continue;
-      const float* sd = (qm.ok[k] && ind) ? dzp + (long long)z_d * HW + qm.goff[k] : zpage;
-      const float* sa = (qm.ok[k] && ina) ? xp + (long long)z_a * HW + qm.goff[k] : zpage;
+      const void* sd = (qm.ok[k] && ind) ? (const void*)(dzp + (long long)z_d * HW + qm.goff[k]) : (const void*)zpage;
       if constexpr (t < TZC + 2) glds16(sd, bz + k * 1024u);
-      if constexpr (t > 0) glds16(sa, ba + k * 1024u);
+      if constexpr (!BH) {
+        const void* sa = (qm.ok[k] && ina) ? (const void*)(xp + (long long)z_a * HW + qm.goff[k]) : (const void*)zpage;
+        if constexpr (t > 0) glds16(sa, ba + k * 1024u);
+      }
+    }
+    if constexpr (BH) {
+      const void* sa = (ok2 && ina) ? (const void*)(xp + (long long)z_a * HW + goff2) : (const void*)zpage;
+      if constexpr (t > 0) glds16(sa, ba);
     }
   };
   if constexpr (GL) {
@@ -1125,8 +980,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
   __syncthreads();
   auto step = [&](auto I) {
     constexpr int s = decltype(I)::value;
-    QPre& pz = pzs[s % PD];
-    QPre& pa = pas[s % PD];
+    QPre<float>& pz = pzs[s % PD];
+    QPre<T>& pa = pas[s % PD];
     // planes of the slab are z0 .. z0+TZC-1 (z1 may cut it short at run time)
     constexpr bool doP = s >= 1 && s <= TZC + 1;    // dA planes zd-1 / zd touch the slab
     constexpr bool doS = s <= TZC - 1;              // dA plane zd+1 in the slab
@@ -1135,17 +990,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
     constexpr bool use2 = s >= 3 && s <= TZC + 2;   // dZ plane zd-2 owned
     constexpr bool fin = s >= 2 && s <= TZC + 1;    // dA plane zd-1 completes in the slab
     const int zd = b.z0 - 1 + s, za = zd - 1;
-    float* dbuf = GL ? lds + (s % GNB) * GPS : dzb + (s & 1) * PP;
-    float* abuf = GL ? lds + (GNB + s % GNB) * GPS : ab + (s & 1) * PP;
+    float* dbuf = GL ? dzl + (s % GNB) * GPSD : dzl + (s & 1) * PP;
+    LTA* abuf = GL ? al + (s % GNB) * GPSA : al + (s & 1) * PP;
     if constexpr (GL) {
       // issue plane s + PD (its ring buffer was last read in step s - 1), then wait for plane s:
       // younger than plane s's 4 DMAs are those of planes s+1 .. s+PD (stores between them only
       // make the wait longer)
       if constexpr (s + L3U_DWG_PD < TZC + 3) gissue(std::integral_constant<int, s + L3U_DWG_PD>{});
-      dw_wait_vm<gl_younger<TZC, L3U_DWG_PD>(s)>();
+      dw_wait_vm<gl_younger<TZC, L3U_DWG_PD, 2, NSA>(s)>();
     } else {
       q_commit<false>(pz, dbuf, qm, in_rng(zd), 1.f, 0.f, 0.f);
-      q_commit<MODE == 1>(pa, abuf, qm, in_rng(za), sc, mean, sh);
+      q_commit<MODE == 1>(pa, (float*)abuf, qm, in_rng(za), sc, mean, sh);
       if constexpr (s + PD < TZC + 3) {
         q_fetch(pz, dzp + zc(zd + PD), qm);
         q_fetch(pa, xp + zc(za + PD), qm);
@@ -1154,16 +1009,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
     const int zf = zd - 1;
     f4 epi = zero4;
     // GL + MODE 1: the pre-IN activation of plane zf = za is the tile's own raw A row in LDS
-    if constexpr (MODE != 0 && fin && !(GL && MODE == 1))
-      epi = *reinterpret_cast<const f4*>((MODE == 1 ? xp : dxp) + (long long)min(max(zf, 0), D - 1) * HW + qofs);
+    if constexpr (MODE == 1 && fin && !GL)
+      epi = ldv4(xp + (long long)min(max(zf, 0), D - 1) * HW + qofs);
+    if constexpr (MODE == 2 && fin)
+      epi = ldv4(dxp + (long long)min(max(zf, 0), D - 1) * HW + qofs);
     __syncthreads();
     // all six LDS rows of the step are read up front (one latency for the step, not three)
     constexpr bool needD = doP || doS || own0, needA = own0 || use1 || use2;
     f4 rowd[3], rowa[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      if (needD) rowd[r] = *reinterpret_cast<const f4*>(dbuf + (b.oy + r) * LP + kLOfs + b.ox);
-      if (needA) rowa[r] = *reinterpret_cast<const f4*>(abuf + (b.oy + r) * LP + kLOfs + b.ox);
+      if (needD) rowd[r] = ldv4(dbuf + (b.oy + r) * LP + kLOfs + b.ox);
+      if (needA) rowa[r] = ldv4(abuf + (b.oy + r) * LP + kLOfs + b.ox);
     }
     f4 pre1 = zero4, d1 = zero4;   // GL + MODE 1: own row's pre-activation and (y - mean)
     if constexpr (GL && MODE == 1 && needA) {
@@ -1263,9 +1120,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
         o += epi;
       }
       if (st) {
-        f4* dst = reinterpret_cast<f4*>(dxp + (long long)zf * HW + qofs);
-        if (GL && L3U_DWP_NT) __builtin_nontemporal_store(o, dst);   // streamed out, not re-read
-        else *dst = o;
+        float* dst = dxp + (long long)zf * HW + qofs;
+        if (GL && L3U_DWP_NT) stv4_nt(dst, o);   // streamed out, not re-read
+        else stv4(dst, o);
       }
     }
 #if L3U_DWP_PIN
@@ -1336,15 +1193,15 @@ bool use_volume(int D, int H, int W) { return (long long)(D + 2) * (H + 2) * (W 
 #endif
 
 // load volume `src` (transformed if XF) into the padded LDS image; the halo is zero
-template <bool XF>
-L3U_DEV void v_load(float* L, const float* __restrict__ src, int D, int H, int W, float sc, float mu,
+template <bool XF, typename T>
+L3U_DEV void v_load(float* L, const T* __restrict__ src, int D, int H, int W, float sc, float mu,
                     float sh) {
   const int PW = W + 2, PH = H + 2, PV = (D + 2) * PH * PW;
   for (int i = threadIdx.x; i < PV; i += blockDim.x) {
     const int x = i % PW - 1, t = i / PW, y = t % PH - 1, z = t / PH - 1;
     float v = 0.f;
     if (x >= 0 && x < W && y >= 0 && y < H && z >= 0 && z < D) {
-      v = src[((long long)z * H + y) * W + x];
+      v = ld1(src + ((long long)z * H + y) * W + x);
       if (XF) v = lrelu(fmaf(sc, v - mu, sh));
     }
     L[i] = v;
@@ -1353,11 +1210,11 @@ L3U_DEV void v_load(float* L, const float* __restrict__ src, int D, int H, int W
 
 // y = conv(x) (EPI 0, taps as given) or the data gradient (EPI 1: dpre epilogue + IN sums,
 // 2: y += conv^T, 3: y = conv^T; flipped taps), one (n, c) per workgroup
-template <int XF, int EPI>
+template <typename T, int XF, int EPI>
 __global__ __launch_bounds__(256) void dwv_fwd_kernel(
-    const float* __restrict__ x, long long xns, const float* __restrict__ w,
-    const float* __restrict__ rec, l3u_norm_src src, int has_src, float* __restrict__ y,
-    long long yns, const float* __restrict__ ep, long long epns, double* __restrict__ in_part,
+    const T* __restrict__ x, long long xns, const float* __restrict__ w,
+    const float* __restrict__ rec, l3u_norm_src src, int has_src, T* __restrict__ y,
+    long long yns, const T* __restrict__ ep, long long epns, double* __restrict__ in_part,
     int N, int C, int D, int H, int W) {
   constexpr bool FLIP = EPI != 0;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1381,8 +1238,8 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
   v_load<XF == 1>(lds, x + (long long)n * xns + cofs, D, H, W, sc, mu, sh);
   __syncthreads();
   const int PW = W + 2, PHW = (H + 2) * PW;
-  float* yp = y + (long long)n * yns + cofs;
-  const float* epp = (EPI == 1 || EPI == 2) ? ep + (long long)n * epns + cofs : nullptr;
+  T* yp = y + (long long)n * yns + cofs;
+  const T* epp = (EPI == 1 || EPI == 2) ? ep + (long long)n * epns + cofs : nullptr;
   float s1 = 0.f, s2 = 0.f;
   for (int v = threadIdx.x; v < S; v += blockDim.x) {
     const int xx = v % W, t = v / W, yy = t % H, zz = t / H;
@@ -1395,15 +1252,15 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) o = fmaf(wk[dz * 9 + dy * 3 + dx], b[dz * PHW + dy * PW + dx], o);
     if (EPI == 1) {
-      const float e = epp[v];
+      const float e = ld1(epp + v);
       const float pre = fmaf(sc, e - mu, sh);
       o = o * kk * lrelu_d(pre);
       s1 += o;
       s2 += o * ((e - mu) * rstd);
     } else if (EPI == 2) {
-      o += epp[v];
+      o += ld1(epp + v);
     }
-    yp[v] = o;
+    st1(yp + v, o);
   }
   if (EPI == 1) {
     __syncthreads();
@@ -1420,64 +1277,14 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
   }
 }
 
-// dw_part[c][n][27] = sum_v dZ(v) * A(v + tap), A = x (XF 0) or lrelu(IN(x)) (XF 1)
-template <int XF>
-__global__ __launch_bounds__(256) void dwv_dw_kernel(
-    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
-    const float* __restrict__ rec, float* __restrict__ dw_part, int N, int C, int D, int H, int W) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int nc = blockIdx.x, c = nc % C, n = nc / C;
-  const long long HW = (long long)H * W, S = D * HW, cofs = (long long)c * S;
-  float sc = 1.f, sh = 0.f, mu = 0.f;
-  if (XF) {
-    const float* r = rec + (long long)nc * kRec;
-    mu = r[0]; sc = r[2]; sh = r[3];
-  }
-  v_load<XF == 1>(lds, x + (long long)n * xns + cofs, D, H, W, sc, mu, sh);
-  __syncthreads();
-  const int PW = W + 2, PHW = (H + 2) * PW;
-  const float* dzp = dz + (long long)n * dzns + cofs;
-  float gw[27];
-#pragma unroll
-  for (int t = 0; t < 27; ++t) gw[t] = 0.f;
-  for (int v = threadIdx.x; v < S; v += blockDim.x) {
-    const int xx = v % W, t = v / W, yy = t % H, zz = t / H;
-    const float* b = lds + zz * PHW + yy * PW + xx;
-    const float g = dzp[v];
-#pragma unroll
-    for (int dz2 = 0; dz2 < 3; ++dz2)
-#pragma unroll
-      for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx) {
-          const int tp = dz2 * 9 + dy * 3 + dx;
-          gw[tp] = fmaf(g, b[dz2 * PHW + dy * PW + dx], gw[tp]);
-        }
-  }
-  __syncthreads();
-  float* red = lds;   // [4 waves][32]
-  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, nw = blockDim.x >> 6;
-#pragma unroll
-  for (int t = 0; t < 27; ++t) {
-    const float r = wave_sum(gw[t]);
-    if (ln == 0) red[wv * 32 + t] = r;
-  }
-  __syncthreads();
-  if (threadIdx.x < 27) {
-    float r = 0.f;
-    for (int k = 0; k < nw; ++k) r += red[k * 32 + threadIdx.x];
-    dw_part[((long long)c * N + n) * 27 + threadIdx.x] = r;
-  }
-}
-
 // Both backward halves of the whole-volume form in ONE launch (6^3 level, where each launch is
 // latency): the (n, c) volumes of dZ and of A (= x, or lrelu(IN(x)) in MODE 1) sit in LDS side
 // by side; each thread forms the flipped-tap data gradient of its voxels (MODE 1: the IN-fused
 // dpre epilogue and IN sums; 2: accumulate; 0: overwrite) and the 27 weight-gradient products.
 // Same per-voxel arithmetic as dwv_fwd_kernel<0, EPI> + dwv_dw_kernel<XF>.
-template <int MODE>
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void dwv_bwd_kernel(
-    const float* __restrict__ dz, long long dzns, const float* __restrict__ x, long long xns,
+    const float* __restrict__ dz, long long dzns, const T* __restrict__ x, long long xns,
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
     long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part, int N, int C, int D,
     int H, int W) {
@@ -1498,7 +1305,7 @@ __global__ __launch_bounds__(256) void dwv_bwd_kernel(
   v_load<false>(dzl, dz + (long long)n * dzns + cofs, D, H, W, 1.f, 0.f, 0.f);
   v_load<MODE == 1>(al, x + (long long)n * xns + cofs, D, H, W, sc, mu, sh);
   __syncthreads();
-  const float* xp = x + (long long)n * xns + cofs;
+  const T* xp = x + (long long)n * xns + cofs;
   float* dxp = dx + (long long)n * dxns + cofs;
   float gw[27];
 #pragma unroll
@@ -1528,15 +1335,15 @@ __global__ __launch_bounds__(256) void dwv_bwd_kernel(
           gw[tp] = fmaf(g, ba[dzz * PHW + dy * PW + dxx], gw[tp]);
         }
     if (MODE == 1) {
-      const float e = xp[v];
+      const float e = ld1(xp + v);
       const float pre = fmaf(sc, e - mu, sh);
       o = o * kk * lrelu_d(pre);
       s1 += o;
       s2 += o * ((e - mu) * rstd);
     } else if (MODE == 2) {
-      o += dxp[v];
+      o += ld1(dxp + v);
     }
-    dxp[v] = o;
+    st1(dxp + v, o);
   }
   __syncthreads();
   float* red = lds;                                        // [4 waves][32]
@@ -1569,30 +1376,28 @@ __global__ __launch_bounds__(256) void dwv_bwd_kernel(
 
 #define DW_DISPATCH_P(KERNEL, MODE, ...)                                               \
   do {                                                                                 \
-    if (P <= 1) hipLaunchKernelGGL((KERNEL<MODE, 1>), __VA_ARGS__);                    \
-    else if (P <= 2) hipLaunchKernelGGL((KERNEL<MODE, 2>), __VA_ARGS__);               \
-    else if (P <= 3) hipLaunchKernelGGL((KERNEL<MODE, 3>), __VA_ARGS__);               \
-    else if (P <= 4) hipLaunchKernelGGL((KERNEL<MODE, 4>), __VA_ARGS__);               \
-    else if (P <= 6) hipLaunchKernelGGL((KERNEL<MODE, 6>), __VA_ARGS__);               \
-    else if (P <= 9) hipLaunchKernelGGL((KERNEL<MODE, 9>), __VA_ARGS__);               \
-    else if (P <= 12) hipLaunchKernelGGL((KERNEL<MODE, 12>), __VA_ARGS__);             \
-    else hipLaunchKernelGGL((KERNEL<MODE, 16>), __VA_ARGS__);                          \
+    if (P <= 1) hipLaunchKernelGGL((KERNEL<T, MODE, 1>), __VA_ARGS__);                 \
+    else if (P <= 2) hipLaunchKernelGGL((KERNEL<T, MODE, 2>), __VA_ARGS__);            \
+    else if (P <= 3) hipLaunchKernelGGL((KERNEL<T, MODE, 3>), __VA_ARGS__);            \
+    else if (P <= 4) hipLaunchKernelGGL((KERNEL<T, MODE, 4>), __VA_ARGS__);            \
+    else if (P <= 6) hipLaunchKernelGGL((KERNEL<T, MODE, 6>), __VA_ARGS__);            \
+    else if (P <= 9) hipLaunchKernelGGL((KERNEL<T, MODE, 9>), __VA_ARGS__);            \
+    else if (P <= 12) hipLaunchKernelGGL((KERNEL<T, MODE, 12>), __VA_ARGS__);          \
+    else hipLaunchKernelGGL((KERNEL<T, MODE, 16>), __VA_ARGS__);                       \
   } while (0)
 
-extern "C" {
+namespace {
 
-int l3u_dw3_nchunk(int N, int C, int D, int H, int W) {
-  if (use_volume(D, H, W)) return 1;
-  if (use_quads(H, W)) {
-    const QGeom g = qgeom(N, C, D, H, W);
-    return g.nz * g.ny;
-  }
-  return (D + pick_tz(D) - 1) / pick_tz(D);
+// the LDS-DMA single-pass backward takes one-wave tiles of <= 128 quads; bf16 moves quad pairs
+bool dw_gl(const QGeom& g, int W, int esize) {
+  return L3U_DWG && g.threads == 64 && (g.RB + 2) * g.WQ <= 128 && g.WQ * 4 == W &&
+         (esize == 4 || g.WQ % 2 == 0);
 }
 
-int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float* rec,
-                const l3u_norm_src* src, float* y, long long y_nstride, int N, int C, int D,
-                int H, int W, hipStream_t stream) {
+template <typename T>
+int dw3_fwd_impl(const T* x, long long x_nstride, const float* w, const float* rec,
+                 const l3u_norm_src* src, T* y, long long y_nstride, int N, int C, int D, int H,
+                 int W, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && D > 0 && H > 0 && W > 0);
   const l3u_norm_src z{};
   const l3u_norm_src s = src ? *src : z;
@@ -1601,8 +1406,8 @@ int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float
   if (use_volume(D, H, W)) {
     size_t lds = (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
     if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);
-    if (xf) hipLaunchKernelGGL((dwv_fwd_kernel<1, 0>), dim3(N * C), dim3(256), lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W);
-    else hipLaunchKernelGGL((dwv_fwd_kernel<0, 0>), dim3(N * C), dim3(256), lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W);
+    if (xf) hipLaunchKernelGGL((dwv_fwd_kernel<T, 1, 0>), dim3(N * C), dim3(256), lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W);
+    else hipLaunchKernelGGL((dwv_fwd_kernel<T, 0, 0>), dim3(N * C), dim3(256), lds, stream, x, x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W);
     L3U_CHECK_LAUNCH();
   }
   if (use_quads(H, W) && x_nstride % 4 == 0 && y_nstride % 4 == 0) {
@@ -1610,7 +1415,7 @@ int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float
     size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
     if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);   // reduction scratch
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
-#define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<M_, 0, T_>), grid, block, lds, stream, x, \
+#define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<T, T, M_, 0, T_>), grid, block, lds, stream, x, \
       x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W, g.RB, g.RPW, \
       g.ny, g.TZ, g.nz)
     if (xf) { TZ24(DWQF(1, 24)) if (g.TZ == 16) DWQF(1, 16); else if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
@@ -1628,64 +1433,42 @@ int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float
   L3U_CHECK_LAUNCH();
 }
 
-}  // extern "C"
-
-namespace {
-
-// parts: 1 = data gradient (dx, IN-backward sums), 2 = weight gradient (dw_part), 3 = both
-int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
-                   const float* w, const float* rec, float* dx, long long dx_nstride,
-                   int accumulate, float* dw_part, double* in_part, int N, int C, int D, int H,
-                   int W, int parts, hipStream_t stream) {
+// data gradient (dx, IN-backward sums) and weight-gradient partials (dw_part) in one call
+template <typename T>
+int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_nstride,
+                 const float* w, const float* rec, float* dx, long long dx_nstride, int accumulate,
+                 float* dw_part, double* in_part, int N, int C, int D, int H, int W,
+                 hipStream_t stream) {
+  constexpr int E = (int)sizeof(T);
   L3U_REQUIRE(N > 0 && C > 0 && D > 0 && H > 0 && W > 0);
-  L3U_REQUIRE(!(parts & 1) || dx != nullptr);
-  L3U_REQUIRE(!(parts & 2) || dw_part != nullptr);
-  L3U_REQUIRE(!(parts & 1) || rec == nullptr || in_part != nullptr);
+  L3U_REQUIRE(dx != nullptr && dw_part != nullptr);
+  L3U_REQUIRE(rec == nullptr || in_part != nullptr);
   L3U_REQUIRE(rec == nullptr || accumulate == 0);
-  if (use_volume(D, H, W)) {
-    size_t lds = (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
-    if (lds < 128 * sizeof(float)) lds = 128 * sizeof(float);
-    if (parts == 3 && L3U_DWV_FUSED) {   // both halves in one launch
-      size_t lds2 = 2 * (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
-      if (lds2 < 160 * sizeof(float)) lds2 = 160 * sizeof(float);
-#define DWVB(M_) hipLaunchKernelGGL((dwv_bwd_kernel<M_>), dim3(N * C), dim3(256), lds2, stream, dz, \
+  if (use_volume(D, H, W)) {   // data + weight gradient in one launch
+    size_t lds2 = 2 * (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
+    if (lds2 < 160 * sizeof(float)) lds2 = 160 * sizeof(float);
+#define DWVB(M_) hipLaunchKernelGGL((dwv_bwd_kernel<T, M_>), dim3(N * C), dim3(256), lds2, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W)
-      if (rec) DWVB(1);
-      else if (accumulate) DWVB(2);
-      else DWVB(0);
+    if (rec) DWVB(1);
+    else if (accumulate) DWVB(2);
+    else DWVB(0);
 #undef DWVB
-      L3U_CHECK_LAUNCH();
-    }
-    if (parts & 1) {
-      const l3u_norm_src z{};
-#define DWVX(E_) hipLaunchKernelGGL((dwv_fwd_kernel<0, E_>), dim3(N * C), dim3(256), lds, stream, dz, \
-      dz_nstride, w, rec, z, 0, dx, dx_nstride, (E_ == 1 ? x : dx), (E_ == 1 ? x_nstride : dx_nstride), \
-      in_part, N, C, D, H, W)
-      if (rec) DWVX(1);
-      else if (accumulate) DWVX(2);
-      else DWVX(3);
-#undef DWVX
-    }
-    if (parts & 2) {
-      if (rec) hipLaunchKernelGGL((dwv_dw_kernel<1>), dim3(N * C), dim3(256), lds, stream, dz, dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W);
-      else hipLaunchKernelGGL((dwv_dw_kernel<0>), dim3(N * C), dim3(256), lds, stream, dz, dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W);
-    }
     L3U_CHECK_LAUNCH();
   }
   if (use_quads(H, W) && x_nstride % 4 == 0 && dz_nstride % 4 == 0 && dx_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
-    const bool gl = L3U_DWG && g.threads == 64 && (g.RB + 2) * g.WQ <= 128 && g.WQ * 4 == W;
+    const bool gl = dw_gl(g, W, E);
     // MODE 1 (IN-fused) only on the LDS-DMA variant: register-staged it measured faster split
-    if (L3U_DW_FUSED && parts == 3 && (rec == nullptr || (gl && L3U_DWG_MODE1))) {
+    if (L3U_DW_FUSED && (rec == nullptr || (gl && L3U_DWG_MODE1))) {
       // single pass: data + weight gradient from one read of dZ and A
       size_t lds = 4 * (size_t)(g.RB + 2) * (W + kLPad) * sizeof(float);
       if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch
-      if (gl) lds = 2 * (L3U_DWG_PD + 1) * (size_t)(g.RB + 2) * g.WQ * 16;
-#define DWPB(M_, T_) do { if (gl) hipLaunchKernelGGL((dw3p_bwd_kernel<M_, T_, true>), grid, block, lds, stream, dz, \
+      if (gl) lds = (L3U_DWG_PD + 1) * ((size_t)(g.RB + 2) * g.WQ * 16 + (E == 4 ? (size_t)(g.RB + 2) * g.WQ * 16 : 1024));
+#define DWPB(M_, T_) do { if (gl) hipLaunchKernelGGL((dw3p_bwd_kernel<T, M_, T_, true>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
       g.RPW, g.ny, g.TZ, g.nz); \
-      else hipLaunchKernelGGL((dw3p_bwd_kernel<M_, T_>), grid, block, lds, stream, dz, \
+      else hipLaunchKernelGGL((dw3p_bwd_kernel<T, M_, T_>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
       g.RPW, g.ny, g.TZ, g.nz); } while (0)
 #define DWPB_T(M_) do { TZ24(DWPB(M_, 24)) if (g.TZ == 16) DWPB(M_, 16); else if (g.TZ == 8) DWPB(M_, 8); else if (g.TZ == 4) DWPB(M_, 4); else DWPB(M_, 2); } while (0)
@@ -1696,89 +1479,59 @@ int dw3_bwd_launch(const float* dz, long long dz_nstride, const float* x, long l
 #undef DWPB
       L3U_CHECK_LAUNCH();
     }
-    if (dw_split(H, W) || parts != 3) {
-      // data gradient = the forward stencil with flipped taps (+ epilogue), then the weight
-      // gradient on its own; both use the same tile geometry, so the chunking of dw_part /
-      // in_part is identical to the fused kernel's
-      if (parts & 1) {
-        const l3u_norm_src z{};
-        size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
-        if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);
-#define DWQX(E_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<0, E_, T_>), grid, block, lds, stream, dz, \
-      dz_nstride, w, rec, z, 0, dx, dx_nstride, (E_ == 1 ? x : dx), (E_ == 1 ? x_nstride : dx_nstride), \
-      in_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
-#define DWQX_T(E_) do { TZ24(DWQX(E_, 24)) if (g.TZ == 16) DWQX(E_, 16); else if (g.TZ == 8) DWQX(E_, 8); else if (g.TZ == 4) DWQX(E_, 4); else DWQX(E_, 2); } while (0)
-        if (rec) DWQX_T(1);
-        else if (accumulate) DWQX_T(2);
-        else DWQX_T(3);
-#undef DWQX_T
+    // IN-fused on register-staged tiles: the data gradient = the forward stencil with flipped
+    // taps and the dpre epilogue, then the weight gradient on its own; both use the same tile
+    // geometry, so the chunking of dw_part / in_part is identical to the single pass's
+    {
+      const l3u_norm_src z{};
+      size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
+      if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);
+#define DWQX(T_) hipLaunchKernelGGL((dw3q_fwd_kernel<float, T, 0, 1, T_>), grid, block, lds, stream, dz, \
+      dz_nstride, w, rec, z, 0, dx, dx_nstride, x, x_nstride, in_part, N, C, D, H, W, g.RB, g.RPW, \
+      g.ny, g.TZ, g.nz)
+      TZ24(DWQX(24)) if (g.TZ == 16) DWQX(16); else if (g.TZ == 8) DWQX(8); else if (g.TZ == 4) DWQX(4); else DWQX(2);
 #undef DWQX
-      }
-      if (parts & 2) {
-        size_t lds2 = 2 * (size_t)(g.RB + 2) * W * sizeof(float);
-        if (lds2 < 128 * sizeof(float)) lds2 = 128 * sizeof(float);
-#define DWQW(X_, T_) hipLaunchKernelGGL((dw3q_dw_kernel<X_, T_>), grid, block, lds2, stream, dz, \
-      dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
-#define DWQW_T(X_) do { TZ24(DWQW(X_, 24)) if (g.TZ == 16) DWQW(X_, 16); else if (g.TZ == 8) DWQW(X_, 8); else if (g.TZ == 4) DWQW(X_, 4); else DWQW(X_, 2); } while (0)
-        if (rec) DWQW_T(1);
-        else DWQW_T(0);
-#undef DWQW_T
-#undef DWQW
-      }
-      L3U_CHECK_LAUNCH();
     }
-    size_t lds = 4 * (size_t)(g.RB + 2) * W * sizeof(float);
-    if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch
-#define DWQB(M_, T_) hipLaunchKernelGGL((dw3q_bwd_kernel<M_, T_>), grid, block, lds, stream, dz, \
-      dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
-      g.RPW, g.ny, g.TZ, g.nz)
-#define DWQB_T(M_) do { TZ24(DWQB(M_, 24)) if (g.TZ == 16) DWQB(M_, 16); else if (g.TZ == 8) DWQB(M_, 8); else if (g.TZ == 4) DWQB(M_, 4); else DWQB(M_, 2); } while (0)
-    if (rec) DWQB_T(1);
-    else if (accumulate) DWQB_T(2);
-    else DWQB_T(0);
-#undef DWQB_T
-#undef DWQB
+    {
+      size_t lds2 = 2 * (size_t)(g.RB + 2) * W * sizeof(float);
+      if (lds2 < 128 * sizeof(float)) lds2 = 128 * sizeof(float);
+#define DWQW(T_) hipLaunchKernelGGL((dw3q_dw_kernel<T, 1, T_>), grid, block, lds2, stream, dz, \
+      dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
+      TZ24(DWQW(24)) if (g.TZ == 16) DWQW(16); else if (g.TZ == 8) DWQW(8); else if (g.TZ == 4) DWQW(4); else DWQW(2);
+#undef DWQW
+    }
     L3U_CHECK_LAUNCH();
   }
-  // small / odd planes: one fused kernel; a partial call only skips the other part's stores
+  // small / odd planes: one fused kernel
   L3U_REQUIRE(H * W <= 4096);
   const int TZ = pick_tz(D), nchunk = (D + TZ - 1) / TZ;
   const int P = (H * W + 255) / 256;
   size_t lds = 4 * (size_t)(H + 2) * (W + 2) * sizeof(float);
   if (lds < 128 * sizeof(float)) lds = 128 * sizeof(float);   // reduction scratch
   dim3 grid(N * C * nchunk), block(256);
-  float* dxs = (parts & 1) ? dx : nullptr;
-  float* dws = (parts & 2) ? dw_part : nullptr;
-  if (rec) DW_DISPATCH_P(dw3_bwd_kernel, 1, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dxs, dx_nstride, accumulate, dws, in_part, N, C, D, H, W, TZ, nchunk);
-  else DW_DISPATCH_P(dw3_bwd_kernel, 0, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dxs, dx_nstride, accumulate, dws, in_part, N, C, D, H, W, TZ, nchunk);
+  if (rec) DW_DISPATCH_P(dw3_bwd_kernel, 1, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part, in_part, N, C, D, H, W, TZ, nchunk);
+  else DW_DISPATCH_P(dw3_bwd_kernel, 0, grid, block, lds, stream, dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part, in_part, N, C, D, H, W, TZ, nchunk);
   L3U_CHECK_LAUNCH();
 }
 
 }  // namespace
 
-extern "C" {
-
-int l3u_dw3_bwd(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
-                const float* w, const float* rec, float* dx, long long dx_nstride, int accumulate,
-                float* dw_part, double* in_part, int N, int C, int D, int H, int W,
-                hipStream_t stream) {
-  return dw3_bwd_launch(dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, dw_part,
-                        in_part, N, C, D, H, W, 3, stream);
+extern "C" int l3u_dw3_nchunk(int N, int C, int D, int H, int W) {
+  if (use_volume(D, H, W)) return 1;
+  if (use_quads(H, W)) {
+    const QGeom g = qgeom(N, C, D, H, W);
+    return g.nz * g.ny;
+  }
+  return (D + pick_tz(D) - 1) / pick_tz(D);
 }
 
-int l3u_dw3_bwd_data(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
-                     const float* w, const float* rec, float* dx, long long dx_nstride,
-                     int accumulate, double* in_part, int N, int C, int D, int H, int W,
-                     hipStream_t stream) {
-  return dw3_bwd_launch(dz, dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, accumulate, nullptr,
-                        in_part, N, C, D, H, W, 1, stream);
-}
-
-int l3u_dw3_bwd_weight(const float* dz, long long dz_nstride, const float* x, long long x_nstride,
-                       const float* w, const float* rec, float* dw_part, int N, int C, int D,
-                       int H, int W, hipStream_t stream) {
-  return dw3_bwd_launch(dz, dz_nstride, x, x_nstride, w, rec, nullptr, dz_nstride, 0, dw_part,
-                        nullptr, N, C, D, H, W, 2, stream);
-}
-
-}  // extern "C"
+#define P_DWF(TT) (const TT* x, long long x_nstride, const float* w, const float* rec,            \
+    const l3u_norm_src* src, TT* y, long long y_nstride, int N, int C, int D, int H, int W,          \
+    hipStream_t stream)
+L3U_TWIN(l3u_dw3_fwd, P_DWF, dw3_fwd_impl(bp(x), x_nstride, w, rec, src, bp(y), y_nstride, N, C, D, H,
+         W, stream))
+#define P_DWB(TT) (const float* dz, long long dz_nstride, const TT* x, long long x_nstride,        \
+    const float* w, const float* rec, float* dx, long long dx_nstride, int accumulate, float* dw_part, \
+    double* in_part, int N, int C, int D, int H, int W, hipStream_t stream)
+L3U_TWIN(l3u_dw3_bwd, P_DWB, dw3_bwd_impl(dz, dz_nstride, bp(x), x_nstride, w, rec, dx, dx_nstride,
+         accumulate, dw_part, in_part, N, C, D, H, W, stream))

@@ -29,11 +29,11 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(l3u_norm_src src, int 
 // out = lrelu(scale2*(y2-mean2) + shift2 + R),  R = r (identity) or scale_r*(r-mean_r) + shift_r.
 // With HAS_SRC the records are finalized here from the GEMM partials (no in_finalize launch);
 // workgroup x == 0 of each (n, c) stores them for the backward.
-template <bool VEC, bool HAS_SRC>
+template <typename T, bool VEC, bool HAS_SRC>
 __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
-    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2, l3u_norm_src src2,
-    const float* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
-    int shortcut, float* __restrict__ out, long long ons, int C, int S) {
+    const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2, l3u_norm_src src2,
+    const T* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
+    int shortcut, T* __restrict__ out, long long ons, int C, int S) {
   __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f;
@@ -51,20 +51,20 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
       br = recr[(long long)nc * kRec + 3];
     }
   }
-  const float* yp = y2 + (long long)n * y2ns + (long long)c * S;
-  const float* rp = r + (long long)n * rns + (long long)c * S;
-  float* op = out + (long long)n * ons + (long long)c * S;
+  const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
+  const T* rp = r + (long long)n * rns + (long long)c * S;
+  T* op = out + (long long)n * ons + (long long)c * S;
   if (VEC) {
     for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += gridDim.x * 1024) {
-      const f4 yv = *reinterpret_cast<const f4*>(yp + i), rv = *reinterpret_cast<const f4*>(rp + i);
+      const f4 yv = ldv4(yp + i), rv = ldv4(rp + i);
       f4 o;
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = lrelu(fmaf(a2, yv[q] - m2, b2) + fmaf(ar, rv[q] - mr, br));
-      *reinterpret_cast<f4*>(op + i) = o;
+      stv4(op + i, o);
     }
   } else {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256)
-      op[i] = lrelu(fmaf(a2, yp[i] - m2, b2) + fmaf(ar, rp[i] - mr, br));
+      st1(op + i, lrelu(fmaf(a2, ld1(yp + i) - m2, b2) + fmaf(ar, ld1(rp + i) - mr, br)));
   }
 }
 
@@ -73,11 +73,11 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
 // (four float4 rows), stores them and the two window maxima (float2) with their argmax bytes.
 // Same scan order and comparison as maxpool2_fwd_v_kernel (misc.hip).  Needs even D, H and
 // W % 4 == 0.
-template <bool HAS_SRC>
+template <typename T, bool HAS_SRC>
 __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
-    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2, l3u_norm_src src2,
-    const float* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
-    int shortcut, float* __restrict__ out, long long ons, float* __restrict__ pooled,
+    const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2, l3u_norm_src src2,
+    const T* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
+    int shortcut, T* __restrict__ out, long long ons, T* __restrict__ pooled,
     long long pns, unsigned char* __restrict__ idx, int C, int D, int H, int W) {
   __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
@@ -99,10 +99,10 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
   const long long S = (long long)D * H * W;
   const int Ho = H / 2, W4 = W / 4;
   const long long So = (long long)(D / 2) * Ho * (W / 2), Sp = So / 2;
-  const float* yp = y2 + (long long)n * y2ns + (long long)c * S;
-  const float* rp = r + (long long)n * rns + (long long)c * S;
-  float* op = out + (long long)n * ons + (long long)c * S;
-  float2* pp = reinterpret_cast<float2*>(pooled + (long long)n * pns + (long long)c * So);
+  const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
+  const T* rp = r + (long long)n * rns + (long long)c * S;
+  T* op = out + (long long)n * ons + (long long)c * S;
+  T* pp = pooled + (long long)n * pns + (long long)c * So;
   unsigned short* ip = reinterpret_cast<unsigned short*>(idx + (long long)nc * So);
   for (long long o = blockIdx.x * 256ll + threadIdx.x; o < Sp; o += (long long)gridDim.x * 256) {
     const int q = (int)(o % W4), t = (int)(o / W4), oy = t % Ho, oz = t / Ho;
@@ -111,10 +111,13 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const long long off = base + ((long long)(j >> 1) * H + (j & 1)) * W;
-      const f4 yv = *reinterpret_cast<const f4*>(yp + off), rv = *reinterpret_cast<const f4*>(rp + off);
+      const f4 yv = ldv4(yp + off), rv = ldv4(rp + off);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[j][e] = lrelu(fmaf(a2, yv[e] - m2, b2) + fmaf(ar, rv[e] - mr, br));
-      *reinterpret_cast<f4*>(op + off) = v[j];
+      stv4(op + off, v[j]);
+      // the pooled maxima are taken over the values as stored (bf16: rounded), so that the
+      // pooled tensor equals MaxPool3d of `out`
+      v[j] = round_to(v[j], (const T*)nullptr);
     }
     float b0 = v[0][0], b1 = v[0][2];
     int i0 = 0, i1 = 0;
@@ -127,17 +130,17 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
         if (u0 > b0 || u0 != u0) { b0 = u0; i0 = 2 * j + dx; }
         if (u1 > b1 || u1 != u1) { b1 = u1; i1 = 2 * j + dx; }
       }
-    pp[o] = make_float2(b0, b1);
+    stv2(pp + 2 * o, f2_t{b0, b1});
     ip[o] = (unsigned short)(i0 | (i1 << 8));
   }
 }
 
 // partials per (c, n, block): [sum g, sum g*xhat2, sum g*xhat_r],  g = dout * lrelu'(out)
-template <bool VEC>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
-    const float* __restrict__ dout, long long dns, const float* __restrict__ out, long long ons,
-    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
-    const float* __restrict__ r, long long rns, const float* __restrict__ recr,
+    const float* __restrict__ dout, long long dns, const T* __restrict__ out, long long ons,
+    const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
+    const T* __restrict__ r, long long rns, const float* __restrict__ recr,
     double* __restrict__ part, int N, int C, int S) {
   __shared__ double red[4];
   const int nc = blockIdx.y, c = nc % C, n = nc / C, nb = gridDim.x;
@@ -146,16 +149,16 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
   if (recr) { mr = recr[(long long)nc * kRec + 0]; rsr = recr[(long long)nc * kRec + 1]; }
   const long long co = (long long)c * S;
   const float* dp = dout + (long long)n * dns + co;
-  const float* op = out + (long long)n * ons + co;
-  const float* yp = y2 + (long long)n * y2ns + co;
-  const float* rp = r + (long long)n * rns + co;
+  const T* op = out + (long long)n * ons + co;
+  const T* yp = y2 + (long long)n * y2ns + co;
+  const T* rp = r + (long long)n * rns + co;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
   if (VEC) {
     for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += nb * 1024) {
-      const f4 dv = *reinterpret_cast<const f4*>(dp + i), ov = *reinterpret_cast<const f4*>(op + i);
-      const f4 yv = *reinterpret_cast<const f4*>(yp + i);
+      const f4 dv = ldv4(dp + i), ov = ldv4(op + i);
+      const f4 yv = ldv4(yp + i);
       f4 rv = f4{0.f, 0.f, 0.f, 0.f};
-      if (recr) rv = *reinterpret_cast<const f4*>(rp + i);
+      if (recr) rv = ldv4(rp + i);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float g = dv[q] * lrelu_d(ov[q]);
@@ -166,10 +169,10 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     }
   } else {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += nb * 256) {
-      const float g = dp[i] * lrelu_d(op[i]);
+      const float g = ld1(dp + i) * lrelu_d(ld1(op + i));
       s0 += g;
-      s1 += (double)g * ((yp[i] - m2) * rs2);
-      if (recr) s2 += (double)g * ((rp[i] - mr) * rsr);
+      s1 += (double)g * ((ld1(yp + i) - m2) * rs2);
+      if (recr) s2 += (double)g * ((ld1(rp + i) - mr) * rsr);
     }
   }
   s0 = block_sum256d(s0, red);
@@ -182,11 +185,11 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
 }
 
 // dy2 = rstd2*g2*(g - M0 - xhat2*M1);  dr = shortcut ? rstd_r*g_r*(g - M0 - xhat_r*M2) : g
-template <bool VEC>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void norm_act_bwd_apply_kernel(
-    const float* __restrict__ dout, long long dns, const float* __restrict__ out, long long ons,
-    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
-    const float* __restrict__ r, long long rns, const float* __restrict__ recr,
+    const float* __restrict__ dout, long long dns, const T* __restrict__ out, long long ons,
+    const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
+    const T* __restrict__ r, long long rns, const float* __restrict__ recr,
     const double* __restrict__ part, int npart, float* __restrict__ dy2, long long dy2ns,
     float* __restrict__ dr, long long drns, int N, int C, int S) {
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
@@ -201,17 +204,17 @@ __global__ __launch_bounds__(256) void norm_act_bwd_apply_kernel(
   if (recr) { const float* qr = recr + (long long)nc * kRec; mur = qr[0]; rsr = qr[1]; fr = qr[1] * qr[5]; }
   const long long co = (long long)c * S;
   const float* dp = dout + (long long)n * dns + co;
-  const float* op = out + (long long)n * ons + co;
-  const float* yp = y2 + (long long)n * y2ns + co;
-  const float* rp = r + (long long)n * rns + co;
+  const T* op = out + (long long)n * ons + co;
+  const T* yp = y2 + (long long)n * y2ns + co;
+  const T* rp = r + (long long)n * rns + co;
   float* d2 = dy2 + (long long)n * dy2ns + co;
   float* drp = dr + (long long)n * drns + co;
   if (VEC) {
     for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += gridDim.x * 1024) {
-      const f4 dv = *reinterpret_cast<const f4*>(dp + i), ov = *reinterpret_cast<const f4*>(op + i);
-      const f4 yv = *reinterpret_cast<const f4*>(yp + i);
+      const f4 dv = ldv4(dp + i), ov = ldv4(op + i);
+      const f4 yv = ldv4(yp + i);
       f4 rv = f4{0.f, 0.f, 0.f, 0.f};
-      if (recr) rv = *reinterpret_cast<const f4*>(rp + i);
+      if (recr) rv = ldv4(rp + i);
       f4 o2, orr;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -219,14 +222,14 @@ __global__ __launch_bounds__(256) void norm_act_bwd_apply_kernel(
         o2[q] = f2 * (g - M0 - (yv[q] - mu2) * rs2 * M1);
         orr[q] = recr ? fr * (g - M0 - (rv[q] - mur) * rsr * M2) : g;
       }
-      *reinterpret_cast<f4*>(d2 + i) = o2;
-      *reinterpret_cast<f4*>(drp + i) = orr;
+      stv4(d2 + i, o2);
+      stv4(drp + i, orr);
     }
   } else {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256) {
-      const float g = dp[i] * lrelu_d(op[i]);
-      d2[i] = f2 * (g - M0 - (yp[i] - mu2) * rs2 * M1);
-      drp[i] = recr ? fr * (g - M0 - (rp[i] - mur) * rsr * M2) : g;
+      const float g = ld1(dp + i) * lrelu_d(ld1(op + i));
+      st1(d2 + i, f2 * (g - M0 - (ld1(yp + i) - mu2) * rs2 * M1));
+      st1(drp + i, recr ? fr * (g - M0 - (ld1(rp + i) - mur) * rsr * M2) : g);
     }
   }
 }
@@ -235,11 +238,11 @@ __global__ __launch_bounds__(256) void norm_act_bwd_apply_kernel(
 // the 12^3 / 6^3 levels, where a launch costs more than the work): the three plane sums are
 // workgroup sums held by every thread, stored as the single partial, then applied.  Same values,
 // bit for bit, as the reduce + apply pair (the apply's fixed-order merge of one partial is exact).
-template <bool VEC>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
-    const float* __restrict__ dout, long long dns, const float* __restrict__ out, long long ons,
-    const float* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
-    const float* __restrict__ r, long long rns, const float* __restrict__ recr,
+    const float* __restrict__ dout, long long dns, const T* __restrict__ out, long long ons,
+    const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
+    const T* __restrict__ r, long long rns, const float* __restrict__ recr,
     double* __restrict__ part, float* __restrict__ dy2, long long dy2ns, float* __restrict__ dr,
     long long drns, int N, int C, int S) {
   __shared__ double red[4];
@@ -250,16 +253,16 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
   if (recr) { const float* qr = recr + (long long)nc * kRec; mr = qr[0]; rsr = qr[1]; fr = qr[1] * qr[5]; }
   const long long co = (long long)c * S;
   const float* dp = dout + (long long)n * dns + co;
-  const float* op = out + (long long)n * ons + co;
-  const float* yp = y2 + (long long)n * y2ns + co;
-  const float* rp = r + (long long)n * rns + co;
+  const T* op = out + (long long)n * ons + co;
+  const T* yp = y2 + (long long)n * y2ns + co;
+  const T* rp = r + (long long)n * rns + co;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
   if (VEC) {
     for (int i = threadIdx.x * 4; i < S; i += 1024) {
-      const f4 dv = *reinterpret_cast<const f4*>(dp + i), ov = *reinterpret_cast<const f4*>(op + i);
-      const f4 yv = *reinterpret_cast<const f4*>(yp + i);
+      const f4 dv = ldv4(dp + i), ov = ldv4(op + i);
+      const f4 yv = ldv4(yp + i);
       f4 rv = f4{0.f, 0.f, 0.f, 0.f};
-      if (recr) rv = *reinterpret_cast<const f4*>(rp + i);
+      if (recr) rv = ldv4(rp + i);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float g = dv[q] * lrelu_d(ov[q]);
@@ -270,10 +273,10 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
     }
   } else {
     for (int i = threadIdx.x; i < S; i += 256) {
-      const float g = dp[i] * lrelu_d(op[i]);
+      const float g = ld1(dp + i) * lrelu_d(ld1(op + i));
       s0 += g;
-      s1 += (double)g * ((yp[i] - m2) * rs2);
-      if (recr) s2 += (double)g * ((rp[i] - mr) * rsr);
+      s1 += (double)g * ((ld1(yp + i) - m2) * rs2);
+      if (recr) s2 += (double)g * ((ld1(rp + i) - mr) * rsr);
     }
   }
   s0 = block_sum256d(s0, red);
@@ -288,10 +291,10 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
   float* drp = dr + (long long)n * drns + co;
   if (VEC) {
     for (int i = threadIdx.x * 4; i < S; i += 1024) {
-      const f4 dv = *reinterpret_cast<const f4*>(dp + i), ov = *reinterpret_cast<const f4*>(op + i);
-      const f4 yv = *reinterpret_cast<const f4*>(yp + i);
+      const f4 dv = ldv4(dp + i), ov = ldv4(op + i);
+      const f4 yv = ldv4(yp + i);
       f4 rv = f4{0.f, 0.f, 0.f, 0.f};
-      if (recr) rv = *reinterpret_cast<const f4*>(rp + i);
+      if (recr) rv = ldv4(rp + i);
       f4 o2, orr;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -299,23 +302,23 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
         o2[q] = f2 * (g - M0 - (yv[q] - m2) * rs2 * M1);
         orr[q] = recr ? fr * (g - M0 - (rv[q] - mr) * rsr * M2) : g;
       }
-      *reinterpret_cast<f4*>(d2 + i) = o2;
-      *reinterpret_cast<f4*>(drp + i) = orr;
+      stv4(d2 + i, o2);
+      stv4(drp + i, orr);
     }
   } else {
     for (int i = threadIdx.x; i < S; i += 256) {
-      const float g = dp[i] * lrelu_d(op[i]);
-      d2[i] = f2 * (g - M0 - (yp[i] - m2) * rs2 * M1);
-      drp[i] = recr ? fr * (g - M0 - (rp[i] - mr) * rsr * M2) : g;
+      const float g = ld1(dp + i) * lrelu_d(ld1(op + i));
+      st1(d2 + i, f2 * (g - M0 - (ld1(yp + i) - m2) * rs2 * M1));
+      st1(drp + i, recr ? fr * (g - M0 - (ld1(rp + i) - mr) * rsr * M2) : g);
     }
   }
 }
 
 // InstanceNorm backward apply for the inner norm (after dw3_bwd MODE 1 produced dpre + sums):
 // dy = rstd*gamma*(dpre - M1 - xhat*M2); in-place allowed (dy == dpre)
-template <bool VEC>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void in_bwd_apply_kernel(
-    const float* dpre, long long dns, const float* __restrict__ y, long long yns,
+    const float* dpre, long long dns, const T* __restrict__ y, long long yns,
     const float* __restrict__ rec, const double* __restrict__ part, int npart, float* dy,
     long long dyns, int N, int C, int S) {
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
@@ -328,19 +331,19 @@ __global__ __launch_bounds__(256) void in_bwd_apply_kernel(
   const float mu = q[0], rs = q[1], f = q[1] * q[5];
   const long long co = (long long)c * S;
   const float* dp = dpre + (long long)n * dns + co;
-  const float* yp = y + (long long)n * yns + co;
+  const T* yp = y + (long long)n * yns + co;
   float* op = dy + (long long)n * dyns + co;
   if (VEC) {
     for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += gridDim.x * 1024) {
-      const f4 dv = *reinterpret_cast<const f4*>(dp + i), yv = *reinterpret_cast<const f4*>(yp + i);
+      const f4 dv = ldv4(dp + i), yv = ldv4(yp + i);
       f4 o;
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = f * (dv[k] - M1 - (yv[k] - mu) * rs * M2);
-      *reinterpret_cast<f4*>(op + i) = o;
+      stv4(op + i, o);
     }
   } else {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256)
-      op[i] = f * (dp[i] - M1 - (yp[i] - mu) * rs * M2);
+      st1(op + i, f * (ld1(dp + i) - M1 - (ld1(yp + i) - mu) * rs * M2));
   }
 }
 
@@ -373,17 +376,22 @@ int l3u_in_finalize(const float* stat_part, int nsb, const float* gamma, const f
 
 int l3u_norm_act_nblocks(int S) { return elem_blocks(S); }
 
-int l3u_norm_act_fwd(const float* y2, long long y2_nstride, const float* rec2,
-                     const l3u_norm_src* src2, const float* r, long long r_nstride,
-                     const float* rec_r, const l3u_norm_src* src_r, int shortcut, float* out,
-                     long long out_nstride, int N, int C, int S, hipStream_t stream) {
+}  // extern "C"
+
+namespace {
+
+template <typename T>
+int norm_act_fwd_impl(const T* y2, long long y2_nstride, const float* rec2,
+                      const l3u_norm_src* src2, const T* r, long long r_nstride,
+                      const float* rec_r, const l3u_norm_src* src_r, int shortcut, T* out,
+                      long long out_nstride, int N, int C, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
   L3U_REQUIRE(src2 ? (!shortcut || src_r) : (rec2 && (!shortcut || rec_r)));
   const bool vec = S % 4 == 0 && y2_nstride % 4 == 0 && r_nstride % 4 == 0 && out_nstride % 4 == 0;
   dim3 grid(elem_blocks(S), N * C);
   const l3u_norm_src z{};
   const l3u_norm_src s2 = src2 ? *src2 : z, sr = src_r ? *src_r : z;
-#define NAF(V_, S_) hipLaunchKernelGGL((norm_act_fwd_kernel<V_, S_>), grid, dim3(256), 0, stream, y2, \
+#define NAF(V_, S_) hipLaunchKernelGGL((norm_act_fwd_kernel<T, V_, S_>), grid, dim3(256), 0, stream, y2, \
       y2_nstride, rec2, s2, r, r_nstride, rec_r, sr, shortcut, out, out_nstride, C, S)
   if (src2) { if (vec) NAF(true, true); else NAF(false, true); }
   else { if (vec) NAF(true, false); else NAF(false, false); }
@@ -391,23 +399,25 @@ int l3u_norm_act_fwd(const float* y2, long long y2_nstride, const float* rec2,
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_norm_act_pool_fwd(const float* y2, long long y2_nstride, const float* rec2,
-                          const l3u_norm_src* src2, const float* r, long long r_nstride,
-                          const float* rec_r, const l3u_norm_src* src_r, int shortcut, float* out,
-                          long long out_nstride, float* pooled, long long pooled_nstride,
-                          unsigned char* idx, int N, int C, int D, int H, int W,
-                          hipStream_t stream) {
+template <typename T>
+int norm_act_pool_fwd_impl(const T* y2, long long y2_nstride, const float* rec2,
+                           const l3u_norm_src* src2, const T* r, long long r_nstride,
+                           const float* rec_r, const l3u_norm_src* src_r, int shortcut, T* out,
+                           long long out_nstride, T* pooled, long long pooled_nstride,
+                           unsigned char* idx, int N, int C, int D, int H, int W,
+                           hipStream_t stream) {
+  constexpr int E = (int)sizeof(T);
   L3U_REQUIRE(N > 0 && C > 0 && D >= 2 && H >= 2 && W >= 4);
   L3U_REQUIRE(src2 ? (!shortcut || src_r) : (rec2 && (!shortcut || rec_r)));
   L3U_REQUIRE(!(D & 1) && !(H & 1) && !(W & 3) && y2_nstride % 4 == 0 && r_nstride % 4 == 0 &&
-              out_nstride % 4 == 0 && pooled_nstride % 2 == 0 && ((uintptr_t)y2 & 15) == 0 &&
-              ((uintptr_t)r & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
-              ((uintptr_t)pooled & 7) == 0 && ((uintptr_t)idx & 1) == 0);
+              out_nstride % 4 == 0 && pooled_nstride % 2 == 0 && ((uintptr_t)y2 & (4 * E - 1)) == 0 &&
+              ((uintptr_t)r & (4 * E - 1)) == 0 && ((uintptr_t)out & (4 * E - 1)) == 0 &&
+              ((uintptr_t)pooled & (2 * E - 1)) == 0 && ((uintptr_t)idx & 1) == 0);
   const long long S = (long long)D * H * W;
   dim3 grid(elem_blocks((int)S), N * C);
   const l3u_norm_src z{};
   const l3u_norm_src s2 = src2 ? *src2 : z, sr = src_r ? *src_r : z;
-#define NAP(S_) hipLaunchKernelGGL((norm_act_pool_fwd_kernel<S_>), grid, dim3(256), 0, stream, y2, \
+#define NAP(S_) hipLaunchKernelGGL((norm_act_pool_fwd_kernel<T, S_>), grid, dim3(256), 0, stream, y2, \
       y2_nstride, rec2, s2, r, r_nstride, rec_r, sr, shortcut, out, out_nstride, pooled, \
       pooled_nstride, idx, C, D, H, W)
   if (src2) NAP(true);
@@ -416,61 +426,105 @@ int l3u_norm_act_pool_fwd(const float* y2, long long y2_nstride, const float* re
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_norm_act_bwd_reduce(const float* dout, long long dout_nstride, const float* out,
-                            long long out_nstride, const float* y2, long long y2_nstride,
-                            const float* rec2, const float* r, long long r_nstride,
-                            const float* rec_r, double* part, int N, int C, int S,
-                            hipStream_t stream) {
+template <typename T>
+int norm_act_bwd_reduce_impl(const float* dout, long long dout_nstride, const T* out,
+                             long long out_nstride, const T* y2, long long y2_nstride,
+                             const float* rec2, const T* r, long long r_nstride,
+                             const float* rec_r, double* part, int N, int C, int S,
+                             hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
   const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
                    y2_nstride % 4 == 0 && r_nstride % 4 == 0;
   dim3 grid(elem_blocks(S), N * C);
-  if (vec) hipLaunchKernelGGL(norm_act_bwd_reduce_kernel<true>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S);
-  else hipLaunchKernelGGL(norm_act_bwd_reduce_kernel<false>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S);
+  if (vec) hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S);
+  else hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, false>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S);
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_norm_act_bwd_apply(const float* dout, long long dout_nstride, const float* out,
-                           long long out_nstride, const float* y2, long long y2_nstride,
-                           const float* rec2, const float* r, long long r_nstride,
-                           const float* rec_r, const double* part, float* dy2,
-                           long long dy2_nstride, float* dr, long long dr_nstride, int N, int C,
-                           int S, hipStream_t stream) {
+template <typename T>
+int norm_act_bwd_apply_impl(const float* dout, long long dout_nstride, const T* out,
+                            long long out_nstride, const T* y2, long long y2_nstride,
+                            const float* rec2, const T* r, long long r_nstride,
+                            const float* rec_r, const double* part, float* dy2,
+                            long long dy2_nstride, float* dr, long long dr_nstride, int N, int C,
+                            int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
   const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
                    y2_nstride % 4 == 0 && r_nstride % 4 == 0 && dy2_nstride % 4 == 0 &&
                    dr_nstride % 4 == 0;
   const int npart = elem_blocks(S);
   dim3 grid(npart, N * C);
-  if (vec) hipLaunchKernelGGL(norm_act_bwd_apply_kernel<true>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, npart, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
-  else hipLaunchKernelGGL(norm_act_bwd_apply_kernel<false>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, npart, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
+  if (vec) hipLaunchKernelGGL((norm_act_bwd_apply_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, npart, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
+  else hipLaunchKernelGGL((norm_act_bwd_apply_kernel<T, false>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, npart, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_norm_act_bwd(const float* dout, long long dout_nstride, const float* out,
-                     long long out_nstride, const float* y2, long long y2_nstride,
-                     const float* rec2, const float* r, long long r_nstride, const float* rec_r,
-                     double* part, float* dy2, long long dy2_nstride, float* dr,
-                     long long dr_nstride, int N, int C, int S, hipStream_t stream) {
+template <typename T>
+int norm_act_bwd_impl(const float* dout, long long dout_nstride, const T* out,
+                      long long out_nstride, const T* y2, long long y2_nstride,
+                      const float* rec2, const T* r, long long r_nstride, const float* rec_r,
+                      double* part, float* dy2, long long dy2_nstride, float* dr,
+                      long long dr_nstride, int N, int C, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0 && elem_blocks(S) == 1);
   const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
                    y2_nstride % 4 == 0 && r_nstride % 4 == 0 && dy2_nstride % 4 == 0 &&
                    dr_nstride % 4 == 0;
   dim3 grid(1, N * C);
-  if (vec) hipLaunchKernelGGL(norm_act_bwd_one_kernel<true>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
-  else hipLaunchKernelGGL(norm_act_bwd_one_kernel<false>, grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
+  if (vec) hipLaunchKernelGGL((norm_act_bwd_one_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
+  else hipLaunchKernelGGL((norm_act_bwd_one_kernel<T, false>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_in_bwd_apply(const float* dpre, long long dpre_nstride, const float* y, long long y_nstride,
-                     const float* rec, const double* in_part, int npart, float* dy,
-                     long long dy_nstride, int N, int C, int S, hipStream_t stream) {
+template <typename T>
+int in_bwd_apply_impl(const float* dpre, long long dpre_nstride, const T* y, long long y_nstride,
+                      const float* rec, const double* in_part, int npart, float* dy,
+                      long long dy_nstride, int N, int C, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0 && npart > 0);
   const bool vec = S % 4 == 0 && dpre_nstride % 4 == 0 && y_nstride % 4 == 0 && dy_nstride % 4 == 0;
   dim3 grid(elem_blocks(S), N * C);
-  if (vec) hipLaunchKernelGGL(in_bwd_apply_kernel<true>, grid, dim3(256), 0, stream, dpre, dpre_nstride, y, y_nstride, rec, in_part, npart, dy, dy_nstride, N, C, S);
-  else hipLaunchKernelGGL(in_bwd_apply_kernel<false>, grid, dim3(256), 0, stream, dpre, dpre_nstride, y, y_nstride, rec, in_part, npart, dy, dy_nstride, N, C, S);
+  if (vec) hipLaunchKernelGGL((in_bwd_apply_kernel<T, true>), grid, dim3(256), 0, stream, dpre, dpre_nstride, y, y_nstride, rec, in_part, npart, dy, dy_nstride, N, C, S);
+  else hipLaunchKernelGGL((in_bwd_apply_kernel<T, false>), grid, dim3(256), 0, stream, dpre, dpre_nstride, y, y_nstride, rec, in_part, npart, dy, dy_nstride, N, C, S);
   L3U_CHECK_LAUNCH();
 }
 
-}  // extern "C"
+}  // namespace
+
+// ---- C-ABI: fp32 entry points and their _bf16 twins (include/l3u.h) ----------------------------
+#define P_NAF(TT) (const TT* y2, long long y2_nstride, const float* rec2, const l3u_norm_src* src2, \
+    const TT* r, long long r_nstride, const float* rec_r, const l3u_norm_src* src_r, int shortcut,  \
+    TT* out, long long out_nstride, int N, int C, int S, hipStream_t stream)
+L3U_TWIN(l3u_norm_act_fwd, P_NAF, norm_act_fwd_impl(bp(y2), y2_nstride, rec2, src2, bp(r), r_nstride,
+         rec_r, src_r, shortcut, bp(out), out_nstride, N, C, S, stream))
+#define P_NAP(TT) (const TT* y2, long long y2_nstride, const float* rec2, const l3u_norm_src* src2, \
+    const TT* r, long long r_nstride, const float* rec_r, const l3u_norm_src* src_r, int shortcut,  \
+    TT* out, long long out_nstride, TT* pooled, long long pooled_nstride, unsigned char* idx, int N, \
+    int C, int D, int H, int W, hipStream_t stream)
+L3U_TWIN(l3u_norm_act_pool_fwd, P_NAP, norm_act_pool_fwd_impl(bp(y2), y2_nstride, rec2, src2, bp(r),
+         r_nstride, rec_r, src_r, shortcut, bp(out), out_nstride, bp(pooled), pooled_nstride, idx, N,
+         C, D, H, W, stream))
+#define P_NBR(TT) (const float* dout, long long dout_nstride, const TT* out, long long out_nstride,   \
+    const TT* y2, long long y2_nstride, const float* rec2, const TT* r, long long r_nstride,        \
+    const float* rec_r, double* part, int N, int C, int S, hipStream_t stream)
+L3U_TWIN(l3u_norm_act_bwd_reduce, P_NBR, norm_act_bwd_reduce_impl(dout, dout_nstride, bp(out),
+         out_nstride, bp(y2), y2_nstride, rec2, bp(r), r_nstride, rec_r, part, N, C, S, stream))
+#define P_NBA(TT) (const float* dout, long long dout_nstride, const TT* out, long long out_nstride,   \
+    const TT* y2, long long y2_nstride, const float* rec2, const TT* r, long long r_nstride,        \
+    const float* rec_r, const double* part, float* dy2, long long dy2_nstride, float* dr,          \
+    long long dr_nstride, int N, int C, int S, hipStream_t stream)
+L3U_TWIN(l3u_norm_act_bwd_apply, P_NBA, norm_act_bwd_apply_impl(dout, dout_nstride, bp(out),
+         out_nstride, bp(y2), y2_nstride, rec2, bp(r), r_nstride, rec_r, part, dy2, dy2_nstride,
+         dr, dr_nstride, N, C, S, stream))
+#define P_NB1(TT) (const float* dout, long long dout_nstride, const TT* out, long long out_nstride,   \
+    const TT* y2, long long y2_nstride, const float* rec2, const TT* r, long long r_nstride,        \
+    const float* rec_r, double* part, float* dy2, long long dy2_nstride, float* dr,                 \
+    long long dr_nstride,                                                                            \
+    int N, int C, int S, hipStream_t stream)
+L3U_TWIN(l3u_norm_act_bwd, P_NB1, norm_act_bwd_impl(dout, dout_nstride, bp(out), out_nstride,
+         bp(y2), y2_nstride, rec2, bp(r), r_nstride, rec_r, part, dy2, dy2_nstride, dr,
+         dr_nstride, N, C, S, stream))
+#define P_IBA(TT) (const float* dpre, long long dpre_nstride, const TT* y, long long y_nstride,    \
+    const float* rec, const double* in_part, int npart, float* dy, long long dy_nstride, int N,      \
+    int C,                                                                                           \
+    int S, hipStream_t stream)
+L3U_TWIN(l3u_in_bwd_apply, P_IBA, in_bwd_apply_impl(dpre, dpre_nstride, bp(y), y_nstride, rec,
+         in_part, npart, dy, dy_nstride, N, C, S, stream))

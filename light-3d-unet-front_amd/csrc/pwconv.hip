@@ -30,19 +30,19 @@ L3U_DEV f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x1
 // src[co][2z+a][2y+b][2x+c], channel stride 8S, dims (Dq, Hq, Wq) = the input (low-res) volume.
 // With W % 4 == 0 the 4 voxels share an output row: two float4 loads of 8 consecutive floats and
 // an even/odd pick.
-template <bool VEC, bool GATHER>
-L3U_DEV f4 load_x4(const float* __restrict__ xn, int kk, int K, int s, int lim, int S, int Hq,
+template <bool VEC, bool GATHER, typename T>
+L3U_DEV f4 load_x4(const T* __restrict__ xn, int kk, int K, int s, int lim, int S, int Hq,
                    int Wq) {   // voxels >= lim (<= S) read as zero
   f4 a = {0.f, 0.f, 0.f, 0.f};
   if (kk >= K) return a;
   if (GATHER) {
     const int a_ = (kk >> 2) & 1, b_ = (kk >> 1) & 1, c_ = kk & 1;
-    const float* base = xn + (long long)(kk >> 3) * (8ll * S);
+    const T* base = xn + (long long)(kk >> 3) * (8ll * S);
     if (VEC) {
       if (s < lim) {
         const int x = s % Wq, t = s / Wq, y = t % Hq, z = t / Hq;
-        const float* p = base + ((long long)(2 * z + a_) * (2 * Hq) + (2 * y + b_)) * (2 * Wq) + 2 * x;
-        const f4 lo = *reinterpret_cast<const f4*>(p), hi = *reinterpret_cast<const f4*>(p + 4);
+        const T* p = base + ((long long)(2 * z + a_) * (2 * Hq) + (2 * y + b_)) * (2 * Wq) + 2 * x;
+        const f4 lo = ldv4(p), hi = ldv4(p + 4);
         a = c_ ? f4{lo[1], lo[3], hi[1], hi[3]} : f4{lo[0], lo[2], hi[0], hi[2]};
       }
     } else {
@@ -50,18 +50,18 @@ L3U_DEV f4 load_x4(const float* __restrict__ xn, int kk, int K, int s, int lim, 
       for (int q = 0; q < 4; ++q)
         if (s + q < lim) {
           const int x = (s + q) % Wq, t = (s + q) / Wq, y = t % Hq, z = t / Hq;
-          a[q] = base[((long long)(2 * z + a_) * (2 * Hq) + (2 * y + b_)) * (2 * Wq) + 2 * x + c_];
+          a[q] = ld1(base + ((long long)(2 * z + a_) * (2 * Hq) + (2 * y + b_)) * (2 * Wq) + 2 * x + c_);
         }
     }
     return a;
   }
-  const float* src = xn + (long long)kk * S + s;
+  const T* src = xn + (long long)kk * S + s;
   if (VEC) {
-    if (s < lim) a = *reinterpret_cast<const f4*>(src);
+    if (s < lim) a = ldv4(src);
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (s + q < lim) a[q] = src[q];
+      if (s + q < lim) a[q] = ld1(src + q);
   }
   return a;
 }
@@ -70,30 +70,30 @@ L3U_DEV f4 load_x4(const float* __restrict__ xn, int kk, int K, int s, int lim, 
 // out[co][2z+a][2y+b][2x+c] (+ bias[co]).  A lane holds rows j0 (c = 0) and j0 + 1 (c = 1) of the
 // same 4 consecutive input voxels, i.e. 8 CONTIGUOUS outputs [2x0 .. 2x0+7]: two float4 stores.
 // Requires W % 4 == 0 (VEC); otherwise per-voxel scalar stores.
-template <bool VEC>
-L3U_DEV void d2s_store2(float* outn, int j0, int Nout, const float* __restrict__ bias, int s, f4 v0,
+template <bool VEC, typename T>
+L3U_DEV void d2s_store2(T* outn, int j0, int Nout, const float* __restrict__ bias, int s, f4 v0,
                         f4 v1, int S, int D, int H, int W) {
   const bool ok = j0 < Nout;
   const int co = j0 >> 3, a = (j0 >> 2) & 1, bq = (j0 >> 1) & 1;
   const float bv = (bias && ok) ? bias[co] : 0.f;
   v0 += bv;
   v1 += bv;
-  float* oc = outn + (long long)co * (8ll * S);
+  T* oc = outn + (long long)co * (8ll * S);
   if (VEC) {
     if (ok && s < S) {
       const int x = s % W, t = s / W, y = t % H, z = t / H;
-      float* dst = oc + ((long long)(2 * z + a) * (2 * H) + (2 * y + bq)) * (2 * W) + 2 * x;
-      *reinterpret_cast<f4*>(dst) = f4{v0[0], v1[0], v0[1], v1[1]};
-      *reinterpret_cast<f4*>(dst + 4) = f4{v0[2], v1[2], v0[3], v1[3]};
+      T* dst = oc + ((long long)(2 * z + a) * (2 * H) + (2 * y + bq)) * (2 * W) + 2 * x;
+      stv4(dst, f4{v0[0], v1[0], v0[1], v1[1]});
+      stv4(dst + 4, f4{v0[2], v1[2], v0[3], v1[3]});
     }
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (ok && s + q < S) {
         const int x = (s + q) % W, t = (s + q) / W, y = t % H, z = t / H;
-        float* dst = oc + ((long long)(2 * z + a) * (2 * H) + (2 * y + bq)) * (2 * W) + 2 * x;
-        dst[0] = v0[q];
-        dst[1] = v1[q];
+        T* dst = oc + ((long long)(2 * z + a) * (2 * H) + (2 * y + bq)) * (2 * W) + 2 * x;
+        st1(dst, v0[q]);
+        st1(dst + 1, v1[q]);
       }
     }
   }
@@ -102,13 +102,13 @@ L3U_DEV void d2s_store2(float* outn, int j0, int Nout, const float* __restrict__
 // KS > 0: the whole reduction (K <= 4*KS) in registers, X and weight loads (weights straight
 // from L1/L2, no LDS staging barrier) all issued before the first MFMA; KS = 0: generic K loop
 // with the weights staged through LDS in chunks of 128 reduction rows.
-template <int NC, int NSW, bool VEC, int XM, int KS>   // XM: 0 plain, 1 scatter epilogue, 2 gathered X
+template <typename T, int NC, int NSW, bool VEC, int XM, int KS>   // XM: 0 plain, 1 scatter epilogue, 2 gathered X
 __global__ __launch_bounds__(256) void pw_fwd_kernel(
-    const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
-    const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
+    const T* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
+    const float* __restrict__ bias, T* __restrict__ y, long long yns, int accumulate,
     float* __restrict__ stat_part, int K, int Nout, int S, int nsb, int Dq, int Hq, int Wq,
-    const float* __restrict__ x2 = nullptr, long long xns2 = 0, const float* __restrict__ w2 = nullptr,
-    float* __restrict__ y2 = nullptr, long long yns2 = 0, float* __restrict__ stat2 = nullptr,
+    const T* __restrict__ x2 = nullptr, long long xns2 = 0, const float* __restrict__ w2 = nullptr,
+    T* __restrict__ y2 = nullptr, long long yns2 = 0, float* __restrict__ stat2 = nullptr,
     int N1 = 0) {
   constexpr int CO_BLK = 16 * NC;
   constexpr int TSB = 256 * NSW;
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
   }
   const int Kp = (K + 3) & ~3;
   const int wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
-  const float* xn = x + (long long)n * xns;
+  const T* xn = x + (long long)n * xns;
   const int sbase = sb * TSB + wave * 64 * NSW;
 
   f4 acc[NSW][NC][4];
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
 
   // epilogue: lane (lr, lk) holds Y[co0 + 16m + 4lk + r][sbase + 64j + 4lr + q]: per (m, r) the
   // 16 lanes of a row store 64 consecutive voxels of one channel (256 B, coalesced)
-  float* yn = y + (long long)n * yns;
+  T* yn = y + (long long)n * yns;
   if (XM == 1) {
 #pragma unroll
     for (int m = 0; m < NC; ++m)
@@ -221,22 +221,23 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
       for (int j = 0; j < NSW; ++j) {
         const int s = sbase + j * 64 + 4 * lr;
         f4 v = f4{acc[j][m][0][r], acc[j][m][1][r], acc[j][m][2][r], acc[j][m][3][r]} + bv;
-        float* dst = yn + (long long)co * S + s;
+        T* dst = yn + (long long)co * S + s;
         if (cok) {
           if (VEC) {
             if (s < S) {
-              if (accumulate) v += *reinterpret_cast<const f4*>(dst);
-              *reinterpret_cast<f4*>(dst) = v;
+              if (accumulate) v += ldv4(dst);
+              stv4(dst, v);
             }
           } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
               if (s + q < S) {
-                if (accumulate) v[q] += dst[q];
-                dst[q] = v[q];
+                if (accumulate) v[q] += ld1(dst + q);
+                st1(dst + q, v[q]);
               }
           }
         }
+        v = round_to(v, dst);   // statistics of the stored values
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           acc[j][m][q][r] = v[q];                       // keep the stored value for the stats
@@ -308,24 +309,24 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
 // share ONE 64-voxel tile and split the reduction dimension K (k-steps interleaved by wave), then
 // combine through LDS in a fixed order; weights are read straight from L2 (they are tiny and
 // every workgroup re-reads them).  This turns an 8-workgroup grid into hundreds.
-template <int NC, bool VEC, int XM>
+template <typename T, int NC, bool VEC, int XM>
 __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
-    const float* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
-    const float* __restrict__ bias, float* __restrict__ y, long long yns, int accumulate,
+    const T* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
+    const float* __restrict__ bias, T* __restrict__ y, long long yns, int accumulate,
     float* __restrict__ stat_part, int K, int Nout, int S, int nsb, int Dq, int Hq, int Wq,
-    const float* __restrict__ x2 = nullptr, long long xns2 = 0, const float* __restrict__ w2 = nullptr,
-    float* __restrict__ y2 = nullptr, long long yns2 = 0, float* __restrict__ stat2 = nullptr,
+    const T* __restrict__ x2 = nullptr, long long xns2 = 0, const float* __restrict__ w2 = nullptr,
+    T* __restrict__ y2 = nullptr, long long yns2 = 0, float* __restrict__ stat2 = nullptr,
     int N1 = 0) {
   constexpr int CO_BLK = 16 * NC;
-  constexpr int T = NC * 16;   // accumulator floats per lane
-  extern __shared__ __attribute__((aligned(16))) float lds[];   // [4 waves][T][64 lanes]
+  constexpr int NT = NC * 16;   // accumulator floats per lane
+  extern __shared__ __attribute__((aligned(16))) float lds[];   // [4 waves][NT][64 lanes]
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const int sb = blockIdx.x, co0 = blockIdx.y * CO_BLK;
   int n = blockIdx.z;
   if (x2 != nullptr && n >= N1) {   // the second problem of a paired launch (l3u_pw_fwd2)
     n -= N1; x = x2; xns = xns2; w = w2; y = y2; yns = yns2; stat_part = stat2;
   }
-  const float* xn = x + (long long)n * xns;
+  const T* xn = x + (long long)n * xns;
   const int s = sb * 64 + 4 * lr;
   const int ksteps = (K + 3) >> 2;
   f4 acc[NC][4];
@@ -351,7 +352,7 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
   // tile m = w (16 channels x 64 voxels) and adds the four waves' partials of that tile in wave
   // order (fixed: deterministic), so the epilogue stores are spread over min(NC, 4) waves.
   {
-    float* dst = lds + wave * T * 64 + l;
+    float* dst = lds + wave * NT * 64 + l;
 #pragma unroll
     for (int m = 0; m < NC; ++m)
 #pragma unroll
@@ -368,11 +369,11 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float* src = lds + ((m * 4 + q) * 4 + r) * 64 + l;
-      t4[q][r] = ((src[0] + src[T * 64]) + src[2 * T * 64]) + src[3 * T * 64];
+      t4[q][r] = ((src[0] + src[NT * 64]) + src[2 * NT * 64]) + src[3 * NT * 64];
     }
   }
   // epilogue: lane (lr, lk) holds Y[co0 + 16m + 4lk + r][sb*64 + 4lr + q]
-  float* yn = y + (long long)n * yns;
+  T* yn = y + (long long)n * yns;
   const int sv = sb * 64 + 4 * lr;
   if (XM == 1) {
 #pragma unroll
@@ -389,22 +390,23 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
     const bool cok = co < Nout;
     const float bv = (bias && cok) ? bias[co] : 0.f;
     f4 v = f4{t4[0][r], t4[1][r], t4[2][r], t4[3][r]} + bv;
-    float* dst = yn + (long long)co * S + sv;
+    T* dst = yn + (long long)co * S + sv;
     if (cok) {
       if (VEC) {
         if (sv < S) {
-          if (accumulate) v += *reinterpret_cast<const f4*>(dst);
-          *reinterpret_cast<f4*>(dst) = v;
+          if (accumulate) v += ldv4(dst);
+          stv4(dst, v);
         }
       } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (sv + q < S) {
-            if (accumulate) v[q] += dst[q];
-            dst[q] = v[q];
+            if (accumulate) v[q] += ld1(dst + q);
+            st1(dst + q, v[q]);
           }
       }
     }
+    v = round_to(v, dst);   // statistics of the stored values
     if (stat_part != nullptr) {
       float ls = 0.f;
 #pragma unroll
@@ -432,9 +434,9 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
 // dW[j][k] partial over one voxel chunk of one sample.  A = dY (rows j), B = X^T (cols k),
 // the MFMA k-dimension is the voxel: lane l loads float4 dY[j0+16mo+(l&15)][s+4(l>>4)..+3] and
 // X[k0+16mi+(l&15)][s+4(l>>4)..+3]; component q feeds MFMA q.
-template <int NJ, int NK, bool VEC, bool GATHER>
+template <typename TD, typename TX, int NJ, int NK, bool VEC, bool GATHER>
 __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
-    const float* __restrict__ dy, long long dyns, const float* __restrict__ x, long long xns,
+    const TD* __restrict__ dy, long long dyns, const TX* __restrict__ x, long long xns,
     float* __restrict__ part, float* __restrict__ bsum, int J, int K, int S, int SCH, int nsc,
     int Hq, int Wq) {
   constexpr int TJ = 16 * NJ, TK = 16 * NK;
@@ -443,8 +445,8 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
   const int sc = blockIdx.x % nsc, n = blockIdx.x / nsc;
   const int ntk = (K + TK - 1) / TK;
   const int j0 = (blockIdx.y / ntk) * TJ, k0 = (blockIdx.y % ntk) * TK;
-  const float* dyn = dy + (long long)n * dyns;
-  const float* xn = x + (long long)n * xns;
+  const TD* dyn = dy + (long long)n * dyns;
+  const TX* xn = x + (long long)n * xns;
   const int s_lo = sc * SCH, s_hi = min(S, s_lo + SCH);
 
   f4 acc[NJ][NK];
@@ -468,13 +470,13 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
       const int jj = j0 + 16 * a + lr;
       av[a] = f4{0.f, 0.f, 0.f, 0.f};
       if (jj < J) {
-        const float* src = dyn + (long long)jj * S + sl;
+        const TD* src = dyn + (long long)jj * S + sl;
         if (VEC) {
-          if (sl < s_hi) av[a] = *reinterpret_cast<const f4*>(src);
+          if (sl < s_hi) av[a] = ldv4(src);
         } else {
 #pragma unroll
           for (int q = 0; q < 4; ++q)
-            if (sl + q < s_hi) av[a][q] = src[q];
+            if (sl + q < s_hi) av[a][q] = ld1(src + q);
         }
       }
     }
@@ -557,13 +559,13 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 // (row lr, voxels 16g + 4lk..+3) is read back transposed, conflict-free.  X is only needed by
 // the weight gradient and is loaded in its B layout.  The weights sit in LDS as W[j][k] with a
 // row stride = 16 mod 64 floats (conflict-free A-operand reads for the data gradient).
-template <int NJ, int NK, int PRO>
+template <typename T, int NJ, int NK, int PRO>
 __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
-    const float* __restrict__ dy, long long dyns, const float* __restrict__ yin, long long yns,
+    const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
-    const float* __restrict__ x, long long xns, const float* __restrict__ w,
+    const T* __restrict__ x, long long xns, const float* __restrict__ w,
     float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part, int N, int J,
-    int K, int S, int SCH, int nsc, const float* __restrict__ oin = nullptr, long long oins = 0,
+    int K, int S, int SCH, int nsc, const T* __restrict__ oin = nullptr, long long oins = 0,
     int sel = 1) {
   constexpr int TJ = 16 * NJ, TK = 16 * NK, JR = TJ / 4;
   constexpr int WS = TK + ((16 - TK) % 64 + 64) % 64;   // >= TK, = 16 mod 64
@@ -581,7 +583,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   const int sw = s_lo + 64 * wave;
   const int sd = sw + 4 * lr;                           // data-gradient layout voxels
   const float* dyn = dy + (long long)n * dyns;
-  const float* xn = x + (long long)n * xns;
+  const T* xn = x + (long long)n * xns;
   float* dxn = dx + (long long)n * dxns;
 
   // 1. every streamed load of the tile is issued first ...
@@ -590,24 +592,24 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   for (int jr = 0; jr < JR; ++jr) {
     const int j = 4 * jr + lk;
     g[jr] = f4{0.f, 0.f, 0.f, 0.f};
-    if (j < J && sd < s_hi) g[jr] = *reinterpret_cast<const f4*>(dyn + (long long)j * S + sd);
+    if (j < J && sd < s_hi) g[jr] = ldv4(dyn + (long long)j * S + sd);
   }
   if (PRO == 2) {   // the block output (LeakyReLU mask of the tail)
-    const float* on = oin + (long long)n * oins;
+    const T* on = oin + (long long)n * oins;
 #pragma unroll
     for (int jr = 0; jr < JR; ++jr) {
       const int j = 4 * jr + lk;
       ov[jr] = f4{0.f, 0.f, 0.f, 0.f};
-      if (j < J && sd < s_hi) ov[jr] = *reinterpret_cast<const f4*>(on + (long long)j * S + sd);
+      if (j < J && sd < s_hi) ov[jr] = ldv4(on + (long long)j * S + sd);
     }
   }
   if (PRO) {
-    const float* yn = yin + (long long)n * yns;
+    const T* yn = yin + (long long)n * yns;
 #pragma unroll
     for (int jr = 0; jr < JR; ++jr) {
       const int j = 4 * jr + lk;
       yv[jr] = f4{0.f, 0.f, 0.f, 0.f};
-      if (j < J && sd < s_hi) yv[jr] = *reinterpret_cast<const f4*>(yn + (long long)j * S + sd);
+      if (j < J && sd < s_hi) yv[jr] = ldv4(yn + (long long)j * S + sd);
     }
   }
   f4 xv[4][NK];
@@ -696,8 +698,8 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       if (k < K && sd < s_hi) {
         float* dst = dxn + (long long)k * S + sd;
         f4 v = f4{acc[0][r], acc[1][r], acc[2][r], acc[3][r]};
-        if (accumulate) v += *reinterpret_cast<const f4*>(dst);
-        *reinterpret_cast<f4*>(dst) = v;
+        if (accumulate) v += ldv4(dst);
+        stv4(dst, v);
       }
     }
   }
@@ -764,11 +766,11 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
 // (the ConvTranspose3d weight [Ci][Co*8]) and so are the partials; bpart != NULL receives the
 // bias partials sum_{tile, abc} dY[co] per (tile, co) from the K-tile-0 workgroups.
 // Partials are per 64-voxel tile: part[N * ceil(S/64)][J][K] ([K][J] for GATHER).
-template <int JT, int NWV, int PRO, int GATHER>
+template <typename T, int JT, int NWV, int PRO, int GATHER>
 __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
-    const float* __restrict__ dy, long long dyns, const float* __restrict__ yin, long long yns,
+    const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
-    const float* __restrict__ x, long long xns, const float* __restrict__ w,
+    const T* __restrict__ x, long long xns, const float* __restrict__ w,
     float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part,
     float* __restrict__ bpart, int N, int J, int K, int S, int Hq, int Wq) {
   constexpr int JW = 16 * JT;                 // dY rows per wave
@@ -781,7 +783,7 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
   const int tile = blockIdx.x % ntile, n = blockIdx.x / ntile, k0 = blockIdx.y * 16;
   const int v0 = tile * 64, jb = wave * JW;
   const float* dyn = dy + (long long)n * dyns;
-  const float* xn = x + (long long)n * xns;
+  const T* xn = x + (long long)n * xns;
 
   // streamed loads first: dY in the data-gradient B layout (rows jb + 4jr + lk, voxels
   // v0 + 4lr..), dY in the weight-gradient A layout (rows jb + 16t + lr, voxels v0 + 16g + 4lk..),
@@ -802,7 +804,7 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
     for (int g = 0; g < 4; ++g)
       ga[t][g] = load_x4<GV, G>(dyn, jb + 16 * t + lr, J, v0 + 16 * g + 4 * lk, S, S, Hq, Wq);
   if (PRO) {
-    const float* yn = yin + (long long)n * yns;
+    const T* yn = yin + (long long)n * yns;
 #pragma unroll
     for (int jr = 0; jr < JT * 4; ++jr) yd[jr] = load_x4<true, false>(yn, jb + 4 * jr + lk, J, vd, S, S, 0, 0);
 #pragma unroll
@@ -914,13 +916,13 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
       float* dst = dx + (long long)n * dxns + (long long)k * S + vd;
       if (GV) {
         if (vd < S) {
-          if (accumulate) v += *reinterpret_cast<const f4*>(dst);
-          *reinterpret_cast<f4*>(dst) = v;
+          if (accumulate) v += ldv4(dst);
+          stv4(dst, v);
         }
       } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (vd + q < S) dst[q] = accumulate ? dst[q] + v[q] : v[q];
+          if (vd + q < S) st1(dst + q, accumulate ? ld1(dst + q) + v[q] : v[q]);
       }
     }
   }
@@ -949,22 +951,20 @@ bool pw_use_ks(int S, int K) { return S < 32768 && K >= L3U_PW_KS_MIN_K; }
 
 }  // namespace
 
-extern "C" {
-
-}  // extern "C"
-
 namespace {
 
+template <typename T>
 struct PwSecond {   // the second problem of a paired launch: same K, Nout, S, N and options
-  const float* x; long long xns; const float* w; float* y; long long yns; float* stat;
+  const T* x; long long xns; const float* w; T* y; long long yns; float* stat;
 };
 
-int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout, const float* bias,
-              float* y, long long y_nstride, int accumulate, float* stat_part, int N, int K,
+template <typename T>
+int pw_launch(const T* x, long long x_nstride, const float* w, int w_layout, const float* bias,
+              T* y, long long y_nstride, int accumulate, float* stat_part, int N, int K,
               int Nout, int S, int xm, int Dq, int Hq, int Wq, hipStream_t stream,
-              const PwSecond* sec = nullptr) {
-  const PwSecond z2{nullptr, 0, nullptr, nullptr, 0, nullptr};
-  const PwSecond& p2 = sec ? *sec : z2;
+              const PwSecond<T>* sec = nullptr) {
+  const PwSecond<T> z2{nullptr, 0, nullptr, nullptr, 0, nullptr};
+  const PwSecond<T>& p2 = sec ? *sec : z2;
   const int NZ = sec ? 2 * N : N;
   // xm: 0 plain GEMM, 1 ConvTranspose3d scatter epilogue, 2 X gathered from the up-sampled
   // ConvTranspose3d gradient; (Dq, Hq, Wq) = the low-resolution volume for xm != 0
@@ -978,7 +978,7 @@ int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout,
     while (NC > 1 && (long long)nsb * ((Nout + 16 * NC - 1) / (16 * NC)) * N < 256) NC >>= 1;
     const size_t lds = 4 * 64 * (size_t)NC * 16 * sizeof(float);
     dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), NZ), block(256);
-#define PWK(NC_, V_, X_) hipLaunchKernelGGL((pw_fwd_ks_kernel<NC_, V_, X_>), grid, block, lds, stream, \
+#define PWK(NC_, V_, X_) hipLaunchKernelGGL((pw_fwd_ks_kernel<T, NC_, V_, X_>), grid, block, lds, stream, \
       x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq, \
       p2.x, p2.xns, p2.w, p2.y, p2.yns, p2.stat, N)
 #define PWK_X(NC_, V_) do { if (xm == 1) PWK(NC_, V_, 1); else if (xm == 2) PWK(NC_, V_, 2); else PWK(NC_, V_, 0); } while (0)
@@ -1002,7 +1002,7 @@ int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout,
   dim3 grid(nsb, (Nout + CO_BLK - 1) / CO_BLK, NZ), block(256);
   L3U_REQUIRE(NSW == 1);
   const int KSn = K <= 16 ? 4 : (K <= 32 ? 8 : (K <= 64 ? 16 : 0));
-#define PWF(NC_, V_, X_, KS_) hipLaunchKernelGGL((pw_fwd_kernel<NC_, 1, V_, X_, KS_>), grid, block, lds, \
+#define PWF(NC_, V_, X_, KS_) hipLaunchKernelGGL((pw_fwd_kernel<T, NC_, 1, V_, X_, KS_>), grid, block, lds, \
       stream, x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, \
       Dq, Hq, Wq, p2.x, p2.xns, p2.w, p2.y, p2.yns, p2.stat, N)
 #define PWF_K(NC_, V_, X_) do { if (KSn == 4) PWF(NC_, V_, X_, 4); else if (KSn == 8) PWF(NC_, V_, X_, 8); \
@@ -1019,7 +1019,8 @@ int pw_launch(const float* x, long long x_nstride, const float* w, int w_layout,
   L3U_CHECK_LAUNCH();
 }
 
-int pw_bwd_weight_launch(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
+template <typename TD, typename TX>
+int pw_bwd_weight_launch(const TD* dy, long long dy_nstride, const TX* x, long long x_nstride,
                          float* part, float* bsum, int N, int J, int K, int S, bool gather, int Hq,
                          int Wq, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && J > 0 && K > 0 && S > 0);
@@ -1038,7 +1039,7 @@ int pw_bwd_weight_launch(const float* dy, long long dy_nstride, const float* x, 
   const int ntj = (J + 16 * NJ - 1) / (16 * NJ), ntk = (K + 16 * NK - 1) / (16 * NK);
   const size_t lds = 64 * (size_t)NJ * NK * 4 * sizeof(float);
   dim3 grid(N * nsc, ntj * ntk), block(256);
-#define PWB0(A_, B_, V_, G_) hipLaunchKernelGGL((pw_bwd_weight_kernel<A_, B_, V_, G_>), grid, block, lds, \
+#define PWB0(A_, B_, V_, G_) hipLaunchKernelGGL((pw_bwd_weight_kernel<TD, TX, A_, B_, V_, G_>), grid, block, lds, \
       stream, dy, dy_nstride, x, x_nstride, part, bsum, J, K, S, SCH, nsc, Hq, Wq)
 #define PWB(A_, B_) do { if (gather) { if (vec) PWB0(A_, B_, true, true); else PWB0(A_, B_, false, true); } \
                          else { if (vec) PWB0(A_, B_, true, false); else PWB0(A_, B_, false, false); } } while (0)
@@ -1054,55 +1055,6 @@ int pw_bwd_weight_launch(const float* dy, long long dy_nstride, const float* x, 
 #undef PWB
 #undef PWB0
   L3U_CHECK_LAUNCH();
-}
-
-}  // namespace
-
-extern "C" {
-
-int l3u_pw_fwd(const float* x, long long x_nstride, const float* w, int w_layout,
-               const float* bias, float* y, long long y_nstride, int accumulate,
-               float* stat_part, int N, int K, int Nout, int S, hipStream_t stream) {
-  return pw_launch(x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, N, K,
-                   Nout, S, 0, 0, 0, 0, stream);
-}
-
-int l3u_pw_fwd2(const float* xa, long long xa_nstride, const float* wa, float* ya,
-                long long ya_nstride, float* stat_a, const float* xb, long long xb_nstride,
-                const float* wb, float* yb, long long yb_nstride, float* stat_b, int N, int K,
-                int Nout, int S, hipStream_t stream) {
-  L3U_REQUIRE(xa && wa && ya && xb && wb && yb && (stat_a == nullptr) == (stat_b == nullptr));
-  L3U_REQUIRE(S % 4 == 0 && xa_nstride % 4 == 0 && ya_nstride % 4 == 0 && xb_nstride % 4 == 0 &&
-              yb_nstride % 4 == 0);   // both problems on the vector path
-  const PwSecond b{xb, xb_nstride, wb, yb, yb_nstride, stat_b};
-  return pw_launch(xa, xa_nstride, wa, 0, nullptr, ya, ya_nstride, 0, stat_a, N, K, Nout, S, 0, 0,
-                   0, 0, stream, &b);
-}
-
-int l3u_convt_fwd(const float* x, long long x_nstride, const float* w, const float* bias,
-                  float* out, long long out_nstride, int N, int Ci, int Co, int D, int H, int W,
-                  hipStream_t stream) {
-  L3U_REQUIRE(D > 0 && H > 0 && W > 0);
-  return pw_launch(x, x_nstride, w, 1, bias, out, out_nstride, 0, nullptr, N, Ci, Co * 8,
-                   D * H * W, 1, D, H, W, stream);
-}
-
-int l3u_pw_stat_nsb(int K, int Nout, int S) {
-  if (pw_use_ks(S, K)) return (S + 63) / 64;
-  const int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
-  const int TSB = 256 * pw_nsw(CO_BLK / 16);
-  return (S + TSB - 1) / TSB;
-}
-
-int l3u_pw_bwd_weight_nparts(int N, int S) {
-  const int SCH = pw_sch(S);
-  return N * ((S + SCH - 1) / SCH);
-}
-
-int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
-                      float* part, int N, int J, int K, int S, hipStream_t stream) {
-  return pw_bwd_weight_launch(dy, dy_nstride, x, x_nstride, part, nullptr, N, J, K, S, false, 0, 0,
-                              stream);
 }
 
 #ifndef L3U_CONVT_ONEPASS_ANYW
@@ -1121,31 +1073,22 @@ int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, lon
 #endif
 bool pw_bwd_wide(int J) { return L3U_PW_BWD_WIDE && (J == 64 || J == 128); }
 
-int l3u_pw_bwd_supported(int J, int K, int S) {
-  if (!(J > 0 && K > 0 && S > 0 && S % 4 == 0)) return 0;
-  return (pw_bwd_wide(J) || (J <= 32 && K <= 64)) ? 1 : 0;
-}
+// every pointer aligned to 4 elements of T (one vector load / store)
+template <typename T>
+bool al4(const void* p) { return ((uintptr_t)p & (4 * sizeof(T) - 1)) == 0; }
 
-int l3u_pw_bwd_nparts(int N, int J, int K, int S) {
-  if (!l3u_pw_bwd_supported(J, K, S)) return 0;
-  return pw_bwd_wide(J) ? N * ((S + 63) / 64) : l3u_pw_bwd_weight_nparts(N, S);
-}
-
-// the pointwise backward of conv2.pointwise (sel 1: yr = y2, rec = rec2) or of the shortcut conv
-// (sel 2: yr = r, rec = rec_r) with the block tail's backward (l3u_norm_act_bwd_apply) formed in
-// its prologue from dout / out / yr and the tail partials, so dy2 / dr are never written
-int l3u_pw_bwd_tail(const float* dout, long long dout_nstride, const float* out,
-                    long long out_nstride, const float* yr, long long yr_nstride, const float* rec,
-                    const double* tail_part, int npart, int sel, const float* x,
-                    long long x_nstride, const float* w, float* dx, long long dx_nstride,
-                    int accumulate, float* part, int N, int J, int K, int S, hipStream_t stream) {
+template <typename T>
+int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, long long out_nstride,
+                     const T* yr, long long yr_nstride, const float* rec, const double* tail_part,
+                     int npart, int sel, const T* x, long long x_nstride, const float* w, float* dx,
+                     long long dx_nstride, int accumulate, float* part, int N, int J, int K, int S,
+                     hipStream_t stream) {
   L3U_REQUIRE(N > 0 && l3u_pw_bwd_supported(J, K, S) && !pw_bwd_wide(J));
   L3U_REQUIRE(dout && out && yr && rec && tail_part && npart > 0 && (sel == 1 || sel == 2));
   L3U_REQUIRE(x && w && dx && part);
-  const bool al = ((uintptr_t)dout & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
-                  ((uintptr_t)yr & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
-                  ((uintptr_t)dx & 15) == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
-                  yr_nstride % 4 == 0 && x_nstride % 4 == 0 && dx_nstride % 4 == 0;
+  const bool al = al4<float>(dout) && al4<T>(out) && al4<T>(yr) && al4<T>(x) && al4<float>(dx) &&
+                  dout_nstride % 4 == 0 && out_nstride % 4 == 0 && yr_nstride % 4 == 0 &&
+                  x_nstride % 4 == 0 && dx_nstride % 4 == 0;
   L3U_REQUIRE(al);
   const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
   const int NJ = J <= 16 ? 1 : 2;
@@ -1154,7 +1097,7 @@ int l3u_pw_bwd_tail(const float* dout, long long dout_nstride, const float* out,
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
-#define PWBT(A_, B_) hipLaunchKernelGGL((pw_bwd_fused_kernel<A_, B_, 2>), grid, block, 0, stream, \
+#define PWBT(A_, B_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2>), grid, block, 0, stream, \
       dout, dout_nstride, yr, yr_nstride, rec, tail_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel)
   if (NJ == 1 && NK == 1) PWBT(1, 1);
@@ -1167,20 +1110,20 @@ int l3u_pw_bwd_tail(const float* dout, long long dout_nstride, const float* out,
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long y_nstride,
-               const float* rec, const double* in_part, int npart, const float* x,
-               long long x_nstride, const float* w, float* dx, long long dx_nstride, int accumulate,
-               float* part, int N, int J, int K, int S, hipStream_t stream) {
+template <typename T>
+int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_nstride,
+                const float* rec, const double* in_part, int npart, const T* x,
+                long long x_nstride, const float* w, float* dx, long long dx_nstride, int accumulate,
+                float* part, int N, int J, int K, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && l3u_pw_bwd_supported(J, K, S) && dy && x && w && dx && part);
   L3U_REQUIRE(y == nullptr || (rec && in_part && npart > 0));
-  const bool al = ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
-                  ((uintptr_t)dx & 15) == 0 && (dy_nstride % 4 == 0) && (x_nstride % 4 == 0) &&
-                  (dx_nstride % 4 == 0) &&
-                  (y == nullptr || (((uintptr_t)y & 15) == 0 && y_nstride % 4 == 0));
+  const bool al = al4<float>(dy) && al4<T>(x) && al4<float>(dx) && (dy_nstride % 4 == 0) &&
+                  (x_nstride % 4 == 0) && (dx_nstride % 4 == 0) &&
+                  (y == nullptr || (al4<T>(y) && y_nstride % 4 == 0));
   L3U_REQUIRE(al);
   if (pw_bwd_wide(J)) {
     dim3 grid(N * ((S + 63) / 64), (K + 15) / 16), block(256);
-#define PWBW(T_, P_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T_, 4, P_, 0>), grid, block, 0, stream, \
+#define PWBW(T_, P_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T, T_, 4, P_, 0>), grid, block, 0, stream, \
       dy, dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, nullptr, N, J, K, S, 0, 0)
     if (J == 64) { if (y) PWBW(1, 1); else PWBW(1, 0); }
@@ -1196,10 +1139,10 @@ int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long 
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);   // one sweep of the chunk per workgroup
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
-#define PWBF(A_, B_) do { if (y) hipLaunchKernelGGL((pw_bwd_fused_kernel<A_, B_, 1>), grid, block, 0, \
+#define PWBF(A_, B_) do { if (y) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 1>), grid, block, 0, \
       stream, dy, dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, N, J, K, S, SCH, nsc); \
-    else hipLaunchKernelGGL((pw_bwd_fused_kernel<A_, B_, 0>), grid, block, 0, stream, dy, dy_nstride, \
+    else hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 0>), grid, block, 0, stream, dy, dy_nstride, \
       y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, accumulate, part, N, J, K, \
       S, SCH, nsc); } while (0)
   if (NJ == 1 && NK == 1) PWBF(1, 1);
@@ -1210,6 +1153,84 @@ int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long 
   else PWBF(2, 4);
 #undef PWBF
   L3U_CHECK_LAUNCH();
+}
+
+template <typename T>
+int convt_bwd_fused_impl(const float* dy, long long dy_nstride, const T* x, long long x_nstride,
+                         const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
+                         int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
+  L3U_REQUIRE(l3u_convt_bwd_fused_nparts(N, Ci, Co, D, H, W) > 0 && dy && x && w && dx && wpart);
+  const int S = D * H * W, J = Co * 8;
+  const bool vec = W % 4 == 0 && S % 4 == 0 && dy_nstride % 4 == 0 && x_nstride % 4 == 0 &&
+                   dx_nstride % 4 == 0 && al4<float>(dy) && al4<T>(x) && al4<float>(dx);
+  dim3 grid(N * ((S + 63) / 64), (Ci + 15) / 16);
+#define CTB(T_, NW_, G_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T, T_, NW_, 0, G_>), grid, dim3(64 * NW_), \
+      0, stream, dy, dy_nstride, nullptr, 0, nullptr, nullptr, 0, x, x_nstride, w, dx, dx_nstride, 0, \
+      wpart, bpart, N, J, Ci, S, H, W)
+#define CTB_G(T_, NW_) do { if (vec) CTB(T_, NW_, 1); else CTB(T_, NW_, 2); } while (0)
+  if (J == 64) CTB_G(1, 4);
+  else if (J == 128) CTB_G(2, 4);
+  else if (J == 256) CTB_G(2, 8);
+  else CTB_G(2, 16);
+#undef CTB_G
+#undef CTB
+  L3U_CHECK_LAUNCH();
+}
+
+template <typename T>
+int convt_bwd_impl(const float* dy, long long dy_nstride, const T* x, long long x_nstride,
+                   const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
+                   int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && Ci > 0 && Co > 0 && D > 0 && H > 0 && W > 0);
+  const int S = D * H * W;
+  // dX[ci][s] = sum_{co,abc} w[ci][co*8+abc] dY[co][up(s, abc)]: the GEMM with X gathered (all
+  // gradients: fp32)
+  int rc = pw_launch<float>(dy, dy_nstride, w, 0, nullptr, dx, dx_nstride, 0, nullptr, N, Co * 8, Ci,
+                            S, 2, D, H, W, stream);
+  if (rc != 0) return rc;
+  // dW[ci][co*8+abc] = sum_s x[ci][s] dY[co][up(s, abc)] and, in the same launch,
+  // db[co] = sum of dY over the up-sampled volume: bpart[N*nsc][Co]
+  return pw_bwd_weight_launch<T, float>(x, x_nstride, dy, dy_nstride, wpart, bpart, N, Ci, Co * 8, S,
+                                        true, H, W, stream);
+}
+
+template <typename T>
+int pw_fwd2_impl(const T* xa, long long xa_nstride, const float* wa, T* ya, long long ya_nstride,
+                 float* stat_a, const T* xb, long long xb_nstride, const float* wb, T* yb,
+                 long long yb_nstride, float* stat_b, int N, int K, int Nout, int S,
+                 hipStream_t stream) {
+  L3U_REQUIRE(xa && wa && ya && xb && wb && yb && (stat_a == nullptr) == (stat_b == nullptr));
+  L3U_REQUIRE(S % 4 == 0 && xa_nstride % 4 == 0 && ya_nstride % 4 == 0 && xb_nstride % 4 == 0 &&
+              yb_nstride % 4 == 0);   // both problems on the vector path
+  const PwSecond<T> b{xb, xb_nstride, wb, yb, yb_nstride, stat_b};
+  return pw_launch<T>(xa, xa_nstride, wa, 0, nullptr, ya, ya_nstride, 0, stat_a, N, K, Nout, S, 0, 0,
+                      0, 0, stream, &b);
+}
+
+}  // namespace
+
+extern "C" {
+
+int l3u_pw_stat_nsb(int K, int Nout, int S) {
+  if (pw_use_ks(S, K)) return (S + 63) / 64;
+  const int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
+  const int TSB = 256 * pw_nsw(CO_BLK / 16);
+  return (S + TSB - 1) / TSB;
+}
+
+int l3u_pw_bwd_weight_nparts(int N, int S) {
+  const int SCH = pw_sch(S);
+  return N * ((S + SCH - 1) / SCH);
+}
+
+int l3u_pw_bwd_supported(int J, int K, int S) {
+  if (!(J > 0 && K > 0 && S > 0 && S % 4 == 0)) return 0;
+  return (pw_bwd_wide(J) || (J <= 32 && K <= 64)) ? 1 : 0;
+}
+
+int l3u_pw_bwd_nparts(int N, int J, int K, int S) {
+  if (!l3u_pw_bwd_supported(J, K, S)) return 0;
+  return pw_bwd_wide(J) ? N * ((S + 63) / 64) : l3u_pw_bwd_weight_nparts(N, S);
 }
 
 // fused ConvTranspose3d backward: Co*8 = 16 * 2 * NWV rows (Co in {8, 16, 32, 64}).  Offered for
@@ -1223,41 +1244,46 @@ int l3u_convt_bwd_fused_nparts(int N, int Ci, int Co, int D, int H, int W) {
   return N * ((D * H * W + 63) / 64);
 }
 
-int l3u_convt_bwd_fused(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
-                        const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
-                        int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
-  L3U_REQUIRE(l3u_convt_bwd_fused_nparts(N, Ci, Co, D, H, W) > 0 && dy && x && w && dx && wpart);
-  const int S = D * H * W, J = Co * 8;
-  const bool vec = W % 4 == 0 && S % 4 == 0 && dy_nstride % 4 == 0 && x_nstride % 4 == 0 &&
-                   dx_nstride % 4 == 0 && ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
-                   ((uintptr_t)dx & 15) == 0;
-  dim3 grid(N * ((S + 63) / 64), (Ci + 15) / 16);
-#define CTB(T_, NW_, G_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T_, NW_, 0, G_>), grid, dim3(64 * NW_), \
-      0, stream, dy, dy_nstride, nullptr, 0, nullptr, nullptr, 0, x, x_nstride, w, dx, dx_nstride, 0, \
-      wpart, bpart, N, J, Ci, S, H, W)
-#define CTB_G(T_, NW_) do { if (vec) CTB(T_, NW_, 1); else CTB(T_, NW_, 2); } while (0)
-  if (J == 64) CTB_G(1, 4);
-  else if (J == 128) CTB_G(2, 4);
-  else if (J == 256) CTB_G(2, 8);
-  else CTB_G(2, 16);
-#undef CTB_G
-#undef CTB
-  L3U_CHECK_LAUNCH();
-}
-
-int l3u_convt_bwd(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
-                  const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
-                  int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
-  L3U_REQUIRE(N > 0 && Ci > 0 && Co > 0 && D > 0 && H > 0 && W > 0);
-  const int S = D * H * W;
-  // dX[ci][s] = sum_{co,abc} w[ci][co*8+abc] dY[co][up(s, abc)]: the GEMM with X gathered
-  int rc = pw_launch(dy, dy_nstride, w, 0, nullptr, dx, dx_nstride, 0, nullptr, N, Co * 8, Ci, S,
-                     2, D, H, W, stream);
-  if (rc != 0) return rc;
-  // dW[ci][co*8+abc] = sum_s x[ci][s] dY[co][up(s, abc)] and, in the same launch,
-  // db[co] = sum of dY over the up-sampled volume: bpart[N*nsc][Co]
-  return pw_bwd_weight_launch(x, x_nstride, dy, dy_nstride, wpart, bpart, N, Ci, Co * 8, S, true, H,
-                              W, stream);
-}
-
 }  // extern "C"
+
+// ---- C-ABI: fp32 entry points and their _bf16 twins (include/l3u.h) ----------------------------
+#define P_PWF(TT) (const TT* x, long long x_nstride, const float* w, int w_layout,                \
+    const float* bias, TT* y, long long y_nstride, int accumulate, float* stat_part, int N, int K,  \
+    int Nout, int S, hipStream_t stream)
+L3U_TWIN(l3u_pw_fwd, P_PWF, pw_launch(bp(x), x_nstride, w, w_layout, bias, bp(y), y_nstride,
+         accumulate, stat_part, N, K, Nout, S, 0, 0, 0, 0, stream))
+#define P_PF2(TT) (const TT* xa, long long xa_nstride, const float* wa, TT* ya,                    \
+    long long ya_nstride, float* stat_a, const TT* xb, long long xb_nstride, const float* wb,       \
+    TT* yb, long long yb_nstride, float* stat_b, int N, int K, int Nout, int S, hipStream_t stream)
+L3U_TWIN(l3u_pw_fwd2, P_PF2, pw_fwd2_impl(bp(xa), xa_nstride, wa, bp(ya), ya_nstride, stat_a, bp(xb),
+         xb_nstride, wb, bp(yb), yb_nstride, stat_b, N, K, Nout, S, stream))
+#define P_CTF(TT) (const TT* x, long long x_nstride, const float* w, const float* bias, TT* out,   \
+    long long out_nstride, int N, int Ci, int Co, int D, int H, int W, hipStream_t stream)
+L3U_TWIN(l3u_convt_fwd, P_CTF, (D > 0 && H > 0 && W > 0)
+         ? pw_launch(bp(x), x_nstride, w, 1, bias, bp(out), out_nstride, 0, nullptr, N, Ci, Co * 8,
+                     D * H * W, 1, D, H, W, stream)
+         : (int)hipErrorInvalidValue)
+#define P_PBW(TT) (const float* dy, long long dy_nstride, const TT* x, long long x_nstride,        \
+    float* part, int N, int J, int K, int S, hipStream_t stream)
+L3U_TWIN(l3u_pw_bwd_weight, P_PBW, pw_bwd_weight_launch(dy, dy_nstride, bp(x), x_nstride, part,
+         nullptr, N, J, K, S, false, 0, 0, stream))
+#define P_PBT(TT) (const float* dout, long long dout_nstride, const TT* out, long long out_nstride, \
+    const TT* yr, long long yr_nstride, const float* rec, const double* tail_part, int npart,        \
+    int sel, const TT* x, long long x_nstride, const float* w, float* dx, long long dx_nstride,     \
+    int accumulate, float* part, int N, int J, int K, int S, hipStream_t stream)
+L3U_TWIN(l3u_pw_bwd_tail, P_PBT, pw_bwd_tail_impl(dout, dout_nstride, bp(out), out_nstride, bp(yr),
+         yr_nstride, rec, tail_part, npart, sel, bp(x), x_nstride, w, dx, dx_nstride, accumulate,
+         part, N, J, K, S, stream))
+#define P_PBD(TT) (const float* dy, long long dy_nstride, const TT* y, long long y_nstride,         \
+    const float* rec, const double* in_part, int npart, const TT* x, long long x_nstride,           \
+    const float* w, float* dx, long long dx_nstride, int accumulate, float* part, int N, int J,     \
+    int K, int S, hipStream_t stream)
+L3U_TWIN(l3u_pw_bwd, P_PBD, pw_bwd_impl(dy, dy_nstride, bp(y), y_nstride, rec, in_part, npart,
+         bp(x), x_nstride, w, dx, dx_nstride, accumulate, part, N, J, K, S, stream))
+#define P_CBF(TT) (const float* dy, long long dy_nstride, const TT* x, long long x_nstride,         \
+    const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart, int N, int Ci,     \
+    int Co, int D, int H, int W, hipStream_t stream)
+L3U_TWIN(l3u_convt_bwd_fused, P_CBF, convt_bwd_fused_impl(dy, dy_nstride, bp(x), x_nstride, w,
+         dx, dx_nstride, wpart, bpart, N, Ci, Co, D, H, W, stream))
+L3U_TWIN(l3u_convt_bwd, P_CBF, convt_bwd_impl(dy, dy_nstride, bp(x), x_nstride, w, dx,
+         dx_nstride, wpart, bpart, N, Ci, Co, D, H, W, stream))

@@ -25,8 +25,6 @@ _SIGS = {
     "l3u_dw3_nchunk": [I, I, I, I, I],
     "l3u_dw3_fwd": [P, L, P, P, P, P, L, I, I, I, I, I, P],
     "l3u_dw3_bwd": [P, L, P, L, P, P, P, L, I, P, P, I, I, I, I, I, P],
-    "l3u_dw3_bwd_data": [P, L, P, L, P, P, P, L, I, P, I, I, I, I, I, P],
-    "l3u_dw3_bwd_weight": [P, L, P, L, P, P, P, I, I, I, I, I, P],
     "l3u_pw_stat_nsb": [I, I, I],
     "l3u_pw_fwd": [P, L, P, I, P, P, L, I, P, I, I, I, I, P],
     "l3u_pw_bwd_weight_nparts": [I, I],
@@ -43,14 +41,10 @@ _SIGS = {
     "l3u_in_bwd_apply": [P, L, P, L, P, P, I, P, L, I, I, I, P],
     "l3u_maxpool2_fwd": [P, L, P, L, P, I, I, I, I, I, P],
     "l3u_maxpool2_bwd": [P, L, P, P, L, P, L, I, I, I, I, I, P],
-    "l3u_convt_d2s": [P, P, P, L, I, I, I, I, I, P],
     "l3u_convt_fwd": [P, L, P, P, P, L, I, I, I, I, I, I, P],
     "l3u_convt_bwd": [P, L, P, L, P, P, L, P, P, I, I, I, I, I, I, P],
     "l3u_convt_bwd_fused_nparts": [I, I, I, I, I, I],
     "l3u_convt_bwd_fused": [P, L, P, L, P, P, L, P, P, I, I, I, I, I, I, P],
-    "l3u_convt_s2d": [P, L, P, I, I, I, I, I, P],
-    "l3u_chan_sum_nblocks": [L],
-    "l3u_chan_sum": [P, L, P, I, I, L, P],
     "l3u_outconv_nblocks": [I],
     "l3u_outconv_fwd": [P, L, P, P, P, P, P, I, I, I, P],
     "l3u_outconv_bwd": [P, P, P, P, D, D, D, D, P, P, L, P, P, L, P, P, I, I, I, P],
@@ -61,14 +55,11 @@ _SIGS = {
     "l3u_window_blend": [P, P, I, P, I, P, I, P, I, I, I, I, I, I, P, P],
     "l3u_ftl_loss": [P, D, D, D, D, P, P],
     "l3u_ftl_bwd": [P, P, L, P, D, D, D, D, P, I, P, P],
-    "l3u_adamw": [P, P, P, P, L, P, F, F, F, F, P, F, P],
     "l3u_reduce_segments": [P, P, I, P, P],
     "l3u_pw_fwd2": [P, L, P, P, L, P, P, L, P, P, L, P, I, I, I, I, P],
     "l3u_adamw_tick": [P, P, P, P, L, P, F, F, F, F, P, F, P, P, P],
     "l3u_front_nblocks": [I],
-    "l3u_front_fwd": [P, L, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
-    "l3u_outconv_bwd_tail": [P, P, P, P, D, D, D, D, P, P, L, P, P, L, P, P, P, L, P, P, L, P, P,
-                             I, I, I, P],
+    "l3u_front_fwd": [P, L, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "l3u_pw_bwd_tail": [P, L, P, L, P, L, P, P, I, I, P, L, P, P, L, I, P, I, I, I, I, P],
     "l3u_norm_act_bwd": [P, L, P, L, P, L, P, P, L, P, P, P, L, P, L, I, I, I, P],
     "l3u_gconv3_nblocks": [I],
@@ -77,11 +68,23 @@ _SIGS = {
     "l3u_gconv3_bwd_data": [P, L, P, P, P, L, P, L, I, P, I, I, I, I, I, I, I, P],
     "l3u_gconv3_bwd_weight": [P, L, P, L, P, P, I, I, I, I, I, I, I, P],
     "l3u_counter_add": [P, I, P],
+    "l3u_cast_f32_bf16": [P, P, L, P],
+    "l3u_cast_bf16_f32": [P, P, L, P],
 }
+# entry points with a _bf16 twin (same arguments; saved activations stored as bf16, gradients
+# fp32, include/l3u.h)
+BF16_TWINS = ("l3u_dw3_fwd", "l3u_dw3_bwd", "l3u_pw_fwd", "l3u_pw_fwd2", "l3u_pw_bwd_weight",
+              "l3u_pw_bwd", "l3u_pw_bwd_tail", "l3u_convt_fwd", "l3u_convt_bwd",
+              "l3u_convt_bwd_fused", "l3u_norm_act_fwd", "l3u_norm_act_pool_fwd",
+              "l3u_norm_act_bwd_reduce", "l3u_norm_act_bwd_apply", "l3u_norm_act_bwd",
+              "l3u_in_bwd_apply", "l3u_maxpool2_fwd", "l3u_outconv_fwd", "l3u_outconv_bwd",
+              "l3u_front_fwd")
+for _n in BF16_TWINS:
+    _SIGS[_n + "_bf16"] = _SIGS[_n]
 # query helpers that return a value instead of an error code
 _QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_weight_nparts",
             "l3u_pw_bwd_supported", "l3u_pw_bwd_nparts", "l3u_convt_bwd_fused_nparts",
-            "l3u_norm_act_nblocks", "l3u_chan_sum_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks",
+            "l3u_norm_act_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks",
             "l3u_gconv3_nblocks", "l3u_gconv3_wgrad_nparts", "l3u_front_nblocks"}
 
 _lib = None
@@ -148,8 +151,8 @@ def ptr(t, offset=0):
 def require_device(*tensors):
     for t in tensors:
         if t is not None and (not t.is_cuda or t.dtype not in (torch.float32, torch.float64,
-                                                               torch.int32, torch.int64,
-                                                               torch.uint8)):
+                                                               torch.bfloat16, torch.int32,
+                                                               torch.int64, torch.uint8)):
             raise NativeError(
                 f"light_unet MI355X path needs ROCm device tensors (got {t.device}, {t.dtype}); "
                 "there is no CPU fallback")

@@ -30,8 +30,6 @@ _PAIR_PW = os.environ.get("L3U_PAIR_PW", "1") != "0"
 # 32..256 on the 48^3 step (tools/seg_caps.sh); L3U_SEG_CAPS overrides
 # block-tail backward inside the pointwise backwards (l3u_pw_bwd_tail); L3U_TAIL_FUSE=0 disables
 _TAIL_FUSE = os.environ.get("L3U_TAIL_FUSE", "1") != "0"
-# ... and the last decoder block's tail reduce inside the out_conv backward (L3U_OUTCONV_TAIL)
-_OUTCONV_TAIL = os.environ.get("L3U_OUTCONV_TAIL", "0") != "0"   # measured +4 us: off
 _SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32").split(","))
 
 
@@ -44,7 +42,7 @@ class V:
 
     @property
     def p(self):
-        return self.t.data_ptr() + F32 * self.off
+        return self.t.data_ptr() + self.t.element_size() * self.off
 
 
 def conv_kinds(cin, cout, use_depthwise_separable=True, use_grouped=True, groups=8):
@@ -176,6 +174,10 @@ class UNetEngine:
         self.debug = None      # dict -> backward stashes each block's output-gradient view
         self.fwd_arena = _Arena()
         self.bwd_arena = _Arena()
+        # activation storage: fp32, or bf16 (BASELINE config 3) through the _bf16 entry points;
+        # parameters, records and partial sums stay fp32 either way
+        self.act_dtype = torch.float32
+        self._grad_phase = False   # backward: gradient buffers are fp32 in either storage mode
 
     # ------------------------------------------------------------------ helpers
     @property
@@ -191,7 +193,25 @@ class UNetEngine:
             r = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         return stream_seed(self.base_seed, r)
 
+    def set_act_dtype(self, dtype):
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"activation storage must be float32 or bfloat16, got {dtype}")
+        if dtype == torch.bfloat16 and any(k[0][0] != "ds" for k in self.kinds.values()):
+            raise NotImplementedError("the bf16 path covers the depthwise-separable network "
+                                      "(use_depthwise_separable=True, BASELINE config 3)")
+        self.act_dtype = dtype
+
+    @property
+    def bf16(self):
+        return self.act_dtype == torch.bfloat16
+
     def _call(self, name, *args):
+        """A C-ABI call in the engine's storage mode (the _bf16 twin when activations are bf16)."""
+        if not self._dry:
+            nat.call(name + "_bf16" if self.bf16 and name in nat.BF16_TWINS else name, *args)
+
+    def _call32(self, name, *args):
+        """A call on fp32 operands only (gradient-only GEMMs) in either mode."""
         if not self._dry:
             nat.call(name, *args)
 
@@ -201,8 +221,14 @@ class UNetEngine:
     def _has(self, name):
         return name in self.offsets
 
-    def _empty(self, *shape, dtype=torch.float32, device=None):
-        return torch.empty(shape, dtype=dtype, device=device)
+    def _empty(self, *shape, dtype=None, device=None):
+        """Forward activations in the engine's storage dtype, backward gradients in fp32, unless
+        dtype is given."""
+        dt = dtype or (torch.float32 if self._grad_phase else self.act_dtype)
+        return torch.empty(shape, dtype=dt, device=device)
+
+    def _f32(self, *shape, device=None):
+        return torch.empty(shape, dtype=torch.float32, device=device)
 
     def _seg(self, src_off, count, istride, tstride, length, dst_name, dst_elem=0, accumulate=0,
              f64=0):
@@ -239,9 +265,11 @@ class UNetEngine:
         ftl_part [N * l3u_outconv_nblocks(S)][3]."""
         self.check_shape(x)
         x = x.contiguous()
+        if x.dtype != torch.float32:
+            raise NotImplementedError("the network input is fp32 (bf16 storage is internal)")
         N, _, D, H, W = x.shape
         dev = x.device
-        key = ("f", N, D, H, W)
+        key = ("f", N, D, H, W, self.act_dtype)
         if key not in self._arenas:
             self._dry = True
             self.fwd_arena.reset(None)
@@ -265,7 +293,7 @@ class UNetEngine:
         e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
         drop = dropout_p if training else 0.0
         st = nat.stream()
-        sv = {"N": N, "dims": dims, "S": S, "x": x, "drop": drop}
+        sv = {"N": N, "dims": dims, "S": S, "x": x, "drop": drop, "adt": self.act_dtype}
         if drop > 0.0 and counter is not None and bump_counter:
             self._call("l3u_counter_add", counter.data_ptr(), 1, st)
         cptr = counter.data_ptr() if counter is not None else None
@@ -274,6 +302,11 @@ class UNetEngine:
         x4 = e(N, c3, S[3])
         sv.update(cat3=cat3, cat2=cat2, cat1=cat1, x4=x4)
         x_in = V(x, 0, S[0], 1)
+        if self.bf16 and not self._front_ok(x_in, dims[0]):
+            # the bf16 network's input (the front kernel writes this copy itself when it runs)
+            xb = e(N, 1, S[0])
+            self._call("l3u_cast_f32_bf16", x.data_ptr(), xb.data_ptr(), N * S[0], st)
+            x_in = V(xb, 0, S[0], 1)
         x1 = V(cat3, c0 * S[0], 2 * c0 * S[0], c0)
         x2 = V(cat2, c1 * S[1], 2 * c1 * S[1], c1)
         x3 = V(cat1, c2 * S[2], 2 * c2 * S[2], c2)
@@ -319,7 +352,7 @@ class UNetEngine:
             ups.append((prev, out))
             prev = V(out, 0, co * S[lvl], co)
         sv["ups"] = ups
-        p = e(N, 1, D, H, W)
+        p = self._f32(N, 1, D, H, W, device=dev)   # probabilities stay fp32 (the loss input)
         # with a target, the FocalTversky first-stage partials come out of the same launch
         self._call("l3u_outconv_fwd", prev.p, prev.ns, self._w(flat, "out_conv.weight"),
                    self._w(flat, "out_conv.bias"), p.data_ptr(),
@@ -335,6 +368,10 @@ class UNetEngine:
         return nat.NormSrc(self.fwd_arena.ptr(stat_off), nsb, layer,
                            self._w(flat, norm_prefix + "weight"), self._w(flat, norm_prefix + "bias"),
                            float(drop), self.seed, cptr or 0, rec_out)
+
+    @staticmethod
+    def _front_ok(x, dims):
+        return _FRONT and x.C == 1 and dims[2] % 4 == 0 and x.ns % 4 == 0
 
     @staticmethod
     def _pool_fusable(v, dims):
@@ -354,25 +391,29 @@ class UNetEngine:
         e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
         nsb = nat.query("l3u_pw_stat_nsb", cin, cout, S)      # pw1 / shortcut (K = cin)
         nsb2 = nat.query("l3u_pw_stat_nsb", cout, cout, S)    # pw2 (K = cout)
-        recs = e(3, N * cout, 8)
+        recs = self._f32(3, N * cout, 8, device=dev)
         rec_r, rec1, rec2 = (recs[0].data_ptr(), recs[1].data_ptr(), recs[2].data_ptr())
         sv = {"x": x, "out": out, "recs": recs}
         shortcut = self._has(pre + "shortcut.0.weight")
         # InstanceNorm records are finalized inside their consumer kernels from the GEMM
         # partials (l3u_norm_src); `recs` receives them for the backward pass.
         src_r = src2 = None
-        if _FRONT and shortcut and cin == 1 and w % 4 == 0 and x.ns % 4 == 0:
+        if shortcut and self._front_ok(x, dims) and x.t.dtype == torch.float32:
             # the one-input-channel block: shortcut, conv1.depthwise and conv1.pointwise (both
-            # rank-1 channel maps) and their IN statistics in one launch
+            # rank-1 channel maps) and their IN statistics in one launch (bf16: plus the bf16
+            # copy of the input the backward reads)
             nbf = nat.query("l3u_front_nblocks", S)
             r, z1, y1 = e(N, cout, S), e(N, cin, S), e(N, cout, S)
+            xc = e(N, cin, S) if self.bf16 else None
             so = self.fwd_arena.alloc(N * cout * nbf * 3)
             s1 = self.fwd_arena.alloc(N * cout * nbf * 3)
             self._call("l3u_front_fwd", x.p, x.ns, self._w(flat, pre + "conv1.depthwise.weight"),
                        self._w(flat, pre + "conv1.pointwise.weight"),
                        self._w(flat, pre + "shortcut.0.weight"), z1.data_ptr(), y1.data_ptr(),
-                       r.data_ptr(), self.fwd_arena.ptr(s1), self.fwd_arena.ptr(so), N, cout, d, h,
-                       w, st)
+                       r.data_ptr(), self.fwd_arena.ptr(s1), self.fwd_arena.ptr(so),
+                       xc.data_ptr() if xc is not None else None, N, cout, d, h, w, st)
+            if xc is not None:
+                sv["x"] = V(xc, 0, cin * S, cin)
             src_r = self._src(flat, pre + "shortcut.1.", so, nbf, rec_r, 0.0, cptr, 0)
             rv = V(r, 0, cout * S, cout)
             sv["r"] = rv
@@ -454,7 +495,7 @@ class UNetEngine:
         e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
         nsb = nat.query("l3u_pw_stat_nsb", cin, cout, S)
         nbg = nat.query("l3u_gconv3_nblocks", S)
-        recs = e(3, N * cout, 8)
+        recs = self._f32(3, N * cout, 8, device=dev)
         rec_r, rec1, rec2 = (recs[0].data_ptr(), recs[1].data_ptr(), recs[2].data_ptr())
         sv = {"x": x, "out": out, "recs": recs}
         shortcut = self._has(pre + "shortcut.0.weight")
@@ -505,22 +546,27 @@ class UNetEngine:
         backward, which also writes the loss value when a loss tensor is given."""
         N = sv["N"]
         D, H, W = sv["dims"][0]
-        key = ("b", N, D, H, W, bool(need_dx))
-        if key not in self._arenas:
-            self._dry = True
-            self.bwd_arena.reset(None)
+        self.set_act_dtype(sv["adt"])
+        key = ("b", N, D, H, W, bool(need_dx), self.act_dtype)
+        self._grad_phase = True
+        try:
+            if key not in self._arenas:
+                self._dry = True
+                self.bwd_arena.reset(None)
+                self._items_rec = []
+                try:
+                    self._backward_impl(flat, gflat, sv, dp, need_dx, ftl)
+                finally:
+                    self._dry = False
+                dev = sv["p"].device
+                self._arenas[key] = torch.empty(max(self.bwd_arena.top, 64), dtype=torch.float32,
+                                                device=dev)
+                self._items[key] = torch.tensor(self._items_rec, dtype=torch.int64, device=dev)
+            self.bwd_arena.reset(self._arenas[key])
             self._items_rec = []
-            try:
-                self._backward_impl(flat, gflat, sv, dp, need_dx, ftl)
-            finally:
-                self._dry = False
-            dev = sv["p"].device
-            self._arenas[key] = torch.empty(max(self.bwd_arena.top, 64), dtype=torch.float32,
-                                            device=dev)
-            self._items[key] = torch.tensor(self._items_rec, dtype=torch.int64, device=dev)
-        self.bwd_arena.reset(self._arenas[key])
-        self._items_rec = []
-        dx = self._backward_impl(flat, gflat, sv, dp, need_dx, ftl)
+            dx = self._backward_impl(flat, gflat, sv, dp, need_dx, ftl)
+        finally:
+            self._grad_phase = False
         items = self._items[key]
         nat.call("l3u_reduce_segments", self.bwd_arena.ptr(0), items.data_ptr(), items.shape[0],
                  gflat.data_ptr(), nat.stream())
@@ -547,23 +593,9 @@ class UNetEngine:
             g = (None, t.data_ptr(), sums.data_ptr(), alpha, beta, gamma, smooth, None)
             if len(ftl) > 3 and ftl[3] is not None:   # the loss value, written by the same launch
                 loss_ptr = ftl[3].data_ptr()
-        # the last decoder block's tail reduce rides in the out_conv backward (its output is h)
-        b3 = sv["blk"]["up3.res_block."]
-        tail_pre = None
-        if (_TAIL_FUSE and _OUTCONV_TAIL and c0 <= 16 and S[0] % 4 == 0 and b3["out"].C == c0
-                and self.kinds["up3.res_block."][0][0] == "ds"
-                and self._tail_fusable(b3, b3["x"].C, c0, S[0])):
-            ntp = nat.query("l3u_outconv_nblocks", S[0])
-            pt = A.alloc(2 * c0 * N * ntp * 3)            # fp64 partials
-            self._call("l3u_outconv_bwd_tail", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
-                       self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po), loss_ptr,
-                       b3["y2"].data_ptr(), c0 * S[0], b3["recs"][2].data_ptr(), b3["r"].p, b3["r"].ns,
-                       b3["recs"][0].data_ptr(), A.ptr(pt), N, c0, S[0], st)
-            tail_pre = (pt, ntp)
-        else:
-            self._call("l3u_outconv_bwd", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
-                       self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po),
-                       loss_ptr, N, c0, S[0], st)
+        self._call("l3u_outconv_bwd", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
+                   self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po),
+                   loss_ptr, N, c0, S[0], st)
         self._seg(po // 2, N * nb, c0 + 1, 1, c0, "out_conv.weight", f64=1)
         self._seg(po // 2 + c0, N * nb, c0 + 1, 1, 1, "out_conv.bias", f64=1)
         dcat3, dcat2, dcat1 = e(N, 2 * c0, S[0]), e(N, 2 * c1, S[1]), e(N, 2 * c2, S[2])
@@ -574,8 +606,7 @@ class UNetEngine:
         for up, co, lvl, uidx in up_specs:
             dcat = dcats[lvl]
             self._block_bwd(flat, up + "res_block.", sv["blk"][up + "res_block."], dout,
-                            V(dcat, 0, 2 * co * S[lvl], 2 * co), st, dev,
-                            tail_pre=tail_pre if up == "up3." else None)
+                            V(dcat, 0, 2 * co * S[lvl], 2 * co), st, dev)
             # ConvTranspose3d backward: input = prev (the lower-level output), dOut = dcat[:, :co]
             prev, _ = sv["ups"][uidx]
             ci = prev.C
@@ -617,7 +648,8 @@ class UNetEngine:
             dlev = e(N, cprev, S[lvl])
             d, hh, w = dims[lvl]
             self._call("l3u_maxpool2_bwd", dpool.data_ptr(), cprev * S[lvl + 1], idx.data_ptr(),
-                       dcat.data_ptr() + F32 * cprev * S[lvl], 2 * cprev * S[lvl], dlev.data_ptr(),
+                       dcat.data_ptr() + dcat.element_size() * cprev * S[lvl], 2 * cprev * S[lvl],
+                       dlev.data_ptr(),
                        cprev * S[lvl], N, cprev, d, hh, w, st)
             dout = V(dlev, 0, cprev * S[lvl], cprev)
         # ---- init block
@@ -635,7 +667,7 @@ class UNetEngine:
                 and cout <= 32 and nat.query("l3u_pw_bwd_supported", cout, cout, S)
                 and nat.query("l3u_pw_bwd_supported", cout, cin, S))
 
-    def _tail_bwd(self, pre, sv, dout, dxv, N, cout, S, st, dev, fused=False, tail_pre=None):
+    def _tail_bwd(self, pre, sv, dout, dxv, N, cout, S, st, dev, fused=False):
         """Backward of the block tail out = lrelu(IN2(y2) + residual): d y2 and d residual (the
         shortcut-conv output, or dxv itself for the identity shortcut), with the norm2 / shortcut
         IN parameter-gradient reductions recorded.  fused: only the reduce; returns the tail
@@ -646,20 +678,16 @@ class UNetEngine:
         shortcut = sv["shortcut"]
         rv = sv["r"] if shortcut else sv["x"]
         y2 = sv["y2"]
-        if tail_pre is not None:   # partials already written by the producer of dout
-            pn, nb = tail_pre
-        else:
-            nb = nat.query("l3u_norm_act_nblocks", S)
-            pn = A.alloc(2 * cout * N * nb * 3)            # fp64 partials
+        nb = nat.query("l3u_norm_act_nblocks", S)
+        pn = A.alloc(2 * cout * N * nb * 3)            # fp64 partials
         pnd = pn // 2
         self._seg(pnd + 1, N * nb, 3, N * nb * 3, cout, pre + "norm2.weight", f64=1)
         self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "norm2.bias", f64=1)
         if fused:
             self._seg(pnd + 2, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.weight", f64=1)
             self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.bias", f64=1)
-            if tail_pre is None:
-                self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(),
-                           cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S, st)
+            self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(),
+                       cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S, st)
             return pn, nb
         dy2 = self._empty(N, cout, S, device=dev)
         if shortcut:
@@ -731,10 +759,9 @@ class UNetEngine:
         if self.debug is not None and not self._dry:
             self.debug[pre + "#"] = {"dy2": dy2, "dr": drv, "dy1": dy1, "dx": dxv}
 
-    def _block_bwd(self, flat, pre, sv, dout, dxv, st, dev, tail_pre=None):
+    def _block_bwd(self, flat, pre, sv, dout, dxv, st, dev):
         """Backward of ResidualBlock.forward (unet3d.py:77-93).  Writes d(block input) into dxv
-        (overwrite) and records the block's weight-gradient reductions.  tail_pre = (arena
-        offset, blocks per plane): the tail reduce partials were written by dout's producer."""
+        (overwrite) and records the block's weight-gradient reductions."""
         if self.kinds[pre][0][0] != "ds":
             return self._block_bwd_g(flat, pre, sv, dout, dxv, st, dev)
         A = self.bwd_arena
@@ -752,13 +779,11 @@ class UNetEngine:
         y2, z2, y1, z1 = sv["y2"], sv["z2"], sv["y1"], sv["z1"]
         # (1) block tail: out = lrelu(IN2(y2) + residual)
         fused = self._tail_fusable(sv, cin, cout, S)
-        assert tail_pre is None or fused
         dz2 = e(N, cout, S)
         if fused:
             # (1+2) the tail reduce, then conv2.pointwise backward with the tail's apply in its
             # prologue (dy2 is never written)
-            pn, ntp = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev, fused=True,
-                                     tail_pre=tail_pre)
+            pn, ntp = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev, fused=True)
             self._pw_bwd_tail(flat, dout, sv["out"], V(y2, 0, cout * S, cout), rec2, pn, ntp, 1,
                               V(z2, 0, cout * S, cout), pre + "conv2.pointwise.weight",
                               V(dz2, 0, cout * S, cout), 0, N, S, st)
@@ -830,8 +855,8 @@ class UNetEngine:
             assert pro is None
             npw = nat.query("l3u_pw_bwd_weight_nparts", N, S)
             part = A.alloc(npw * J * K)
-            self._call("l3u_pw_fwd", dy.p, dy.ns, w, 1, None, dx.p, dx.ns, accumulate, None, N, J, K,
-                       S, st)
+            self._call32("l3u_pw_fwd", dy.p, dy.ns, w, 1, None, dx.p, dx.ns, accumulate, None, N, J,
+                         K, S, st)
             self._call("l3u_pw_bwd_weight", dy.p, dy.ns, x.p, x.ns, A.ptr(part), N, J, K, S, st)
         self._seg(part, npw, J * K, 1, J * K, name)
 

@@ -125,6 +125,7 @@ class _UNetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model, x, *params):
         flat = model._flat
+        model.engine.set_act_dtype(model.act_dtype())
         p, sv = model.engine.forward(flat, x, training=model.training, dropout_p=model.dropout_p,
                                      counter=model._rng_counter, save=True)
         ctx.model = model
@@ -148,7 +149,7 @@ class Lightweight3DUNet(nn.Module):
     def __init__(self, in_channels=1, out_channels=1, start_channels=16,
                  encoder_channels=[16, 32, 64, 128],
                  use_depthwise_separable=True, use_grouped=True, groups=8,
-                 dropout_p=0.1):
+                 dropout_p=0.1, *, compute_dtype=None):
         super().__init__()
         self.in_channels = in_channels
         self.out_channels = out_channels
@@ -172,6 +173,11 @@ class Lightweight3DUNet(nn.Module):
         self.engine = _engine.UNetEngine(encoder_channels, in_channels, out_channels,
                                          use_depthwise_separable=use_depthwise_separable,
                                          use_grouped=use_grouped, groups=groups)
+        # None: fp32, or bf16 under torch.autocast; torch.bfloat16 forces the bf16 path
+        self.compute_dtype = None
+        if compute_dtype is not None:
+            self.engine.set_act_dtype(compute_dtype)
+            self.compute_dtype = compute_dtype
         names = [n for n, _ in self.named_parameters()]
         if names != [n for n, _ in self.engine.layout]:
             raise AssertionError("parameter registration order diverged from the engine layout")
@@ -230,13 +236,26 @@ class Lightweight3DUNet(nn.Module):
                 f"Lightweight3DUNet (MI355X path) needs input and model on the same ROCm device; "
                 f"got input on {x.device}, model on {flat.device}.  There is no CPU fallback.")
         if flat.dtype != torch.float32:
-            raise NotImplementedError("the MI355X path computes in fp32")
+            raise NotImplementedError("the MI355X path keeps fp32 parameters (bf16 activations: "
+                                      "compute_dtype=torch.bfloat16 or torch.autocast)")
         x = x.float()
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
             return _UNetFunction.apply(self, x, *self.parameters())
+        self.engine.set_act_dtype(self.act_dtype())
         p, _ = self.engine.forward(flat, x, training=self.training, dropout_p=self.dropout_p,
                                    counter=self._rng_counter, save=False)
         return p
+
+    def act_dtype(self):
+        """Storage dtype of the activations for this call: `compute_dtype` when set, else bf16
+        inside torch.autocast("cuda", dtype=torch.bfloat16), else fp32.  Parameters, InstanceNorm
+        statistics, the returned probabilities and all accumulation stay fp32 (BASELINE config 3:
+        bf16 activations with fp32 master weights)."""
+        if self.compute_dtype is not None:
+            return self.compute_dtype
+        if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+            return torch.bfloat16
+        return torch.float32
 
     def count_parameters(self):
         """Count total and trainable parameters (unet3d.py:225-229)"""

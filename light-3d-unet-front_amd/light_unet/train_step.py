@@ -22,7 +22,10 @@ from .optim import FlatAdamW
 
 class TrainStep:
     def __init__(self, model, loss_cfg=None, lr=1e-4, weight_decay=1e-5, betas=(0.9, 0.999),
-                 eps=1e-8, group=None, ftl_mode="exact", distributed=True):
+                 eps=1e-8, group=None, ftl_mode="exact", distributed=True, dtype=None):
+        """dtype: activation storage of the step (torch.float32 or torch.bfloat16; default the
+        model's compute_dtype, else fp32).  Master weights, AdamW state, gradients and the loss
+        stay fp32."""
         loss_cfg = loss_cfg or {}
         self.alpha = float(loss_cfg.get("alpha", 0.7))
         self.beta = float(loss_cfg.get("beta", 0.3))
@@ -32,6 +35,8 @@ class TrainStep:
         check_mode(ftl_mode)
         self.model = model
         self.engine = model.engine
+        self.act_dtype = dtype or model.compute_dtype or torch.float32
+        self.engine.set_act_dtype(self.act_dtype)
         self.flat = model.flat_parameters()
         self.gflat = torch.zeros_like(self.flat)
         # the update launch also advances the Dropout3d counter (no counter launch per step)
@@ -51,6 +56,7 @@ class TrainStep:
         N, S = x.shape[0], x[0].numel()
         nparts = N * nat.query("l3u_outconv_nblocks", S)
         part = torch.empty(nparts * 3, dtype=torch.float32, device=x.device)
+        self.engine.set_act_dtype(self.act_dtype)
         p, sv = self.engine.forward(self.flat, x, training=self.model.training,
                                     dropout_p=self.model.dropout_p,
                                     counter=self.model._rng_counter, bump_counter=False,

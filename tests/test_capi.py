@@ -56,9 +56,27 @@ def test_ctypes_signatures_match_header():
             assert ctype_of(a) is b, (name, a, b)
 
 
+def test_bf16_twins_mirror_fp32_entry_points():
+    """Every _bf16 twin takes the fp32 entry point's arguments, with some float pointers (the
+    activations) as l3u_bf16 pointers and nothing else changed (fp32 and bf16)."""
+    from light_unet import _native
+    hf = header_functions()
+    twins = [n for n in hf if n.endswith("_bf16") and n != "l3u_cast_f32_bf16"]
+    assert sorted(twins) == sorted(n + "_bf16" for n in _native.BF16_TWINS)
+    for t in twins:
+        a32, a16 = hf[t[:-5]], hf[t]
+        assert len(a32) == len(a16), t
+        nb = 0
+        for x, y in zip(a32, a16):
+            if x != y:
+                assert x.replace("float*", "l3u_bf16*") == y, (t, x, y)
+                nb += 1
+        assert nb >= 1, t
+
+
 def test_host_queries_without_gpu():
     from light_unet import _native
-    assert _native.query("l3u_abi_version") == 1
+    assert _native.query("l3u_abi_version") == 2
     assert _native.query("l3u_dw3_nchunk", 4, 32, 48, 48, 48) == 30   # 3 z-slabs x 10 y-strips
     assert _native.query("l3u_pw_bwd_supported", 16, 32, 48 ** 3) == 1
     assert _native.query("l3u_pw_bwd_supported", 32, 64, 24 ** 3) == 1

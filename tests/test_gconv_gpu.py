@@ -261,8 +261,8 @@ def test_grouped_trainstep_graph_matches_eager(cuda):
     mc = fresh()
     tc = TrainStep(mc, lr=1e-3, weight_decay=1e-5)
     xs, tsb = x.clone(), t.clone()
-    tc.capture(xs, tsb, warmup=2)
-    lc = [tc.replay().item() for _ in range(3)]
+    tc.capture(xs, tsb, warmup=2)   # side-effect free: the replays start at step 1
+    lc = [tc.replay().item() for _ in range(5)]
     assert np.all(np.isfinite(lb))
-    np.testing.assert_array_equal(lb[2:], lc)
+    np.testing.assert_array_equal(lb, lc)
     assert torch.equal(mb.flat_parameters(), mc.flat_parameters())

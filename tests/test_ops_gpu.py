@@ -59,7 +59,10 @@ def xform_ref(y, rec):
 DW_SHAPES = [(2, 3, 7, 6, 9), (1, 2, 5, 5, 5), (2, 4, 12, 12, 12), (4, 16, 48, 48, 48),
              (2, 8, 6, 6, 6), (1, 2, 24, 24, 24), (1, 1, 64, 64, 64),
              # x-quad path edge cases: H not a multiple of the row strip, odd D, WQ odd
-             (2, 3, 7, 10, 8), (1, 2, 9, 52, 20), (2, 2, 33, 4, 4), (1, 3, 3, 8, 12)]
+             (2, 3, 7, 10, 8), (1, 2, 9, 52, 20), (2, 2, 33, 4, 4), (1, 3, 3, 8, 12),
+             # planes above 64 x 64 (LDS-DMA tiles) and W > 128 (register-staged tiles; the
+             # IN-fused backward there takes the two-pass form)
+             (1, 1, 5, 80, 80), (1, 2, 4, 6, 136)]
 
 
 @pytest.mark.parametrize("shape", DW_SHAPES)
@@ -544,49 +547,6 @@ def test_maxpool(cuda, shape, ties, with_add):
     close(dx.view(shape), xr.grad + add, 1e-6, "maxpool bwd")
 
 
-@pytest.mark.parametrize("case", [(2, 8, 4, 3, 4, 5), (4, 32, 16, 24, 24, 24), (2, 128, 64, 6, 6, 6)])
-def test_convt(cuda, case):
-    N, Ci, Co, D, H, W = case
-    Si = D * H * W
-    So = 8 * Si
-    gen = torch.Generator().manual_seed(9)
-    x = torch.randn(N, Ci, D, H, W, generator=gen, dtype=torch.float64)
-    w = torch.randn(Ci, Co, 2, 2, 2, generator=gen, dtype=torch.float64)
-    b = torch.randn(Co, generator=gen, dtype=torch.float64)
-    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
-    y = F.conv_transpose3d(xr, wr, br, stride=2)
-    dy = torch.randn(y.shape, generator=gen, dtype=torch.float64)
-    y.backward(dy)
-    xd, wd, bd = x.float().to(cuda), w.float().to(cuda), b.float().to(cuda)
-    yp = torch.empty(N, Co * 8, Si, device=cuda)
-    nat().call("l3u_pw_fwd", xd.data_ptr(), Ci * Si, wd.data_ptr(), 1, None, yp.data_ptr(),
-               Co * 8 * Si, 0, None, N, Ci, Co * 8, Si, st())
-    # write into the lower half of a concat buffer
-    cat = torch.zeros(N, 2 * Co, So, device=cuda)
-    nat().call("l3u_convt_d2s", yp.data_ptr(), bd.data_ptr(), cat.data_ptr(), 2 * Co * So, N, Co,
-               D, H, W, st())
-    dcat = torch.zeros(N, 2 * Co, So, device=cuda)
-    dcat[:, :Co] = dy.reshape(N, Co, So).float().to(cuda)
-    dyp = torch.empty(N, Co * 8, Si, device=cuda)
-    nat().call("l3u_convt_s2d", dcat.data_ptr(), 2 * Co * So, dyp.data_ptr(), N, Co, D, H, W, st())
-    dx = torch.empty(N, Ci, Si, device=cuda)
-    nat().call("l3u_pw_fwd", dyp.data_ptr(), Co * 8 * Si, wd.data_ptr(), 0, None, dx.data_ptr(),
-               Ci * Si, 0, None, N, Co * 8, Ci, Si, st())
-    P = nat().query("l3u_pw_bwd_weight_nparts", N, Si)
-    part = torch.empty(P * Ci * Co * 8, device=cuda)
-    nat().call("l3u_pw_bwd_weight", xd.data_ptr(), Ci * Si, dyp.data_ptr(), Co * 8 * Si,
-               part.data_ptr(), N, Ci, Co * 8, Si, st())
-    ncs = nat().query("l3u_chan_sum_nblocks", 8 * Si)
-    pb = torch.empty(Co * N * ncs, dtype=torch.float64, device=cuda)
-    nat().call("l3u_chan_sum", dyp.data_ptr(), Co * 8 * Si, pb.data_ptr(), N, Co, 8 * Si, st())
-    torch.cuda.synchronize()
-    close(cat[:, :Co].reshape(y.shape), y, 1e-5, "convT fwd")
-    assert torch.all(cat[:, Co:] == 0)
-    close(dx.view(x.shape), xr.grad, 1e-5, "convT dX")
-    close(part.view(P, Ci, Co * 8).double().sum(0).view(w.shape), wr.grad, 1e-5, "convT dW")
-    close(pb.view(Co, -1).double().sum(1), br.grad, 1e-5, "convT db")
-
-
 @pytest.mark.parametrize("case", [(2, 16, 7 * 6 * 9), (4, 16, 48 ** 3), (1, 32, 64 ** 3)])
 def test_outconv(cuda, case):
     N, C, S = case
@@ -637,28 +597,6 @@ def test_ftl_golden(cuda, golden, case):
     torch.cuda.synchronize()
     assert abs(loss.item() - float(z[f"{case}/loss"])) <= 1e-6 * max(1.0, abs(float(z[f"{case}/loss"])))
     close(dp, torch.from_numpy(z[f"{case}/dpred"]), 1e-5, f"ftl dpred {case}")
-
-
-# ------------------------------------------------------------------------------ AdamW
-def test_adamw_matches_torch(cuda):
-    gen = torch.Generator().manual_seed(11)
-    n = 10007
-    p0 = torch.randn(n, generator=gen)
-    ref = p0.clone().to(cuda).requires_grad_(True)
-    opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=1e-2)
-    p = p0.clone().to(cuda)
-    m, v = torch.zeros_like(p), torch.zeros_like(p)
-    step = torch.zeros(1, dtype=torch.int32, device=cuda)
-    lr = torch.tensor([1e-3], device=cuda)
-    for i in range(5):
-        g = torch.randn(n, generator=gen).to(cuda)
-        ref.grad = g.clone()
-        opt.step()
-        nat().call("l3u_adamw", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n,
-                   lr.data_ptr(), 0.9, 0.999, 1e-8, 1e-2, step.data_ptr(), 1.0, st())
-    torch.cuda.synchronize()
-    assert step.item() == 5
-    close(p, ref.detach(), 1e-6, "adamw")
 
 
 def test_reduce_segments(cuda):
@@ -747,50 +685,6 @@ def test_outconv_ftl_fused(cuda, case):
     ps = part.view(N * nb, C + 1).double().sum(0).cpu()
     close(ps[:C], wr.grad[0], 1e-4, "dw")
     close(ps[C:], br.grad, 1e-4, "db")
-
-
-@pytest.mark.parametrize("shape", [(2, 16, 48, 48, 48), (4, 32, 24, 24, 24), (2, 8, 6, 6, 6),
-                                   (1, 5, 7, 12, 8)])
-@pytest.mark.parametrize("mode", [0, 1, 2])
-def test_dw3_bwd_split_calls(cuda, shape, mode):
-    """l3u_dw3_bwd_data + l3u_dw3_bwd_weight agree with the combined single-pass l3u_dw3_bwd
-    (mode 2 = accumulate into dx).  The combined call sums the taps in another order (packed
-    FMAs), so the comparison is to fp32 rounding: 1e-5 of the tensor's max."""
-    N, C, D, H, W = shape
-    S = D * H * W
-    gen = torch.Generator().manual_seed(31)
-    x = torch.randn(N, C, S, generator=gen).to(cuda)
-    dz = torch.randn(N, C, S, generator=gen).to(cuda)
-    w = torch.randn(C, 27, generator=gen).to(cuda)
-    rec = make_rec(N, C, gen).float().to(cuda) if mode == 1 else None
-    init = torch.randn(N, C, S, generator=gen).to(cuda)
-    nch = nat().query("l3u_dw3_nchunk", N, C, D, H, W)
-    acc = 1 if mode == 2 else 0
-
-    def run(split):
-        dx = init.clone()
-        dwp = torch.full((C * N * nch * 27,), float("nan"), device=cuda)
-        inp = torch.full((C * N * nch * 2,), float("nan"), dtype=torch.float64, device=cuda)
-        r = rec.data_ptr() if rec is not None else None
-        ip = inp.data_ptr() if rec is not None else None
-        if split:
-            nat().call("l3u_dw3_bwd_data", dz.data_ptr(), C * S, x.data_ptr(), C * S, w.data_ptr(), r,
-                       dx.data_ptr(), C * S, acc, ip, N, C, D, H, W, st())
-            nat().call("l3u_dw3_bwd_weight", dz.data_ptr(), C * S, x.data_ptr(), C * S, w.data_ptr(),
-                       r, dwp.data_ptr(), N, C, D, H, W, st())
-        else:
-            nat().call("l3u_dw3_bwd", dz.data_ptr(), C * S, x.data_ptr(), C * S, w.data_ptr(), r,
-                       dx.data_ptr(), C * S, acc, dwp.data_ptr(), ip, N, C, D, H, W, st())
-        torch.cuda.synchronize()
-        return dx, dwp, inp
-
-    a, b = run(False), run(True)
-    close(a[0], b[0], 1e-5, f"dx {shape} mode{mode}")
-    close(a[1].view(C, -1, 27).double().sum(1), b[1].view(C, -1, 27).double().sum(1), 1e-5,
-          f"dW {shape} mode{mode}")
-    if rec is not None:
-        close(a[2].view(C, N, -1, 2).sum(2), b[2].view(C, N, -1, 2).sum(2), 1e-5,
-              f"IN sums {shape}")
 
 
 # (N, Ci, Co, D, H, W): the network's three up-blocks (low-res volumes) plus ragged ones
@@ -941,44 +835,6 @@ def test_pw_bwd_tail_equals_apply_then_pw_bwd(cuda, shape):
         close(outs[1][1], outs[0][1], 1e-5, f"dW sel{sel} {shape}")
 
 
-@pytest.mark.parametrize("shape", [(4, 16, 48 ** 3), (2, 8, 1000), (1, 16, 7 * 9 * 12)])
-def test_outconv_bwd_tail_equals_outconv_bwd_then_reduce(cuda, shape):
-    """l3u_outconv_bwd_tail == l3u_outconv_bwd (dh, weight partials: bitwise) followed by
-    l3u_norm_act_bwd_reduce on dh (per-channel sums, to fp rounding: other block sizes)."""
-    N, C, S = shape
-    gen = torch.Generator().manual_seed(44)
-    t = lambda *s: torch.randn(*s, generator=gen).to(cuda)  # noqa: E731
-    dp, p = t(N, S), torch.rand(N, S, generator=gen).to(cuda)
-    h, y2, r = t(N, C, S), t(N, C, S), t(N, C, S)
-    w = t(C)
-    rec2 = make_rec(N, C, gen).float().to(cuda)
-    recr = make_rec(N, C, gen).float().to(cuda)
-    nb = nat().query("l3u_outconv_nblocks", S)
-    outs = []
-    for tail in (False, True):
-        dh = torch.empty(N, C, S, device=cuda)
-        po = torch.empty(N * nb * (C + 1), dtype=torch.float64, device=cuda)
-        tp = torch.empty(C * N * nb * 3, dtype=torch.float64, device=cuda)
-        a = (dp.data_ptr(), p.data_ptr(), None, None, 0.7, 0.3, 0.75, 1e-6, None, h.data_ptr(), C * S,
-             w.data_ptr(), dh.data_ptr(), C * S, po.data_ptr(), None)
-        if tail:
-            nat().call("l3u_outconv_bwd_tail", *a, y2.data_ptr(), C * S, rec2.data_ptr(), r.data_ptr(),
-                       C * S, recr.data_ptr(), tp.data_ptr(), N, C, S, st())
-            sums = tp.view(C, N, nb, 3).sum(2)
-        else:
-            nat().call("l3u_outconv_bwd", *a, N, C, S, st())
-            nr = nat().query("l3u_norm_act_nblocks", S)
-            rp = torch.empty(C * N * nr * 3, dtype=torch.float64, device=cuda)
-            nat().call("l3u_norm_act_bwd_reduce", dh.data_ptr(), C * S, h.data_ptr(), C * S,
-                       y2.data_ptr(), C * S, rec2.data_ptr(), r.data_ptr(), C * S, recr.data_ptr(),
-                       rp.data_ptr(), N, C, S, st())
-            sums = rp.view(C, N, nr, 3).sum(2)
-        torch.cuda.synchronize()
-        outs.append((dh, po, sums))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    close(outs[1][2], outs[0][2], 1e-6, "tail sums")
-
-
 @pytest.mark.parametrize("shape", [(4, 16, 48, 48, 48), (2, 8, 5, 6, 8), (1, 16, 7, 3, 12)])
 def test_front_fwd(cuda, shape):
     """l3u_front_fwd (first block, one input channel): shortcut r = wr*x, z1 = depthwise3(x),
@@ -1002,7 +858,7 @@ def test_front_fwd(cuda, shape):
     sr = torch.empty(N * C * nb * 3, device=cuda)
     nat().call("l3u_front_fwd", dev[0].data_ptr(), S, dev[1].data_ptr(), dev[2].data_ptr(),
                dev[3].data_ptr(), z1d.data_ptr(), y1d.data_ptr(), rd.data_ptr(), s1.data_ptr(),
-               sr.data_ptr(), N, C, D, H, W, st())
+               sr.data_ptr(), None, N, C, D, H, W, st())
     torch.cuda.synchronize()
     close(z1d, z1, 1e-6, "z1")
     close(y1d, y1, 1e-6, "y1")
@@ -1020,29 +876,32 @@ def test_front_fwd(cuda, shape):
         close(p[..., 2], m2, 1e-5, "block M2")
 
 
-def test_adamw_tick_equals_adamw(cuda):
-    """l3u_adamw_tick (one launch; the last workgroup advances the counters) == l3u_adamw +
-    its step increment, bitwise; the extra counter advances once per call, the ticket resets."""
+# ------------------------------------------------------------------------------ AdamW
+def test_adamw_tick_matches_torch(cuda):
+    """l3u_adamw_tick (one launch; the last workgroup advances the counters) == torch.optim.AdamW
+    (trainer.py:75-79) to fp32 rounding; the extra counter advances once per call, the ticket
+    resets."""
     gen = torch.Generator().manual_seed(12)
     n = 217228
-    p0 = torch.randn(n, generator=gen).to(cuda)
-    pa, pb = p0.clone(), p0.clone()
-    ma, va, mb, vb = (torch.zeros(n, device=cuda) for _ in range(4))
-    sa = torch.zeros(1, dtype=torch.int32, device=cuda)
+    p0 = torch.randn(n, generator=gen)
+    ref = p0.clone().to(cuda).requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=1e-2)
+    pb = p0.clone().to(cuda)
+    mb, vb = torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
     sb = torch.zeros(1, dtype=torch.int32, device=cuda)
     ticket = torch.zeros(1, dtype=torch.int32, device=cuda)
     ctr = torch.full((1,), 7, dtype=torch.int32, device=cuda)
     lr = torch.tensor([1e-3], device=cuda)
     for _ in range(5):
         g = torch.randn(n, generator=gen).to(cuda)
-        nat().call("l3u_adamw", pa.data_ptr(), g.data_ptr(), ma.data_ptr(), va.data_ptr(), n,
-                   lr.data_ptr(), 0.9, 0.999, 1e-8, 1e-2, sa.data_ptr(), 1.0, st())
+        ref.grad = g.clone()
+        opt.step()
         nat().call("l3u_adamw_tick", pb.data_ptr(), g.data_ptr(), mb.data_ptr(), vb.data_ptr(), n,
                    lr.data_ptr(), 0.9, 0.999, 1e-8, 1e-2, sb.data_ptr(), 1.0, ticket.data_ptr(),
                    ctr.data_ptr(), st())
     torch.cuda.synchronize()
-    assert sa.item() == sb.item() == 5 and ctr.item() == 12 and ticket.item() == 0
-    assert torch.equal(pa, pb) and torch.equal(ma, mb) and torch.equal(va, vb)
+    assert sb.item() == 5 and ctr.item() == 12 and ticket.item() == 0
+    close(pb, ref.detach(), 1e-6, "adamw")
 
 
 @pytest.mark.parametrize("shape", [(4, 32, 16, 48 ** 3), (4, 64, 32, 24 ** 3), (4, 128, 64, 12 ** 3),
