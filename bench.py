@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=40)   # ~10-30 s of host work
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the bf16 (config 3) step timing")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in autograd step timing")
     ap.add_argument("--ftl-mode", default="exact", choices=["exact", "local"])
     ap.add_argument("--no-sliding", action="store_true", help="skip the config-4 inference timing")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (32->256, 64^3) timing")
@@ -73,10 +75,10 @@ def synthetic_pool(n_pool, bs, size, rank, device):
     return pool
 
 
-def dw_bytes(N, C, S):
+def dw_bytes(N, C, S, e=4):
     """Algorithmic HBM bytes of one depthwise backward (data + weight gradient):
-    read dZ + read X + write dX (fp32) + 27 weights."""
-    return 4 * (3 * N * C * S) + 4 * 27 * C
+    read dZ + write dX (fp32 gradients) + read X (e = 4 fp32 / 2 bf16 activations) + 27 weights."""
+    return 4 * (2 * N * C * S) + e * N * C * S + 4 * 27 * C
 
 
 def pmc_traffic(N, C, size):
@@ -131,6 +133,164 @@ class KernelTimer:
         e1.record(s)
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
+
+
+class StepRecorder:
+    """Records every C-ABI call (name, arguments: real shapes and buffers) of one eager training
+    step; `time_calls` then re-issues selected calls back-to-back between two HIP events on the
+    launch stream, giving each call's own average duration (warm caches: the call's inputs were
+    just touched, so the MALL may serve part of them; the rocprof in-step figures are in
+    profiles/)."""
+
+    def __init__(self):
+        self.calls = []
+        self.keep = []
+
+    def wrap(self, nat, engine):
+        """Record nat.call; every activation / workspace tensor the engine allocates during the
+        recorded step is kept alive here, so that re-issued calls touch only live buffers
+        (host-side argument structs are kept alive by their pointer objects, _native.norm_src_ptr).
+        Returns the restore function."""
+        orig = nat.call
+        e_empty, e_f32 = engine._empty, engine._f32
+
+        def call(name, *args):
+            self.calls.append((name, args))
+            orig(name, *args)
+
+        def empty(*a, **k):
+            t = e_empty(*a, **k)
+            self.keep.append(t)
+            return t
+
+        def f32(*a, **k):
+            t = e_f32(*a, **k)
+            self.keep.append(t)
+            return t
+        nat.call = call
+        engine._empty, engine._f32 = empty, f32
+
+        def restore():
+            nat.call = orig
+            del engine._empty, engine._f32   # back to the class methods
+        self.orig = orig
+        return restore
+
+    @staticmethod
+    def time_calls(nat_call, calls, reps=20):
+        s = torch.cuda.current_stream()
+        out = []
+        for name, args in calls:
+            a = args[:-1] + (s.cuda_stream,)
+            for _ in range(3):
+                nat_call(name, *a)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(reps):
+                nat_call(name, *a)
+            e1.record(s)
+            torch.cuda.synchronize()
+            out.append(e0.elapsed_time(e1) / reps)
+        return out
+
+
+def _e(name):
+    return 2 if name.endswith("_bf16") else 4
+
+
+def call_bytes(name, a):
+    """Algorithmic HBM bytes of one C-ABI call from its arguments (activations e = 4
+    (fp32) or 2 (the _bf16 twins), gradients fp32), with a shape label; None when the call is not
+    in the depthwise or GEMM families."""
+    e, base = _e(name), name[:-5] if name.endswith("_bf16") else name
+    if base == "l3u_dw3_fwd":     # (x, xns, w, rec, src, y, yns, N, C, D, H, W)
+        N, C, D, H, W = a[7:12]
+        S = D * H * W
+        return "dw", f"fwd [{N},{C},{D}x{H}x{W}]", e * 2 * N * C * S + 108 * C
+    if base == "l3u_dw3_bwd":     # (dz, dzns, x, xns, w, rec, dx, dxns, acc, dwp, inp, N, C, D, H, W)
+        N, C, D, H, W = a[11:16]
+        S = D * H * W
+        acc = a[8]
+        return ("dw", f"bwd{'+IN' if a[5] else ''}{'+acc' if acc else ''} [{N},{C},{D}x{H}x{W}]",
+                4 * N * C * S * (2 + acc) + e * N * C * S + 108 * C)
+    if base == "l3u_pw_fwd":      # (x, xns, w, trans, bias, y, yns, acc, part, N, K, J, S)
+        N, K, J, S = a[9:13]
+        if a[3]:                  # W^T dy of a backward (fp32 operands)
+            e = 4
+        return "gemm", f"pw_fwd{'T' if a[3] else ''} {K}->{J} [{N},{S}]", e * N * S * (K + J * (1 + a[7]))
+    if base == "l3u_pw_fwd2":     # (x, xns, wr, r, rns, so, z1, z1ns, w1, y1, y1ns, s1, N, K, J, S)
+        N, K, J, S = a[12:16]
+        return "gemm", f"pw_fwd2 2x{K}->{J} [{N},{S}]", e * N * S * 2 * (K + J)
+    if base == "l3u_pw_bwd":      # (dy, dyns, y, yns, rec, ip, np, x, xns, w, dx, dxns, acc, part, N, J, K, S)
+        N, J, K, S = a[14:18]
+        pro = a[2] is not None
+        return ("gemm", f"pw_bwd {J}->{K}{'+IN' if pro else ''} [{N},{S}]",
+                N * S * (4 * J + (e * J if pro else 0) + e * K + 4 * K * (1 + a[12])))
+    if base == "l3u_pw_bwd_tail":  # (dout, dns, out, ons, yr, yns, rec, pn, ntp, sel, x, xns, w, dx, dxns, acc, part, N, J, K, S)
+        N, J, K, S = a[17:21]
+        return ("gemm", f"pw_bwd_tail{a[9]} {J}->{K} [{N},{S}]",
+                N * S * (4 * J + 2 * e * J + e * K + 4 * K * (1 + a[15])))
+    if base == "l3u_pw_bwd_weight":  # (dy, dyns, x, xns, part, N, J, K, S)
+        N, J, K, S = a[5:9]
+        return "gemm", f"pw_bwd_weight {J}x{K} [{N},{S}]", N * S * (4 * J + e * K)
+    if base == "l3u_convt_fwd":   # (x, xns, w, b, y, yns, N, ci, co, d, h, w)
+        N, ci, co, d, h, w = a[6:12]
+        Si = d * h * w
+        return "gemm", f"convt_fwd {ci}->{co} [{N},{d}x{h}x{w}]", e * N * Si * (ci + 8 * co)
+    if base in ("l3u_convt_bwd", "l3u_convt_bwd_fused"):  # (dcat, dns, prev, pns, w, dprev, dpns, pw, pb, N, ci, co, d, h, w)
+        N, ci, co, d, h, w = a[9:15]
+        Si = d * h * w
+        return "gemm", f"convt_bwd {ci}<-{co} [{N},{d}x{h}x{w}]", N * Si * (4 * 8 * co + e * ci + 4 * ci)
+    if base == "l3u_front_fwd":   # (x, xns, wdw, wpw, wsc, z1, y1, r, s1, so, xc, N, cout, d, h, w)
+        N, co, d, h, w = a[11:16]
+        S = d * h * w
+        return ("dw", f"front (1ch dw + 2 rank-1 pw) [{N},1->{co},{d}x{h}x{w}]",
+                4 * N * S + e * N * S * (1 + 2 * co + (1 if a[10] else 0)))
+    return None
+
+
+def family_rooflines(nat_call, calls):
+    """Per-launch and aggregate achieved bandwidth of the depthwise and GEMM families of one
+    training step (every call of the family, timed one by one)."""
+    sel = []
+    for name, args in calls:
+        r = call_bytes(name, args)
+        if r is not None:
+            sel.append((name, args, r))
+    ms = StepRecorder.time_calls(nat_call, [(n, a) for n, a, _ in sel])
+    fam = {"dw": [], "gemm": []}
+    for (name, _, (f, label, b)), t in zip(sel, ms):
+        fam[f].append({"call": label, "us": round(1000 * t, 2), "bytes": int(b),
+                       "achieved": round(b / (t * 1e-3) / 1e9, 1),
+                       "frac": round(b / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+    out = {}
+    for f, rows in fam.items():
+        tb = sum(r["bytes"] for r in rows)
+        tt = sum(r["us"] for r in rows) * 1e-6
+        out[f] = {"launches": len(rows), "bytes": tb, "us": round(tt * 1e6, 1),
+                  "achieved": round(tb / tt / 1e9, 1) if tt else None,
+                  "frac": round(tb / tt / 1e9 / HBM_PEAK_GBS, 4) if tt else None, "calls": rows}
+    return out
+
+
+def gemm_mfma_evidence(top=5):
+    """MFMA-busy fractions of the step's GEMM launches from the committed rocprofv3 passes
+    (tools/pmc_step.sh + tools/pmc_gemm.sh -> tools/pmc_launch_json.py -> profiles/*_pmc_step.json)."""
+    import glob
+    files = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r2*_pmc_step.json")))]
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        rec = json.load(f)
+    items = [i for i in rec["items"] if "mfma_util" in i and i["mfma_busy_cycles"] > 0]
+    items.sort(key=lambda i: -i["pmc_dur_us"])
+    return {"source": os.path.relpath(files[-1], ROOT),
+            "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)",
+            "ceiling_note": "fp32 MFMA at the HBM roofline: 5.5 flop/B x 8 TB/s = 44 TFLOP/s = 0.28 of "
+                            "the 157 TFLOP/s fp32 matrix peak",
+            "top": [{"kernel": i["kernel"], "pmc_dur_us": i["pmc_dur_us"],
+                     "mfma_util": round(i["mfma_util"], 4), "traffic": int(i["traffic"])}
+                    for i in items[:top]]}
 
 
 def dw_bwd_cache_exceeding(device, N=8, C=32, L=48, reps=30):
@@ -352,6 +512,102 @@ def grouped_bench(device, steps=10, warmup=3, bs=4, size=48):
             "ms_per_step": round(1000 * dt / steps, 4), "final_loss": round(lv, 6)}
 
 
+def dropin_bench(device, steps=20, warmup=5, bs=4, size=48, dropout=0.1):
+    """The drop-in path l3u_plugin.install() gives the reference Trainer (trainer.py:222-234):
+    model(x) -> FocalTverskyLoss -> zero_grad -> backward (per-parameter autograd) ->
+    torch.optim.AdamW.step -> loss.item() (a host sync every step), eager, one GPU."""
+    from light_unet.models.losses import FocalTverskyLoss
+    from light_unet.models.unet3d import Lightweight3DUNet
+    torch.manual_seed(42)
+    model = Lightweight3DUNet(dropout_p=dropout).to(device).train()
+    crit = FocalTverskyLoss()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-5)
+    rng = np.random.default_rng(42)
+    x = torch.from_numpy(rng.random((bs, 1, size, size, size), dtype=np.float32)).to(device)
+    t = torch.from_numpy((rng.random((bs, 1, size, size, size)) > 0.97).astype(np.float32)).to(device)
+
+    def one():
+        loss = crit(model(x), t)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return loss.item()
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        lv = one()
+    dt = time.perf_counter() - t0
+    return {"workload": "drop-in autograd step (model -> FocalTversky -> backward -> torch AdamW -> "
+                        f"loss.item()), {size}^3, bs {bs}, eager", "dropin_step_ms": round(1000 * dt / steps, 4),
+            "patches_per_s": round(steps * bs / dt, 2), "final_loss": round(lv, 6)}
+
+
+def bf16_bench(device, args, enc, world, rank, pool):
+    """BASELINE config 3: the same step with bf16 activation storage (fp32 master weights, AdamW
+    state, gradients and accumulation), graph-replayed, same pool and exchange as the headline;
+    with the roofline of its dominant call (the _bf16 depthwise backward)."""
+    from light_unet import _native as nat
+    from light_unet.models.unet3d import Lightweight3DUNet
+    from light_unet.train_step import TrainStep
+    torch.manual_seed(42)
+    model = Lightweight3DUNet(encoder_channels=list(enc), dropout_p=args.dropout).to(device).train()
+    if world > 1:
+        dist.broadcast(model.flat_parameters(), 0)
+    step = TrainStep(model, {"alpha": 0.7, "beta": 0.3, "gamma": 0.75}, lr=1e-4, weight_decay=1e-5,
+                     ftl_mode=args.ftl_mode, dtype=torch.bfloat16)
+    xs, ts = [b[0] for b in pool], [b[1] for b in pool]
+    for i in range(2):
+        step(xs[i], ts[i])
+    torch.cuda.synchronize()
+    rec = StepRecorder()
+    restore = rec.wrap(nat, model.engine)
+    step(xs[2], ts[2])
+    torch.cuda.synchronize()
+    restore()
+    orig = rec.orig
+    N, S, cdom = args.batch, args.size ** 3, 2 * enc[0]
+    dom = [(n, a) for n, a in rec.calls if n == "l3u_dw3_bwd_bf16" and a[-5] == cdom and a[-4] == args.size]
+    dom_ms = StepRecorder.time_calls(orig, dom[:1], reps=50)[0] if dom else None
+    xt = pool[0].clone()
+    step.capture(xt[0], xt[1], warmup=2)
+    for i in range(args.warmup):
+        xt.copy_(pool[i % 8], non_blocking=True)
+        step.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        xt.copy_(pool[i % 8], non_blocking=True)
+        loss = step.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    lv = float(loss.item())
+    if not np.isfinite(lv):
+        raise SystemExit(f"bf16 step: non-finite loss {lv}")
+    b = dw_bytes(N, cdom, S, e=2)
+    ach = b / (dom_ms * 1e-3) / 1e9 if dom_ms else None
+    return {"workload": "same step, bf16 activation storage (fp32 weights / AdamW / gradients / "
+                        "accumulation), graph-replayed", "n_gpus": world,
+            "patches_per_s": round(world * args.batch * args.steps / dt, 2),
+            "ms_per_step": round(1000 * dt / args.steps, 4), "launches": len(rec.calls),
+            "final_loss": round(lv, 6),
+            "roofline": {"kernel": f"l3u_dw3_bwd_bf16 [{N},{cdom},{args.size}^3]", "bound": "hbm",
+                         "algorithmic_bytes": b, "avg_launch_ms": round(dom_ms, 5) if dom_ms else None,
+                         "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None}}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -386,18 +642,25 @@ def main():
     xt_static = pool[0].clone()
     x_static, t_static = xt_static[0], xt_static[1]
 
-    # roofline leg (eager, instrumented): HIP events around the dominant kernel's launches
+    # roofline leg (eager, instrumented): every C-ABI call of one step recorded at its real shapes
+    # and buffers; the dominant call and the depthwise / GEMM families re-timed from the record
     N, S = args.batch, args.size ** 3
     cdom = 2 * enc[0]      # up3.res_block conv1.depthwise: [N, 2*c0, D^3] backward
-    # l3u_dw3_bwd args end with (..., N, C, D, H, W, stream)
     dom_name = "l3u_dw3_bwd" + ("_bf16" if args.dtype == "bf16" else "")
-    timer = KernelTimer((dom_name,), lambda a: a[-5] == cdom and a[-4] == args.size)
-    orig = timer.wrap(nat)
-    for i in range(3):
+    for i in range(2):
         step(xs[i % 8], ts[i % 8])
     torch.cuda.synchronize()
-    nat.call = orig
-    dom_ms = timer.mean_ms(orig)
+    rec = StepRecorder()
+    restore = rec.wrap(nat, model.engine)
+    step(xs[2], ts[2])
+    torch.cuda.synchronize()
+    restore()
+    orig = rec.orig
+    dom_calls = [(n, a) for n, a in rec.calls if n == dom_name and a[-5] == cdom and a[-4] == args.size]
+    dom_ms = StepRecorder.time_calls(orig, dom_calls[:1], reps=50)[0] if dom_calls else None
+    fams = family_rooflines(orig, rec.calls) if rank == 0 else None
+    n_launch_calls = len(rec.calls)
+    rec = None   # releases the recorded step's buffers
 
     if args.no_graph:
         def run(i):
@@ -435,13 +698,15 @@ def main():
     cfg5 = config5_bench(device, world, rank) if not args.no_config5 else None   # every rank
     cfg5 = cfg5 if rank == 0 else None
     grouped = grouped_bench(device) if (rank == 0 and not args.no_grouped) else None
+    bf16 = bf16_bench(device, args, enc, world, rank, pool) if (args.dtype == "fp32" and not args.no_bf16) else None
+    dropin = dropin_bench(device) if (rank == 0 and not args.no_dropin) else None
     fwd1 = fwd_ms_per_patch(model, 1, args.size, device) if rank == 0 else None
     fwd4 = fwd_ms_per_patch(model, args.batch, args.size, device) if rank == 0 else None
     out = None
     if rank == 0:
         patches = world * args.batch * args.steps
         value = patches / elapsed
-        dbytes = dw_bytes(N, cdom, S)
+        dbytes = dw_bytes(N, cdom, S, e=2 if args.dtype == "bf16" else 4)
         achieved = dbytes / (dom_ms * 1e-3) / 1e9 if dom_ms else None
         traffic, traffic_src = pmc_traffic(N, cdom, args.size)
         out = {
@@ -455,7 +720,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": args.dtype,
             "data": "synthetic (x~U[0,1), target Bernoulli(0.03); random-init weights, seed 42)",
             "config": {"workload": f"Lightweight3DUNet {'->'.join(map(str, enc))} train step "
                                    f"(fwd+FocalTversky+bwd+AdamW), {args.size}^3 patches",
@@ -469,6 +734,9 @@ def main():
             "sliding_window_256": sliding,
             "config5": cfg5,
             "grouped_1gpu": grouped,
+            "bf16": bf16,
+            "dropin": dropin,
+            "launches_per_step": n_launch_calls,
             "roofline": {
                 "kernel": f"l3u_dw3_bwd [{N},{cdom},{args.size}^3] (up3.res_block.conv1.depthwise "
                           "backward: one single-pass launch, data and weight gradients from one "
@@ -483,6 +751,9 @@ def main():
                 "algorithmic_bytes": dbytes,
                 "avg_launch_ms": round(dom_ms, 5) if dom_ms else None,
                 "cache_exceeding": dw_bwd_cache_exceeding(device),
+                "depthwise": fams["dw"],
+                "gemm": dict(fams["gemm"], calls=sorted(fams["gemm"]["calls"], key=lambda r: -r["us"])[:5],
+                             mfma=gemm_mfma_evidence()),
             },
         }
         if world == 1 and not args.no_cpu_baseline:

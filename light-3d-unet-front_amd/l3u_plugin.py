@@ -47,14 +47,21 @@ def load():
     importlib.import_module(ALIAS + ".models.unet3d")
     importlib.import_module(ALIAS + ".models.losses")
     importlib.import_module(ALIAS + ".utils")
+    importlib.import_module(ALIAS + ".fast_trainer")
     return mod
 
 
-def install():
+def install(fast_step=False):
     """Bind this build's model and loss into the already-importable reference package.
     Returns {module: [names]} of what was replaced.  Raises ImportError when the reference's
-    light_unet.models.{unet3d,losses} cannot be imported (nothing is half-installed)."""
+    light_unet.models.{unet3d,losses} cannot be imported (nothing is half-installed).
+
+    fast_step=True also replaces Trainer.train_epoch / Trainer._train_epoch_step_based
+    (trainer.py:208-347) with the graph-replayed TrainStep loops of light_unet/fast_trainer.py
+    (same batches, update, TensorBoard scalars and return values; no per-step host sync; RCCL
+    data parallelism when torch.distributed is initialised).  Needs light_unet.core.trainer."""
     amd = load()
+    trainer_mod = importlib.import_module("light_unet.core.trainer") if fast_step else None
     src = {
         "Lightweight3DUNet": sys.modules[ALIAS + ".models.unet3d"].Lightweight3DUNet,
         "FocalTverskyLoss": sys.modules[ALIAS + ".models.losses"].FocalTverskyLoss,
@@ -72,5 +79,9 @@ def install():
         for name in REPLACED[modname]:
             setattr(mod, name, src[name])
         done[modname] = list(REPLACED[modname])
+    if fast_step:
+        fast = importlib.import_module(ALIAS + ".fast_trainer")
+        fast.bind(trainer_mod.Trainer)
+        done["light_unet.core.trainer"] = ["Trainer.train_epoch", "Trainer._train_epoch_step_based"]
     amd.installed_into = done
     return done

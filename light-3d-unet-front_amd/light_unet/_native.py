@@ -102,7 +102,9 @@ class NormSrc(ctypes.Structure):
 
 
 def norm_src_ptr(s):
-    return None if s is None else ctypes.addressof(s)
+    """A pointer argument to `s` that keeps `s` alive as long as the argument itself (so a
+    recorded call can be re-issued later)."""
+    return None if s is None else ctypes.pointer(s)
 
 
 def load():

@@ -1,0 +1,163 @@
+"""install(fast_step=True): the reference Trainer's loops (trainer.py:208-347) on the
+graph-replayed TrainStep agree with the drop-in autograd loop they replace.
+
+The Trainer here is a stand-in with the attributes the reference loops read (model, criterion,
+optimizer, loaders, writer, config, mode flags); its own `train_epoch` / step-based loop are the
+plain drop-in path written out (model(x) -> criterion -> zero_grad -> backward -> torch AdamW ->
+loss.item() every step).  Both versions start from the same weights and see the same batches.
+
+Tolerances: per-step losses 1e-5 relative (fp32: FlatAdamW vs torch.optim.AdamW and the fused vs
+autograd loss differ by rounding only; dropout 0 so that neither draws anything random), and the
+parameter difference after the run <= 2e-2 of the L2 size of the update the run made.  Not an
+elementwise bound: Adam normalises each gradient element, so a parameter whose gradient is at
+rounding level (the scale-invariant conv feeding an InstanceNorm, e.g. init_conv.shortcut.0.weight)
+moves by ~lr per step in a direction set by rounding, in either implementation.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+class _Writer:
+    def __init__(self):
+        self.rec = []
+
+    def add_scalar(self, tag, value, step):
+        self.rec.append((tag, float(value), int(step)))
+
+
+class StandInTrainer:
+    """The attributes light_unet/core/trainer.py's loops use, with the drop-in autograd loops."""
+
+    def __init__(self, cuda, batches, step_based=False, fl=None, dl=None, ratio=1.0):
+        from light_unet.models.losses import get_loss_function
+        from light_unet.models.unet3d import Lightweight3DUNet
+        torch.manual_seed(42)
+        self.device = cuda
+        self.model = Lightweight3DUNet(dropout_p=0.0).to(cuda)
+        self.criterion = get_loss_function({"name": "FocalTverskyLoss", "alpha": 0.7,
+                                            "beta": 0.3, "gamma": 0.75})
+        self.optimizer = torch.optim.AdamW(self.model.parameters(), lr=1e-3, weight_decay=1e-5)
+        self.train_loader = batches
+        self.train_dataset = None
+        self.use_mixed_training = False
+        self.use_step_based_mixed = step_based
+        self.fl_loader, self.dlbcl_loader = fl, dl
+        self.config = {"training": {"mixed_domains": {"dlbcl_steps_ratio": ratio}}}
+        self.writer = _Writer()
+        self.step_losses = []
+
+    def _one(self, images, labels):
+        out = self.model(images.to(self.device).float())
+        loss = self.criterion(out, labels.to(self.device))
+        self.optimizer.zero_grad()
+        loss.backward()
+        self.optimizer.step()
+        v = loss.item()
+        self.step_losses.append(v)
+        return v
+
+    def train_epoch(self, epoch):
+        self.model.train()
+        if self.use_step_based_mixed:
+            return self._train_epoch_step_based(epoch)
+        vals = [self._one(x, t) for x, t in self.train_loader]
+        for i, v in enumerate(vals):
+            self.writer.add_scalar("Loss/train_step", v, epoch * len(self.train_loader) + i)
+        return sum(vals) / len(vals)
+
+    def _train_epoch_step_based(self, epoch):
+        nfl = len(self.fl_loader)
+        ndl = round(nfl * self.config["training"]["mixed_domains"]["dlbcl_steps_ratio"])
+        base = epoch * (nfl + ndl)
+        fl = [self._one(x, t) for x, t in self.fl_loader]
+        dl, it = [], iter(self.dlbcl_loader)
+        for _ in range(ndl):
+            try:
+                x, t = next(it)
+            except StopIteration:
+                it = iter(self.dlbcl_loader)
+                x, t = next(it)
+            dl.append(self._one(x, t))
+        for i, v in enumerate(fl):
+            self.writer.add_scalar("Loss/train_step", v, base + i)
+            self.writer.add_scalar("Loss/fl_step", v, base + i)
+        for i, v in enumerate(dl):
+            self.writer.add_scalar("Loss/train_step", v, base + nfl + i)
+            self.writer.add_scalar("Loss/dlbcl_step", v, base + nfl + i)
+        return (sum(fl) + sum(dl)) / (len(fl) + len(dl))
+
+
+def _batches(seed, n, bs=2, size=32, last_bs=None):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        b = last_bs if (last_bs and i == n - 1) else bs
+        x = rng.random((b, 1, size, size, size), dtype=np.float32)
+        t = (rng.random((b, 1, size, size, size)) > 0.9).astype(np.float32)
+        out.append((torch.from_numpy(x), torch.from_numpy(t)))
+    return out
+
+
+def _fast_cls():
+    from light_unet import fast_trainer
+    cls = type("FastTrainer", (StandInTrainer,), {})
+    fast_trainer.bind(cls)
+    return cls
+
+
+def _flat(model):
+    return torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+
+
+def _compare(ref, fast, p0, rtol=1e-5):
+    lr = [v for tag, v, _ in ref.writer.rec if tag == "Loss/train_step"]
+    lf = [v for tag, v, _ in fast.writer.rec if tag == "Loss/train_step"]
+    assert len(lr) == len(lf) > 0
+    np.testing.assert_allclose(lf, lr, rtol=rtol, atol=0)
+    assert [(t, s) for t, _, s in ref.writer.rec] == [(t, s) for t, _, s in fast.writer.rec]
+    pr, pf = _flat(ref.model), _flat(fast.model)
+    rel = float((pr - pf).norm() / (pr - p0).norm())
+    assert rel <= 2e-2, rel
+
+
+def test_fast_train_epoch_matches_dropin_loop(cuda):
+    # four steps of bs 2 at 32^3 plus a ragged last batch (bs 1: the eager step) over two epochs
+    batches = _batches(0, 5, last_bs=1)
+    ref = StandInTrainer(cuda, batches)
+    fast = _fast_cls()(cuda, batches)
+    p0 = _flat(ref.model).clone()
+    for ep in range(2):
+        a = ref.train_epoch(ep)
+        b = fast.train_epoch(ep)
+        assert abs(a - b) <= 1e-5 * abs(a)
+    _compare(ref, fast, p0)
+    # the torch optimizer's state mirrors the flat AdamW moments (checkpoint content)
+    st = fast.optimizer.state
+    q0 = next(fast.model.parameters())
+    r0 = next(ref.model.parameters())
+    assert float(st[q0]["step"]) == float(ref.optimizer.state[r0]["step"]) == 10
+    m_f = torch.cat([st[p]["exp_avg"].reshape(-1) for p in fast.model.parameters()])
+    m_r = torch.cat([ref.optimizer.state[p]["exp_avg"].reshape(-1) for p in ref.model.parameters()])
+    assert float((m_f - m_r).norm() / m_r.norm()) <= 2e-2
+
+
+def test_fast_step_based_matches_dropin_loop(cuda):
+    # 3 FL batches, then round(3 * 1.0) = 3 DLBCL steps over a 2-batch loader (re-iterated)
+    fl, dl = _batches(1, 3), _batches(2, 2)
+    ref = StandInTrainer(cuda, None, step_based=True, fl=fl, dl=dl)
+    fast = _fast_cls()(cuda, None, step_based=True, fl=fl, dl=dl)
+    p0 = _flat(ref.model).clone()
+    a = ref.train_epoch(0)
+    b = fast.train_epoch(0)
+    assert abs(a - b) <= 1e-5 * abs(a)
+    assert len(ref.step_losses) == 6
+    tags = [t for t, _, _ in fast.writer.rec]
+    assert tags.count("Loss/fl_step") == 3 and tags.count("Loss/dlbcl_step") == 3
+    ref.writer.rec = [r for r in ref.writer.rec]
+    fast.writer.rec = [r for r in fast.writer.rec if not r[0].startswith(("Domain/", "Loss/fl_avg",
+                                                                            "Loss/dlbcl_avg",
+                                                                            "Loss/combined"))]
+    _compare(ref, fast, p0)

@@ -26,7 +26,10 @@ def _standin(tmp_path):
     (base / "core" / "trainer.py").write_text(
         "from light_unet.models.unet3d import Lightweight3DUNet\n"
         "from light_unet.models.losses import get_loss_function\n"
-        "from light_unet.utils import sliding_window_inference_3d\n")
+        "from light_unet.utils import sliding_window_inference_3d\n\n"
+        "class Trainer:\n"
+        "    def train_epoch(self, epoch):\n        return 'reference'\n"
+        "    def _train_epoch_step_based(self, epoch):\n        return 'reference'\n")
 
 
 def test_install_binds_model_and_loss(tmp_path):
@@ -49,6 +52,36 @@ def test_install_binds_model_and_loss(tmp_path):
         loss = trainer.get_loss_function({{"name": "FocalTverskyLoss"}})
         assert type(loss).__name__ == "FocalTverskyLoss"
         print("OK", sorted(done))
+    """)
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout
+
+
+def test_install_fast_step_binds_trainer_loops(tmp_path):
+    _standin(tmp_path)
+    script = textwrap.dedent(f"""
+        import importlib.util, sys
+        sys.path.insert(0, {str(tmp_path)!r})
+        spec = importlib.util.spec_from_file_location("l3u_plugin", {os.path.join(PKG, "l3u_plugin.py")!r})
+        plug = importlib.util.module_from_spec(spec); spec.loader.exec_module(plug)
+        done = plug.install(fast_step=True)
+        from light_unet.core.trainer import Trainer
+        assert Trainer.train_epoch.__module__ == "l3u_amd.fast_trainer"
+        assert Trainer._train_epoch_step_based.__module__ == "l3u_amd.fast_trainer"
+        # the reference loops stay reachable (fallback for losses other than FocalTversky)
+        orig = Trainer._l3u_reference_loops
+        assert orig["train_epoch"](None, 0) == "reference"
+        assert "light_unet.core.trainer" in done
+        # binding twice keeps the reference originals
+        plug.install(fast_step=True)
+        assert Trainer._l3u_reference_loops["train_epoch"](None, 0) == "reference"
+        fast = sys.modules["l3u_amd.fast_trainer"]
+        cfg = {{"training": {{"mixed_domains": {{"dlbcl_steps_ratio": 0.5}}}}}}
+        assert fast.dlbcl_step_count(cfg, 7) == round(3.5)
+        cfg["training"]["mixed_domains"]["dlbcl_steps"] = 2
+        assert fast.dlbcl_step_count(cfg, 7) == 2
+        print("OK")
     """)
     r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
