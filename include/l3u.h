@@ -231,6 +231,16 @@ int l3u_outconv_bwd(const float* dp, const float* p, const float* t, const doubl
                     const float* h, long long h_nstride, const float* w, float* dh,
                     long long dh_nstride, double* part, float* loss, int N, int C, int S,
                     hipStream_t stream);
+/* The FocalTversky form of l3u_outconv_bwd with the loss reduction folded in: instead of the
+ * global sums it takes the out_conv forward's FocalTversky partials (ftl_part[ftl_nparts][3],
+ * l3u_outconv_fwd) and every workgroup reduces them itself, in l3u_ftl_reduce's order (so the
+ * sums, the loss and the gradient are bit-identical to l3u_ftl_reduce + l3u_outconv_bwd): the
+ * single-process training step needs no separate reduce launch (losses.py:40-54). */
+int l3u_outconv_bwd_ftl(const float* p, const float* t, const float* ftl_part, int ftl_nparts,
+                        double alpha, double beta, double gamma, double smooth,
+                        const float* gscale, const float* h, long long h_nstride, const float* w,
+                        float* dh, long long dh_nstride, double* part, float* loss, int N, int C,
+                        int S, hipStream_t stream);
 
 /* ---- FocalTverskyLoss (light_unet/models/losses.py:11-54) ----------------------------------
  * sums = {sum p*t, sum p, sum t} over ALL voxels of the batch (pred.view(-1), losses.py:40-46),
@@ -346,6 +356,11 @@ int l3u_outconv_bwd_bf16(const float* dp, const float* p, const float* t, const 
                          const float* gscale, const l3u_bf16* h, long long h_nstride,
                          const float* w, float* dh, long long dh_nstride, double* part, float* loss,
                          int N, int C, int S, hipStream_t stream);
+int l3u_outconv_bwd_ftl_bf16(const float* p, const float* t, const float* ftl_part, int ftl_nparts,
+                             double alpha, double beta, double gamma, double smooth,
+                             const float* gscale, const l3u_bf16* h, long long h_nstride,
+                             const float* w, float* dh, long long dh_nstride, double* part,
+                             float* loss, int N, int C, int S, hipStream_t stream);
 int l3u_front_fwd_bf16(const float* x, long long x_nstride, const float* w_dw, const float* w1,
                        const float* wr, l3u_bf16* z1, l3u_bf16* y1, l3u_bf16* r, float* stat1,
                        float* statr, l3u_bf16* x_copy, int N, int C, int D, int H, int W,

@@ -522,6 +522,17 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
   float wk[27];
 #pragma unroll
   for (int t = 0; t < 27; ++t) wk[t] = w[b.c * 27 + (FLIP ? 26 - t : t)];
+  const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
+  const QMap qm = q_map(b.y0, b.rows, H, W, WQ);
+  auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };   // loads always issue
+  const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
+  // step t consumes input plane zi = z0-1+t; the step count is a compile-time constant and the
+  // loop is fully unrolled, so the two staged registers never move (no back-edge copies that
+  // would force a vmcnt(0) drain of the pipeline).  The first two planes are requested before
+  // the InstanceNorm record is finalized (its partial-sum loads then overlap them).
+  QPre<T> p0, p1;
+  q_fetch(p0, xp + zc(b.z0 - 1), qm);
+  q_fetch(p1, xp + zc(b.z0), qm);
   float sc = 1.f, sh = 0.f, mu = 0.f, rstd = 1.f, kk = 1.f;
   if (XF || EPI == 1) {
     if (has_src) {
@@ -537,16 +548,6 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
   __syncthreads();
   f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0;
   float s1 = 0.f, s2 = 0.f;   // per-thread sums over <= 4*TZ voxels; widened to fp64 per block
-  const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
-  const QMap qm = q_map(b.y0, b.rows, H, W, WQ);
-  auto zc = [&](int z) { return (long long)min(max(z, zlo), zhi) * HW; };   // loads always issue
-  const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
-  // step t consumes input plane zi = z0-1+t; the step count is a compile-time constant and the
-  // loop is fully unrolled, so the two staged registers never move (no back-edge copies that
-  // would force a vmcnt(0) drain of the pipeline)
-  QPre<T> p0, p1;
-  q_fetch(p0, xp + zc(b.z0 - 1), qm);
-  q_fetch(p1, xp + zc(b.z0), qm);
   auto step = [&](int t, QPre<T>& pre) {
     const int zi = b.z0 - 1 + t;
     float* buf = lds + (t & 1) * PP;

@@ -148,11 +148,31 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     const double* __restrict__ sums, double alpha, double beta, double gamma, double smooth,
     const float* __restrict__ gscale, const T* __restrict__ h, long long hns,
     const float* __restrict__ w, float* __restrict__ dh, long long dhns,
-    double* __restrict__ part, float* __restrict__ loss, int C, int S) {
-  extern __shared__ double redd[];   // [4][C+1]
+    double* __restrict__ part, float* __restrict__ loss, int C, int S,
+    const float* __restrict__ fpart = nullptr, int fnp = 0) {
+  extern __shared__ double redd[];   // [4][C+1]; fpart: [3][64]
   __shared__ float coef[2];
+  __shared__ double fsum[3];
   const int n = blockIdx.y, nb = gridDim.x;
   if (dp == nullptr) {
+    if (fpart != nullptr) {
+      // the FocalTversky sums from the out_conv forward's partials, in ftl_sums_kernel's order
+      // (bit-identical to l3u_ftl_reduce): lane-strided fp64 sums, then the 64 lanes in order
+      if (threadIdx.x < 64) {
+        const int l = threadIdx.x;
+        double a = 0, b = 0, c = 0;
+        for (int i = l; i < fnp; i += 64) { a += fpart[i * 3]; b += fpart[i * 3 + 1]; c += fpart[i * 3 + 2]; }
+        redd[l] = a; redd[64 + l] = b; redd[128 + l] = c;
+      }
+      __syncthreads();
+      if (threadIdx.x < 3) {
+        double t = 0;
+        for (int i = 0; i < 64; ++i) t += redd[threadIdx.x * 64 + i];
+        fsum[threadIdx.x] = t;
+      }
+      __syncthreads();
+      sums = fsum;
+    }
     if (threadIdx.x == 0) {
       const FtlCoef r = ftl_coef(sums, alpha, beta, gamma, smooth);
       const double s = gscale ? (double)gscale[0] : 1.0;
@@ -586,14 +606,16 @@ template <typename T>
 int outconv_bwd_impl(const float* dp, const float* p, const float* t, const double* sums,
                      double alpha, double beta, double gamma, double smooth, const float* gscale,
                      const T* h, long long h_nstride, const float* w, float* dh, long long dh_nstride,
-                     double* part, float* loss, int N, int C, int S, hipStream_t stream) {
+                     double* part, float* loss, int N, int C, int S, hipStream_t stream,
+                     const float* fpart = nullptr, int fnp = 0) {
   L3U_REQUIRE(N > 0 && C > 0 && C <= 32 && S > 0);
-  L3U_REQUIRE(dp != nullptr || (t != nullptr && sums != nullptr));
+  L3U_REQUIRE(dp != nullptr || (t != nullptr && (sums != nullptr || (fpart != nullptr && fnp > 0))));
   const bool vec = S % 4 == 0 && h_nstride % 4 == 0 && dh_nstride % 4 == 0;
   dim3 grid((S + 1023) / 1024, N);
-  const size_t lds = 4 * (C + 1) * sizeof(double);
-  if (vec) hipLaunchKernelGGL((outconv_bwd_kernel<T, true>), grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S);
-  else hipLaunchKernelGGL((outconv_bwd_kernel<T, false>), grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S);
+  size_t lds = 4 * (C + 1) * sizeof(double);
+  if (fpart != nullptr && lds < 3 * 64 * sizeof(double)) lds = 3 * 64 * sizeof(double);
+  if (vec) hipLaunchKernelGGL((outconv_bwd_kernel<T, true>), grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S, fpart, fnp);
+  else hipLaunchKernelGGL((outconv_bwd_kernel<T, false>), grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S, fpart, fnp);
   L3U_CHECK_LAUNCH();
 }
 
@@ -636,6 +658,13 @@ L3U_TWIN(l3u_outconv_fwd, P_OCF, outconv_fwd_impl(bp(h), h_nstride, w, b, p, t, 
     hipStream_t stream)
 L3U_TWIN(l3u_outconv_bwd, P_OCB, outconv_bwd_impl(dp, p, t, sums, alpha, beta, gamma, smooth, gscale,
          bp(h), h_nstride, w, dh, dh_nstride, part, loss, N, C, S, stream))
+#define P_OCBF(TT) (const float* p, const float* t, const float* ftl_part, int ftl_nparts,           \
+    double alpha, double beta, double gamma, double smooth, const float* gscale, const TT* h,         \
+    long long h_nstride, const float* w, float* dh, long long dh_nstride, double* part, float* loss,  \
+    int N, int C, int S, hipStream_t stream)
+L3U_TWIN(l3u_outconv_bwd_ftl, P_OCBF, outconv_bwd_impl((const float*)nullptr, p, t, (const double*)nullptr,
+         alpha, beta, gamma, smooth, gscale, bp(h), h_nstride, w, dh, dh_nstride, part, loss, N, C, S,
+         stream, ftl_part, ftl_nparts))
 #define P_FRF(TT) (const float* x, long long x_nstride, const float* w_dw, const float* w1,          \
     const float* wr, TT* z1, TT* y1, TT* r, float* stat1, float* statr, TT* x_copy, int N, int C,    \
     int D, int H, int W, hipStream_t stream)

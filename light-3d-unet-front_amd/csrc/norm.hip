@@ -36,6 +36,14 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
     int shortcut, T* __restrict__ out, long long ons, int C, int S) {
   __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
+  const T* rp = r + (long long)n * rns + (long long)c * S;
+  T* op = out + (long long)n * ons + (long long)c * S;
+  // the first tile is requested before the records are finalized (their partial-sum loads
+  // overlap it); every later tile one iteration ahead
+  const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4, istep = gridDim.x * 1024;
+  f4 yv = {0.f, 0.f, 0.f, 0.f}, rv = yv;
+  if (VEC && i0 < S) { yv = ldv4(yp + i0); rv = ldv4(rp + i0); }
   float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f;
   if (HAS_SRC) {
     block_record2(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh);
@@ -51,16 +59,16 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
       br = recr[(long long)nc * kRec + 3];
     }
   }
-  const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
-  const T* rp = r + (long long)n * rns + (long long)c * S;
-  T* op = out + (long long)n * ons + (long long)c * S;
   if (VEC) {
-    for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += gridDim.x * 1024) {
-      const f4 yv = ldv4(yp + i), rv = ldv4(rp + i);
+    for (int i = i0; i < S; i += istep) {
+      f4 yn = {0.f, 0.f, 0.f, 0.f}, rn = yn;
+      if (i + istep < S) { yn = ldv4(yp + i + istep); rn = ldv4(rp + i + istep); }
       f4 o;
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = lrelu(fmaf(a2, yv[q] - m2, b2) + fmaf(ar, rv[q] - mr, br));
       stv4(op + i, o);
+      yv = yn;
+      rv = rn;
     }
   } else {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256)
@@ -81,6 +89,32 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
     long long pns, unsigned char* __restrict__ idx, int C, int D, int H, int W) {
   __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const long long S = (long long)D * H * W;
+  const int Ho = H / 2, W4 = W / 4;
+  const long long So = (long long)(D / 2) * Ho * (W / 2), Sp = So / 2;
+  const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
+  const T* rp = r + (long long)n * rns + (long long)c * S;
+  T* op = out + (long long)n * ons + (long long)c * S;
+  T* pp = pooled + (long long)n * pns + (long long)c * So;
+  unsigned short* ip = reinterpret_cast<unsigned short*>(idx + (long long)nc * So);
+  auto base_of = [&](long long o) {
+    const int q = (int)(o % W4), t = (int)(o / W4), oy = t % Ho, oz = t / Ho;
+    return ((long long)(2 * oz) * H + 2 * oy) * W + 4 * q;
+  };
+  // the thread's first 2x2x4 block is requested before the records are finalized (the partial-
+  // sum loads overlap it); every later block one iteration ahead
+  const long long o0 = blockIdx.x * 256ll + threadIdx.x, ostep = (long long)gridDim.x * 256;
+  f4 yv[4], rv[4];
+  auto fetch = [&](long long o) {
+    const long long base = base_of(o < Sp ? o : 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long off = base + ((long long)(j >> 1) * H + (j & 1)) * W;
+      yv[j] = ldv4(yp + off);
+      rv[j] = ldv4(rp + off);
+    }
+  };
+  if (o0 < Sp) fetch(o0);
   float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f;
   if (HAS_SRC) {
     block_record2(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh);
@@ -96,24 +130,17 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
       br = recr[(long long)nc * kRec + 3];
     }
   }
-  const long long S = (long long)D * H * W;
-  const int Ho = H / 2, W4 = W / 4;
-  const long long So = (long long)(D / 2) * Ho * (W / 2), Sp = So / 2;
-  const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
-  const T* rp = r + (long long)n * rns + (long long)c * S;
-  T* op = out + (long long)n * ons + (long long)c * S;
-  T* pp = pooled + (long long)n * pns + (long long)c * So;
-  unsigned short* ip = reinterpret_cast<unsigned short*>(idx + (long long)nc * So);
-  for (long long o = blockIdx.x * 256ll + threadIdx.x; o < Sp; o += (long long)gridDim.x * 256) {
-    const int q = (int)(o % W4), t = (int)(o / W4), oy = t % Ho, oz = t / Ho;
-    const long long base = ((long long)(2 * oz) * H + 2 * oy) * W + 4 * q;
+  for (long long o = o0; o < Sp; o += ostep) {
+    const long long base = base_of(o);
     f4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = lrelu(fmaf(a2, yv[j][e] - m2, b2) + fmaf(ar, rv[j][e] - mr, br));
+    if (o + ostep < Sp) fetch(o + ostep);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const long long off = base + ((long long)(j >> 1) * H + (j & 1)) * W;
-      const f4 yv = ldv4(yp + off), rv = ldv4(rp + off);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[j][e] = lrelu(fmaf(a2, yv[e] - m2, b2) + fmaf(ar, rv[e] - mr, br));
       stv4(op + off, v[j]);
       // the pooled maxima are taken over the values as stored (bf16: rounded), so that the
       // pooled tensor equals MaxPool3d of `out`

@@ -48,6 +48,7 @@ _SIGS = {
     "l3u_outconv_nblocks": [I],
     "l3u_outconv_fwd": [P, L, P, P, P, P, P, I, I, I, P],
     "l3u_outconv_bwd": [P, P, P, P, D, D, D, D, P, P, L, P, P, L, P, P, I, I, I, P],
+    "l3u_outconv_bwd_ftl": [P, P, P, I, D, D, D, D, P, P, L, P, P, L, P, P, I, I, I, P],
     "l3u_ftl_nblocks": [L],
     "l3u_ftl_sums": [P, P, L, P, P, P],
     "l3u_ftl_reduce": [P, I, P, P],
@@ -78,6 +79,7 @@ BF16_TWINS = ("l3u_dw3_fwd", "l3u_dw3_bwd", "l3u_pw_fwd", "l3u_pw_fwd2", "l3u_pw
               "l3u_convt_bwd_fused", "l3u_norm_act_fwd", "l3u_norm_act_pool_fwd",
               "l3u_norm_act_bwd_reduce", "l3u_norm_act_bwd_apply", "l3u_norm_act_bwd",
               "l3u_in_bwd_apply", "l3u_maxpool2_fwd", "l3u_outconv_fwd", "l3u_outconv_bwd",
+              "l3u_outconv_bwd_ftl",
               "l3u_front_fwd")
 for _n in BF16_TWINS:
     _SIGS[_n + "_bf16"] = _SIGS[_n]

@@ -542,8 +542,10 @@ class UNetEngine:
     def backward(self, flat, gflat, sv, dp, need_dx=False, ftl=None):
         """Given dL/dp write all parameter gradients into gflat (overwrite) and return dL/dx if
         need_dx.  dp = None: the loss is FocalTversky and ftl = (target, global sums [3] fp64,
-        (alpha, beta, gamma, smooth)[, loss tensor]); its gradient is formed inside the out_conv
-        backward, which also writes the loss value when a loss tensor is given."""
+        (alpha, beta, gamma, smooth)[, loss tensor[, partials, n_partials]]); its gradient is
+        formed inside the out_conv backward, which also writes the loss value when a loss tensor
+        is given.  sums = None: the out_conv backward reduces the forward's FocalTversky
+        partials itself (l3u_outconv_bwd_ftl; no reduce launch)."""
         N = sv["N"]
         D, H, W = sv["dims"][0]
         self.set_act_dtype(sv["adt"])
@@ -588,14 +590,24 @@ class UNetEngine:
         loss_ptr = None
         if dp is not None:
             g = (dp.data_ptr(), None, None, 0.0, 0.0, 0.0, 0.0, None)
+            self._call("l3u_outconv_bwd", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
+                       self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po),
+                       loss_ptr, N, c0, S[0], st)
         else:   # FocalTversky gradient formed inside the kernel from the global sums
             t, sums, (alpha, beta, gamma, smooth) = ftl[:3]
-            g = (None, t.data_ptr(), sums.data_ptr(), alpha, beta, gamma, smooth, None)
             if len(ftl) > 3 and ftl[3] is not None:   # the loss value, written by the same launch
                 loss_ptr = ftl[3].data_ptr()
-        self._call("l3u_outconv_bwd", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
-                   self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po),
-                   loss_ptr, N, c0, S[0], st)
+            if sums is None:   # the sums reduced inside the launch from the forward's partials
+                fpart, fnp = ftl[4], ftl[5]
+                self._call("l3u_outconv_bwd_ftl", sv["p"].data_ptr(), t.data_ptr(), fpart.data_ptr(),
+                           fnp, alpha, beta, gamma, smooth, None, h.p, h.ns,
+                           self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po),
+                           loss_ptr, N, c0, S[0], st)
+            else:
+                self._call("l3u_outconv_bwd", None, sv["p"].data_ptr(), t.data_ptr(), sums.data_ptr(),
+                           alpha, beta, gamma, smooth, None, h.p, h.ns,
+                           self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po),
+                           loss_ptr, N, c0, S[0], st)
         self._seg(po // 2, N * nb, c0 + 1, 1, c0, "out_conv.weight", f64=1)
         self._seg(po // 2 + c0, N * nb, c0 + 1, 1, 1, "out_conv.bias", f64=1)
         dcat3, dcat2, dcat1 = e(N, 2 * c0, S[0]), e(N, 2 * c1, S[1]), e(N, 2 * c2, S[2])

@@ -62,6 +62,9 @@ class TrainStep:
                                     counter=self.model._rng_counter, bump_counter=False,
                                     save=True, target=t,
                                     ftl_part=part)
+        if self.world == 1:
+            # one process: the out_conv backward reduces the partials itself (no reduce launch)
+            return p, sv, (part, nparts)
         sums = torch.empty(3, dtype=torch.float64, device=p.device)
         nat.call("l3u_ftl_reduce", part.data_ptr(), nparts, sums.data_ptr(), nat.stream())
         return p, sv, sums
@@ -69,9 +72,12 @@ class TrainStep:
     def _bwd(self, p, sv, t, sums):
         # dL/dp is formed inside the out_conv backward from t and the (global) sums; the same
         # launch writes the loss value (losses.py:52-54)
-        self.engine.backward(self.flat, self.gflat, sv, None, need_dx=False,
-                             ftl=(t, sums, (self.alpha, self.beta, self.gamma, self.smooth),
-                                  self.loss))
+        abgs = (self.alpha, self.beta, self.gamma, self.smooth)
+        if isinstance(sums, tuple):   # (partials, count): reduced inside the out_conv backward
+            ftl = (t, None, abgs, self.loss, sums[0], sums[1])
+        else:
+            ftl = (t, sums, abgs, self.loss)
+        self.engine.backward(self.flat, self.gflat, sv, None, need_dx=False, ftl=ftl)
 
     def _grad_exchange(self):
         if self.world > 1:

@@ -685,6 +685,15 @@ def test_outconv_ftl_fused(cuda, case):
     ps = part.view(N * nb, C + 1).double().sum(0).cpu()
     close(ps[:C], wr.grad[0], 1e-4, "dw")
     close(ps[C:], br.grad, 1e-4, "db")
+    # the folded form: the backward reduces the forward's partials itself, bit-identically
+    part3 = torch.empty_like(part)
+    dh3 = torch.empty_like(dh)
+    loss3 = torch.full((), float("nan"), device=cuda)
+    nat().call("l3u_outconv_bwd_ftl", pd.data_ptr(), td.data_ptr(), fpart.data_ptr(), N * nb, 0.7,
+               0.3, 0.75, 1e-6, None, hd.data_ptr(), C * S, wd.data_ptr(), dh3.data_ptr(), C * S,
+               part3.data_ptr(), loss3.data_ptr(), N, C, S, st())
+    torch.cuda.synchronize()
+    assert torch.equal(loss3, lossd) and torch.equal(dh3, dh) and torch.equal(part3, part)
 
 
 # (N, Ci, Co, D, H, W): the network's three up-blocks (low-res volumes) plus ragged ones

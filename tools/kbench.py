@@ -14,7 +14,7 @@ import torch  # noqa: E402
 
 from light_unet import _native as nat  # noqa: E402
 
-SHAPES = [(4, 32, 48), (4, 16, 48), (4, 64, 24), (4, 32, 24), (4, 128, 12), (4, 64, 12)]
+SHAPES = [(4, 32, 48), (4, 16, 48), (4, 64, 24), (4, 32, 24), (4, 16, 24), (4, 128, 12), (4, 64, 12)]
 
 
 def timeit(fn, iters):
