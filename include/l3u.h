@@ -242,6 +242,15 @@ int l3u_outconv_bwd_ftl(const float* p, const float* t, const float* ftl_part, i
                         float* dh, long long dh_nstride, double* part, float* loss, int N, int C,
                         int S, hipStream_t stream);
 
+/* ---- UpBlock pad / crop (light_unet/models/unet3d.py:130-138) -----------------------------
+ * dst[n][c][z][y][x] = src[n][c][z-oz][y-oy][x-ox] inside src's (sd, sh, sw) box, 0 elsewhere,
+ * over the whole (dd, dh, dw) dst box.  Forward: the ConvTranspose3d output padded to the skip
+ * volume (F.pad with diff//2 before, the rest after), written straight into the concat buffer;
+ * backward (offsets negated): the concat gradient cropped to the ConvTranspose3d output. */
+int l3u_box_copy(const float* src, long long src_nstride, int sd, int sh, int sw, float* dst,
+                 long long dst_nstride, int dd, int dh, int dw, int oz, int oy, int ox, int N, int C,
+                 hipStream_t stream);
+
 /* ---- FocalTverskyLoss (light_unet/models/losses.py:11-54) ----------------------------------
  * sums = {sum p*t, sum p, sum t} over ALL voxels of the batch (pred.view(-1), losses.py:40-46),
  * reduced in double; loss = (1 - TI)^gamma; bwd writes dL/dp (* gscale[0] if given) or, with
@@ -361,6 +370,9 @@ int l3u_outconv_bwd_ftl_bf16(const float* p, const float* t, const float* ftl_pa
                              const float* gscale, const l3u_bf16* h, long long h_nstride,
                              const float* w, float* dh, long long dh_nstride, double* part,
                              float* loss, int N, int C, int S, hipStream_t stream);
+int l3u_box_copy_bf16(const l3u_bf16* src, long long src_nstride, int sd, int sh, int sw,
+                      l3u_bf16* dst, long long dst_nstride, int dd, int dh, int dw, int oz, int oy,
+                      int ox, int N, int C, hipStream_t stream);
 int l3u_front_fwd_bf16(const float* x, long long x_nstride, const float* w_dw, const float* w1,
                        const float* wr, l3u_bf16* z1, l3u_bf16* y1, l3u_bf16* r, float* stat1,
                        float* statr, l3u_bf16* x_copy, int N, int C, int D, int H, int W,

@@ -547,6 +547,32 @@ __global__ __launch_bounds__(256) void front_fwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------- pad / crop (UpBlock)
+// dst[n][c][z][y][x] = src[n][c][z - oz][y - oy][x - ox] where that lies inside src's box, else 0:
+// F.pad of the ConvTranspose3d output to the skip volume (oz, oy, ox >= 0, unet3d.py:130-138) and,
+// with the offsets negated, its backward (the crop of the concat gradient).  One thread per dst
+// voxel, x fastest: the stores are contiguous rows, the loads contiguous runs of src rows.
+template <typename T>
+__global__ __launch_bounds__(256) void box_copy_kernel(
+    const T* __restrict__ src, long long sns, int sd, int sh, int sw, T* __restrict__ dst,
+    long long dns, int dd, int dh, int dw, int oz, int oy, int ox, int C, long long total) {
+  const long long dS = (long long)dd * dh * dw, sS = (long long)sd * sh * sw;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int x = (int)(i % dw);
+    long long t = i / dw;
+    const int y = (int)(t % dh);
+    t /= dh;
+    const int z = (int)(t % dd);
+    t /= dd;
+    const int c = (int)(t % C), n = (int)(t / C);
+    const int zs = z - oz, ys = y - oy, xs = x - ox;
+    float v = 0.f;
+    if (zs >= 0 && zs < sd && ys >= 0 && ys < sh && xs >= 0 && xs < sw)
+      v = ld1(src + n * sns + c * sS + ((long long)zs * sh + ys) * sw + xs);
+    st1(dst + n * dns + c * dS + ((long long)z * dh + y) * dw + x, v);
+  }
+}
+
 // ---------------------------------------------------------------- storage casts
 template <typename S_, typename D_>
 __global__ __launch_bounds__(256) void cast_kernel(const S_* __restrict__ x, D_* __restrict__ y,
@@ -665,6 +691,20 @@ L3U_TWIN(l3u_outconv_bwd, P_OCB, outconv_bwd_impl(dp, p, t, sums, alpha, beta, g
 L3U_TWIN(l3u_outconv_bwd_ftl, P_OCBF, outconv_bwd_impl((const float*)nullptr, p, t, (const double*)nullptr,
          alpha, beta, gamma, smooth, gscale, bp(h), h_nstride, w, dh, dh_nstride, part, loss, N, C, S,
          stream, ftl_part, ftl_nparts))
+template <typename T>
+int box_copy_impl(const T* src, long long sns, int sd, int sh, int sw, T* dst, long long dns, int dd,
+                  int dh, int dw, int oz, int oy, int ox, int N, int C, hipStream_t stream) {
+  L3U_REQUIRE(src && dst && N > 0 && C > 0 && sd > 0 && sh > 0 && sw > 0 && dd > 0 && dh > 0 && dw > 0);
+  const long long total = (long long)N * C * dd * dh * dw;
+  hipLaunchKernelGGL((box_copy_kernel<T>), dim3(grid_for(total, 256, 8192)), dim3(256), 0, stream, src,
+                     sns, sd, sh, sw, dst, dns, dd, dh, dw, oz, oy, ox, C, total);
+  L3U_CHECK_LAUNCH();
+}
+#define P_BOX(TT) (const TT* src, long long src_nstride, int sd, int sh, int sw, TT* dst,            \
+    long long dst_nstride, int dd, int dh, int dw, int oz, int oy, int ox, int N, int C,             \
+    hipStream_t stream)
+L3U_TWIN(l3u_box_copy, P_BOX, box_copy_impl(bp(src), src_nstride, sd, sh, sw, bp(dst), dst_nstride, dd,
+         dh, dw, oz, oy, ox, N, C, stream))
 #define P_FRF(TT) (const float* x, long long x_nstride, const float* w_dw, const float* w1,          \
     const float* wr, TT* z1, TT* y1, TT* r, float* stat1, float* statr, TT* x_copy, int N, int C,    \
     int D, int H, int W, hipStream_t stream)

@@ -70,6 +70,7 @@ _SIGS = {
     "l3u_gconv3_bwd_weight": [P, L, P, L, P, P, I, I, I, I, I, I, I, P],
     "l3u_counter_add": [P, I, P],
     "l3u_cast_f32_bf16": [P, P, L, P],
+    "l3u_box_copy": [P, L, I, I, I, P, L, I, I, I, I, I, I, I, I, P],
     "l3u_cast_bf16_f32": [P, P, L, P],
 }
 # entry points with a _bf16 twin (same arguments; saved activations stored as bf16, gradients
@@ -79,7 +80,7 @@ BF16_TWINS = ("l3u_dw3_fwd", "l3u_dw3_bwd", "l3u_pw_fwd", "l3u_pw_fwd2", "l3u_pw
               "l3u_convt_bwd_fused", "l3u_norm_act_fwd", "l3u_norm_act_pool_fwd",
               "l3u_norm_act_bwd_reduce", "l3u_norm_act_bwd_apply", "l3u_norm_act_bwd",
               "l3u_in_bwd_apply", "l3u_maxpool2_fwd", "l3u_outconv_fwd", "l3u_outconv_bwd",
-              "l3u_outconv_bwd_ftl",
+              "l3u_outconv_bwd_ftl", "l3u_box_copy",
               "l3u_front_fwd")
 for _n in BF16_TWINS:
     _SIGS[_n + "_bf16"] = _SIGS[_n]

@@ -250,12 +250,26 @@ class UNetEngine:
         if x.dim() != 5 or x.shape[1] != 1:
             raise ValueError(f"expected input [N, 1, D, H, W], got {tuple(x.shape)}")
         _, _, D, H, W = x.shape
-        if D % 8 or H % 8 or W % 8:
-            raise NotImplementedError(
-                "D, H, W must be divisible by 8 on the MI355X path (the reference's pad branch, "
-                f"unet3d.py:130-138, only fires otherwise); got {(D, H, W)}")
-        if H * W > 4096:
-            raise NotImplementedError(f"H*W <= 4096 required by the stencil kernel, got {H * W}")
+        if min(D, H, W) < 8:
+            # three MaxPool3d(2) halvings must leave >= 1 voxel (the reference fails there too)
+            raise ValueError(f"D, H, W must be >= 8 (three 2x poolings), got {(D, H, W)}")
+        for k in range(4):
+            h, w = H >> k, W >> k
+            # the stencil kernels: x-quad tiles for W % 4 == 0 (W <= 256, any H), whole-plane
+            # tiles otherwise (H * W <= 4096)
+            if not ((w % 4 == 0 and w <= 256) or h * w <= 4096):
+                raise NotImplementedError(
+                    f"level-{k} plane {h}x{w}: the stencil kernels need W % 4 == 0 (W <= 256) or "
+                    "H * W <= 4096")
+
+    @staticmethod
+    def up_pad(lo, hi):
+        """UpBlock's F.pad offsets (unet3d.py:130-138): the ConvTranspose3d output 2*lo padded to
+        the skip volume hi, diff // 2 before each axis; None when the sizes already match."""
+        diff = [h - 2 * l for l, h in zip(lo, hi)]
+        if not any(diff):
+            return None
+        return tuple(d // 2 for d in diff)
 
     # ------------------------------------------------------------------ forward
     def forward(self, flat, x, training=False, dropout_p=0.0, counter=None, save=True, target=None,
@@ -341,9 +355,18 @@ class UNetEngine:
                                                 ("up3.", cat3, c0, 0))):
             d, h, w = dims[lvl + 1]
             ci = prev.C
-            self._call("l3u_convt_fwd", prev.p, prev.ns, self._w(flat, up + "up.weight"),
-                       self._w(flat, up + "up.bias"), cat.data_ptr(), 2 * co * S[lvl], N, ci, co,
-                       d, h, w, st)
+            pad = self.up_pad(dims[lvl + 1], dims[lvl])
+            if pad is None:   # the scatter epilogue writes the concat buffer's lower half
+                self._call("l3u_convt_fwd", prev.p, prev.ns, self._w(flat, up + "up.weight"),
+                           self._w(flat, up + "up.bias"), cat.data_ptr(), 2 * co * S[lvl], N, ci,
+                           co, d, h, w, st)
+            else:             # ragged volume: ConvTranspose3d output, then F.pad into the concat
+                upt = e(N, co, 8 * S[lvl + 1])
+                self._call("l3u_convt_fwd", prev.p, prev.ns, self._w(flat, up + "up.weight"),
+                           self._w(flat, up + "up.bias"), upt.data_ptr(), co * 8 * S[lvl + 1], N,
+                           ci, co, d, h, w, st)
+                self._call("l3u_box_copy", upt.data_ptr(), co * 8 * S[lvl + 1], 2 * d, 2 * h, 2 * w,
+                           cat.data_ptr(), 2 * co * S[lvl], *dims[lvl], *pad, N, co, st)
             out = e(N, co, S[lvl])
             cat_v = V(cat, 0, 2 * co * S[lvl], 2 * co)
             blk[up + "res_block."] = self._block_fwd(flat, up + "res_block.", 5 + k, cat_v,
@@ -624,11 +647,19 @@ class UNetEngine:
             ci = prev.C
             d, hh, w = dims[lvl + 1]
             dprev = e(N, ci, S[lvl + 1])
-            # dY read in place from the lower half of the concat gradient
+            # dY read in place from the lower half of the concat gradient (ragged volume: cropped
+            # to the ConvTranspose3d output first, the backward of F.pad)
+            dY, dYns = dcat.data_ptr(), 2 * co * S[lvl]
+            pad = self.up_pad(dims[lvl + 1], dims[lvl])
+            if pad is not None:
+                dup = self._f32(N, co, 8 * S[lvl + 1], device=dev)
+                self._call32("l3u_box_copy", dY, dYns, *dims[lvl], dup.data_ptr(), co * 8 * S[lvl + 1],
+                             2 * d, 2 * hh, 2 * w, *[-o for o in pad], N, co, st)
+                dY, dYns = dup.data_ptr(), co * 8 * S[lvl + 1]
             npf = nat.query("l3u_convt_bwd_fused_nparts", N, ci, co, d, hh, w)
             if npf > 0:   # one launch: data, weight and bias gradients
                 pw, pb = A.alloc(npf * ci * co * 8), A.alloc(npf * co)
-                self._call("l3u_convt_bwd_fused", dcat.data_ptr(), 2 * co * S[lvl], prev.p, prev.ns,
+                self._call("l3u_convt_bwd_fused", dY, dYns, prev.p, prev.ns,
                            self._w(flat, up + "up.weight"), dprev.data_ptr(), ci * S[lvl + 1],
                            A.ptr(pw), A.ptr(pb), N, ci, co, d, hh, w, st)
                 self._seg(pw, npf, ci * co * 8, 1, ci * co * 8, up + "up.weight")
@@ -636,7 +667,7 @@ class UNetEngine:
             else:
                 npw = nat.query("l3u_pw_bwd_weight_nparts", N, S[lvl + 1])
                 pw, pb = A.alloc(npw * ci * co * 8), A.alloc(npw * co)
-                self._call("l3u_convt_bwd", dcat.data_ptr(), 2 * co * S[lvl], prev.p, prev.ns,
+                self._call("l3u_convt_bwd", dY, dYns, prev.p, prev.ns,
                            self._w(flat, up + "up.weight"), dprev.data_ptr(), ci * S[lvl + 1],
                            A.ptr(pw), A.ptr(pb), N, ci, co, d, hh, w, st)
                 self._seg(pw, npw, ci * co * 8, 1, ci * co * 8, up + "up.weight")

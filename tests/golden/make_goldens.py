@@ -243,15 +243,29 @@ def variant_goldens():
                  use_depthwise_separable=False, use_grouped=False, groups=8)
 
 
+def ragged_goldens():
+    """Volumes the MI355X path once refused: D/H/W not divisible by 8 (the UpBlock pad branch,
+    unet3d.py:130-138, fires at every decoder level) and planes above 64x64 (80x80)."""
+    model_golden("model_b1_40_44_36.npz", (16, 32, 64, 128), (1, 1, 40, 44, 36), seed=47)
+    model_golden("model_b1_24_80_80.npz", (16, 32, 64, 128), (1, 1, 24, 80, 80), seed=48)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     if sys.argv[1:] == ["variants"]:
         variant_goldens()
+        sys.exit(0)
+    if sys.argv[1:] == ["ragged"]:
+        ragged_goldens()
+        sys.exit(0)
+    if sys.argv[1:] == ["c32"]:
+        model_golden("model_c32_b1_64.npz", (32, 64, 128, 256), (1, 1, 64, 64, 64), seed=44)
         sys.exit(0)
     variant_goldens()
     block_goldens()
     ftl_goldens()
     model_golden("model_b2_32.npz", (16, 32, 64, 128), (2, 1, 32, 32, 32), seed=42)
     model_golden("model_b1_48.npz", (16, 32, 64, 128), (1, 1, 48, 48, 48), seed=43)
-    model_golden("model_c32_b1_64.npz", (32, 64, 128, 256), (1, 1, 64, 64, 64), seed=44, full=False)
+    model_golden("model_c32_b1_64.npz", (32, 64, 128, 256), (1, 1, 64, 64, 64), seed=44)
+    ragged_goldens()
     sliding_goldens()

@@ -81,14 +81,23 @@ def test_loss_factory_and_errors():
         f(torch.rand(1, 1, 4, 4, 8)[..., ::2], torch.rand(1, 1, 4, 4, 4))  # non-contiguous (view)
 
 
-def test_engine_rejects_bad_shapes():
+def test_engine_shapes_and_up_pad():
     from light_unet.engine import UNetEngine
-    with pytest.raises(NotImplementedError):
-        UNetEngine.check_shape(torch.zeros(1, 1, 44, 48, 48))
+    # ragged volumes (the UpBlock pad branch) and planes above 64x64 are accepted
+    UNetEngine.check_shape(torch.zeros(1, 1, 44, 48, 48))
+    UNetEngine.check_shape(torch.zeros(1, 1, 40, 44, 36))
+    UNetEngine.check_shape(torch.zeros(1, 1, 8, 72, 72))
+    UNetEngine.check_shape(torch.zeros(1, 1, 24, 80, 80))
     with pytest.raises(ValueError):
         UNetEngine.check_shape(torch.zeros(1, 2, 48, 48, 48))
-    with pytest.raises(NotImplementedError):
-        UNetEngine.check_shape(torch.zeros(1, 1, 8, 72, 72))
+    with pytest.raises(ValueError):       # three 2x poolings of 6 leave nothing
+        UNetEngine.check_shape(torch.zeros(1, 1, 6, 48, 48))
+    with pytest.raises(NotImplementedError):   # W % 4 != 0 with a plane above 4096 voxels
+        UNetEngine.check_shape(torch.zeros(1, 1, 8, 100, 102))
+    # F.pad offsets of unet3d.py:130-138: diff // 2 before
+    assert UNetEngine.up_pad((5, 6, 6), (11, 12, 12)) == (0, 0, 0)
+    assert UNetEngine.up_pad((5, 6, 6), (10, 12, 12)) is None
+    assert UNetEngine.up_pad((4, 5, 2), (9, 11, 4)) == (0, 0, 0)
 
 
 def test_sliding_window_host_pieces(golden):

@@ -53,11 +53,21 @@ def _cpu_fp32_errs(sd, z):
     return _grad_errs({k: p.grad.numpy() for k, p in params.items()}, z)
 
 
-@pytest.mark.parametrize("fname", ["model_b2_32.npz", "model_b1_48.npz"])
-def test_model_matches_reference_golden(cuda, golden, fname):
+# (fixture, encoder channels): bs 2 at 32^3, bs 1 at 48^3, the config-5 network (32 -> 256,
+# 812,284 parameters) at 64^3, a ragged volume (40 x 44 x 36: the UpBlock pad branch,
+# unet3d.py:130-138, at every decoder level; odd pooled sizes 11, 5, 9, 4) and large planes (80 x 80)
+GOLDEN_MODELS = [("model_b2_32.npz", (16, 32, 64, 128)), ("model_b1_48.npz", (16, 32, 64, 128)),
+                 ("model_c32_b1_64.npz", (32, 64, 128, 256)),
+                 ("model_b1_40_44_36.npz", (16, 32, 64, 128)),
+                 ("model_b1_24_80_80.npz", (16, 32, 64, 128))]
+
+
+@pytest.mark.parametrize("fname,enc", GOLDEN_MODELS)
+def test_model_matches_reference_golden(cuda, golden, fname, enc):
     from light_unet.models.losses import get_loss_function
     z = golden(fname)
-    model, sd = _model(z, (16, 32, 64, 128), cuda)
+    model, sd = _model(z, enc, cuda)
+    assert model.count_parameters()["total"] == int(z["n_params"])
     model.train()
     x = torch.from_numpy(z["x"]).to(cuda)
     t = torch.from_numpy(z["target"]).to(cuda)
@@ -78,28 +88,6 @@ def test_model_matches_reference_golden(cuda, golden, fname):
     assert not bad, f"gradient errors above tolerance: {bad}"
     print(f"{fname}: out err {np.abs(o - z['out']).max():.2e}, grad L2 err {gerr:.2e} "
           f"(cpu fp32 {g32:.2e}), worst tensor {max(errs.items(), key=lambda kv: kv[1])}")
-
-
-def test_model_c32_64_golden(cuda, golden):
-    """Config 5 architecture (32->256, 812,284 params) at 64^3: sampled outputs + grad norms."""
-    from light_unet.models.losses import FocalTverskyLoss
-    z = golden("model_c32_b1_64.npz")
-    model, _ = _model(z, (32, 64, 128, 256), cuda)
-    assert model.count_parameters()["total"] == int(z["n_params"]) == 812284
-    x = torch.from_numpy(z["x"]).to(cuda)
-    t = torch.from_numpy(z["target"]).to(cuda)
-    out = model(x)
-    loss = FocalTverskyLoss()(out, t)
-    loss.backward()
-    o = out.detach().cpu().numpy().reshape(-1)
-    assert np.abs(o[z["out_idx"]] - z["out_sample"]).max() <= 1e-3
-    assert abs(o.astype(np.float64).sum() - float(z["out_sum"])) <= 1e-5 * float(z["out_sum"])
-    assert abs(loss.item() - float(z["loss"])) <= 1e-4
-    gscale = max(float(z["gnorm/" + k]) for k, _ in model.named_parameters())
-    for k, p in model.named_parameters():
-        gn = float(np.linalg.norm(p.grad.detach().cpu().numpy().ravel()))
-        ref = float(z["gnorm/" + k])
-        assert abs(gn - ref) <= 1e-2 * ref + 1e-4 * gscale, (k, gn, ref)
 
 
 def test_dropout_masks_match_oracle(cuda, golden):

@@ -942,3 +942,25 @@ def test_pw_fwd2_equals_two_pw_fwd(cuda, shape):
     torch.cuda.synchronize()
     for a, b in ((ya, ya2), (sa, sa2), (yb, yb2), (sb, sb2)):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_box_copy_pad_and_crop(cuda, dt):
+    """l3u_box_copy: F.pad of the ConvTranspose3d output to the skip volume (unet3d.py:130-138,
+    diff // 2 before each axis) into a channel range of a concat buffer, and the crop back (the
+    pad's backward), bit-exact vs torch (a copy)."""
+    sfx = "_bf16" if dt == torch.bfloat16 else ""
+    N, C, (d, h, w), (D, H, W) = 2, 3, (10, 8, 6), (11, 9, 7)
+    src = torch.randn(N, C, d, h, w, device=cuda).to(dt)
+    cat = torch.full((N, 2 * C, D, H, W), 7.0, device=cuda).to(dt)
+    oz, oy, ox = (D - d) // 2, (H - h) // 2, (W - w) // 2
+    nat().call("l3u_box_copy" + sfx, src.data_ptr(), C * d * h * w, d, h, w, cat.data_ptr(),
+               2 * C * D * H * W, D, H, W, oz, oy, ox, N, C, st())
+    ref = F.pad(src, [ox, W - w - ox, oy, H - h - oy, oz, D - d - oz])
+    back = torch.empty_like(src)
+    nat().call("l3u_box_copy" + sfx, cat.data_ptr(), 2 * C * D * H * W, D, H, W, back.data_ptr(),
+               C * d * h * w, d, h, w, -oz, -oy, -ox, N, C, st())
+    torch.cuda.synchronize()
+    assert torch.equal(cat[:, :C], ref)
+    assert torch.all(cat[:, C:] == 7.0)
+    assert torch.equal(back, src)

@@ -16,8 +16,10 @@ def _sd(z, prefix="w/", dtype=torch.float64):
     return {k[len(prefix):]: torch.from_numpy(z[k]).to(dtype) for k in z.files if k.startswith(prefix)}
 
 
-@pytest.mark.parametrize("fname", ["model_b2_32.npz"])
+@pytest.mark.parametrize("fname", ["model_b2_32.npz", "model_b1_40_44_36.npz"])
 def test_oracle_model_fp64_matches_reference(golden, fname):
+    """model_b1_40_44_36: D, H, W not divisible by 8, so every UpBlock takes the pad branch
+    (unet3d.py:130-138)."""
     z = golden(fname)
     sd = _sd(z)
     assert [k for k in sd] == [n for n, _ in U.param_names()]
