@@ -242,6 +242,26 @@ int l3u_outconv_bwd_ftl(const float* p, const float* t, const float* ftl_part, i
                         float* dh, long long dh_nstride, double* part, float* loss, int N, int C,
                         int S, hipStream_t stream);
 
+/* ---- Lesion post-processing (light_unet/models/metrics.py:38-63,107-213;
+ *      light_unet/core/inferencer.py:62-111) -------------------------------------------------
+ * l3u_ccl_label: connected components of (src >= threshold) over the 6 face neighbours
+ * (scipy.ndimage.label's default structure in 3 dims), numbered 1..n in the order of each
+ * component's first voxel in a C-order scan (scipy's numbering); background 0.  Workspace:
+ * parent[D*H*W] int32, chunk_count[l3u_ccl_nchunks(D*H*W) + 1] int32; the component count
+ * lands in chunk_count[l3u_ccl_nchunks(D*H*W)].  label[D*H*W] int32.
+ * l3u_ccl_stats: per component l (1-based) 12 uint64: size, sum z, sum y, sum x, min z, y, x,
+ * max z, y, x, max prob as float bits (prob optional, >= 0), 0; remap (optional, int32 indexed by
+ * the old label) renumbers the labels in place first (0 drops the voxel: the min_size filter).
+ * l3u_ccl_pairs: inter[a * (nb + 1) + b] += voxels labelled a in label_a and b in label_b (both
+ * > 0); inter zeroed by the caller. */
+int l3u_ccl_nchunks(long long n);
+int l3u_ccl_label(const float* src, float threshold, int* parent, int* label, int* chunk_count,
+                  int D, int H, int W, hipStream_t stream);
+int l3u_ccl_stats(int* label, const int* remap, const float* prob, unsigned long long* stats,
+                  int ncomp, int D, int H, int W, hipStream_t stream);
+int l3u_ccl_pairs(const int* label_a, const int* label_b, int nb, unsigned int* inter, long long n,
+                  hipStream_t stream);
+
 /* ---- UpBlock pad / crop (light_unet/models/unet3d.py:130-138) -----------------------------
  * dst[n][c][z][y][x] = src[n][c][z-oz][y-oy][x-ox] inside src's (sd, sh, sw) box, 0 elsewhere,
  * over the whole (dd, dh, dw) dst box.  Forward: the ConvTranspose3d output padded to the skip

@@ -48,10 +48,48 @@ def load():
     importlib.import_module(ALIAS + ".models.losses")
     importlib.import_module(ALIAS + ".utils")
     importlib.import_module(ALIAS + ".fast_trainer")
+    importlib.import_module(ALIAS + ".lesion")
     return mod
 
 
-def install(fast_step=False):
+LESION = ("get_connected_components", "match_components", "calculate_lesion_metrics",
+          "calculate_metrics")
+
+
+def _bind_lesion(done):
+    """The device lesion post-processing (light_unet/lesion.py) into the reference's metrics
+    module (metrics.py:38-404) and into the modules that imported those names already
+    (core.trainer: calculate_metrics; core.inferencer: get_connected_components), plus
+    Inferencer.extract_bboxes (inferencer.py:62-111).  Skipped where the reference module cannot
+    be imported (e.g. its scipy / sklearn / nibabel dependencies are missing)."""
+    les = sys.modules[ALIAS + ".lesion"]
+    try:
+        metrics = importlib.import_module("light_unet.models.metrics")
+    except ImportError:
+        return
+    names = [n for n in LESION if hasattr(metrics, n)]
+    for n in names:
+        setattr(metrics, n, getattr(les, n))
+    done["light_unet.models.metrics"] = names
+    for modname in ("light_unet.models", "light_unet.core.trainer", "light_unet.core.inferencer"):
+        mod = sys.modules.get(modname)
+        if mod is None:
+            continue
+        hit = [n for n in LESION if n in vars(mod)]
+        for n in hit:
+            setattr(mod, n, getattr(les, n))
+        if hit:
+            done.setdefault(modname, []).extend(hit)
+    inf = sys.modules.get("light_unet.core.inferencer")
+    if inf is not None and hasattr(inf, "Inferencer"):
+        def extract_bboxes(self, prob_map, threshold=0.3, min_volume_cc=0.5, spacing=(4.0, 4.0, 4.0)):
+            return les.extract_bboxes(prob_map, threshold, min_volume_cc, spacing,
+                                      self.config["data"]["bbox_expansion_voxels"])
+        inf.Inferencer.extract_bboxes = extract_bboxes
+        done.setdefault("light_unet.core.inferencer", []).append("Inferencer.extract_bboxes")
+
+
+def install(fast_step=False, lesion=True):
     """Bind this build's model and loss into the already-importable reference package.
     Returns {module: [names]} of what was replaced.  Raises ImportError when the reference's
     light_unet.models.{unet3d,losses} cannot be imported (nothing is half-installed).
@@ -59,7 +97,11 @@ def install(fast_step=False):
     fast_step=True also replaces Trainer.train_epoch / Trainer._train_epoch_step_based
     (trainer.py:208-347) with the graph-replayed TrainStep loops of light_unet/fast_trainer.py
     (same batches, update, TensorBoard scalars and return values; no per-step host sync; RCCL
-    data parallelism when torch.distributed is initialised).  Needs light_unet.core.trainer."""
+    data parallelism when torch.distributed is initialised).  Needs light_unet.core.trainer.
+
+    lesion=True (default) also binds the device lesion post-processing (connected components,
+    matching, lesion / voxel metrics, bounding boxes: light_unet/lesion.py) where the reference's
+    metrics module imports."""
     amd = load()
     trainer_mod = importlib.import_module("light_unet.core.trainer") if fast_step else None
     src = {
@@ -83,5 +125,7 @@ def install(fast_step=False):
         fast = importlib.import_module(ALIAS + ".fast_trainer")
         fast.bind(trainer_mod.Trainer)
         done["light_unet.core.trainer"] = ["Trainer.train_epoch", "Trainer._train_epoch_step_based"]
+    if lesion:
+        _bind_lesion(done)
     amd.installed_into = done
     return done

@@ -71,6 +71,10 @@ _SIGS = {
     "l3u_counter_add": [P, I, P],
     "l3u_cast_f32_bf16": [P, P, L, P],
     "l3u_box_copy": [P, L, I, I, I, P, L, I, I, I, I, I, I, I, I, P],
+    "l3u_ccl_nchunks": [L],
+    "l3u_ccl_label": [P, F, P, P, P, I, I, I, P],
+    "l3u_ccl_stats": [P, P, P, P, I, I, I, I, P],
+    "l3u_ccl_pairs": [P, P, I, P, L, P],
     "l3u_cast_bf16_f32": [P, P, L, P],
 }
 # entry points with a _bf16 twin (same arguments; saved activations stored as bf16, gradients
@@ -88,7 +92,8 @@ for _n in BF16_TWINS:
 _QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_weight_nparts",
             "l3u_pw_bwd_supported", "l3u_pw_bwd_nparts", "l3u_convt_bwd_fused_nparts",
             "l3u_norm_act_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks",
-            "l3u_gconv3_nblocks", "l3u_gconv3_wgrad_nparts", "l3u_front_nblocks"}
+            "l3u_gconv3_nblocks", "l3u_gconv3_wgrad_nparts", "l3u_front_nblocks",
+            "l3u_ccl_nchunks"}
 
 _lib = None
 

@@ -243,6 +243,100 @@ def variant_goldens():
                  use_depthwise_separable=False, use_grouped=False, groups=8)
 
 
+def _blobs(rng, shape, n, rmax, centers=None):
+    """A smooth synthetic probability map: n Gaussian blobs on a low background (at `centers`
+    when given, else uniform)."""
+    zz, yy, xx = np.meshgrid(*[np.arange(s) for s in shape], indexing="ij")
+    p = rng.random(shape) * 0.05
+    for i in range(n):
+        c = centers[i] if centers is not None else [rng.uniform(0, s) for s in shape]
+        r = rng.uniform(1.0, rmax)
+        amp = rng.uniform(0.3, 1.0)
+        p = np.maximum(p, amp * np.exp(-((zz - c[0]) ** 2 + (yy - c[1]) ** 2 + (xx - c[2]) ** 2) / (2 * r * r)))
+    return p.astype(np.float32)
+
+
+def lesion_goldens():
+    """Lesion post-processing from the REFERENCE light_unet/models/metrics.py:
+    get_connected_components (ndimage.label; min_size filter), match_components,
+    calculate_lesion_metrics, calculate_metrics.  The bounding boxes of inferencer.py:62-111 are
+    restated here on the reference's own labels (that module imports nibabel, absent here)."""
+    metrics = _load("ref_metrics", "light_unet/models/metrics.py")
+    rng = np.random.default_rng(49)
+    rec = {}
+    masks = {
+        "rand30": rng.random((20, 24, 28)) < 0.30,
+        "rand50": rng.random((17, 19, 23)) < 0.50,            # near percolation: long snakes
+        "sparse": rng.random((16, 16, 16)) < 0.05,
+        "empty": np.zeros((8, 9, 10), bool),
+        "full": np.ones((8, 9, 10), bool),
+        "single": np.zeros((9, 9, 9), bool),
+        "checker": (np.indices((10, 12, 14)).sum(0) % 2) == 0,  # no face neighbours at all
+    }
+    masks["single"][4, 5, 6] = True
+    for name, m in masks.items():
+        lab, num = metrics.get_connected_components(m.astype(np.int32))
+        rec[f"cc/{name}/mask"] = m
+        rec[f"cc/{name}/labels"] = lab.astype(np.int32)
+        rec[f"cc/{name}/num"] = np.array(num)
+        lab5, num5 = metrics.get_connected_components(m.astype(np.int32), min_size=5)
+        rec[f"cc/{name}/labels_min5"] = lab5.astype(np.int32)
+        rec[f"cc/{name}/num_min5"] = np.array(num5)
+    # lesion matching / metrics on synthetic probability maps and targets
+    cases = []
+    for i, (shape, npred, ntgt) in enumerate([((32, 36, 40), 9, 7), ((24, 28, 20), 4, 0),
+                                              ((28, 28, 28), 0, 5), ((30, 26, 34), 12, 10)]):
+        # targets at random centres; predictions hit most of them (jittered 0-3 voxels, so both
+        # IoU and centre-distance matches occur) plus false positives elsewhere
+        tc = [[rng.uniform(0, s) for s in shape] for _ in range(ntgt)]
+        hit = [[c + rng.uniform(-3, 3) for c in cc] for cc in tc[: max(0, ntgt - 2)]]
+        pc = (hit + [[rng.uniform(0, s) for s in shape] for _ in range(npred)])[:npred]
+        pred = _blobs(rng, shape, len(pc), 3.5, pc) if npred else (rng.random(shape) * 0.05).astype(np.float32)
+        tgt = (_blobs(rng, shape, ntgt, 3.0, tc) >= 0.5).astype(np.float32) if ntgt else np.zeros(shape, np.float32)
+        cases.append((pred, tgt))
+        rec[f"lm/{i}/pred"] = pred
+        rec[f"lm/{i}/target"] = tgt
+        for thr in (0.3, 0.5):
+            m = metrics.calculate_lesion_metrics(pred, tgt, threshold=thr, spacing=(4.0, 4.0, 4.0))
+            for k, v in m.items():
+                rec[f"lm/{i}/thr{thr}/{k}"] = np.array(v)
+        m2 = metrics.calculate_lesion_metrics(pred, tgt, threshold=0.3, min_size_voxels=6,
+                                              iou_threshold=0.2, distance_threshold_mm=6.0,
+                                              spacing=(2.0, 3.0, 4.0))
+        for k, v in m2.items():
+            rec[f"lm/{i}/opts/{k}"] = np.array(v)
+        pl, _ = metrics.get_connected_components((pred >= 0.3).astype(np.int32))
+        tl, _ = metrics.get_connected_components((tgt >= 0.5).astype(np.int32))
+        mt, up, ut = metrics.match_components(pl, tl, 0.1, 10.0, (4.0, 4.0, 4.0))
+        rec[f"lm/{i}/matches"] = np.array(mt, dtype=np.int64).reshape(-1, 2)
+        rec[f"lm/{i}/unmatched_pred"] = np.array(up, dtype=np.int64)
+        rec[f"lm/{i}/unmatched_target"] = np.array(ut, dtype=np.int64)
+    agg = metrics.calculate_metrics([c[0] for c in cases], [c[1] for c in cases], threshold=0.3,
+                                    spacing=[(4.0, 4.0, 4.0), (2.0, 2.0, 2.0), (4.0, 4.0, 4.0), (3.0, 4.0, 5.0)])
+    for k, v in agg.items():
+        rec[f"agg/{k}"] = np.array(v)
+    # bounding boxes (inferencer.py:62-111 restated on the reference's labels)
+    prob = _blobs(rng, (40, 44, 36), 10, 4.0)
+    spacing, expand = (4.0, 4.0, 4.0), 2
+    vcc = spacing[0] * spacing[1] * spacing[2] / 1000.0
+    minv = int(np.ceil(0.5 / vcc))
+    lab, num = metrics.get_connected_components((prob >= 0.3).astype(np.int32), min_size=minv)
+    boxes = []
+    for cid in range(1, num + 1):
+        cm = lab == cid
+        co = np.argwhere(cm)
+        lo, hi = co.min(0), co.max(0)
+        lo = np.maximum(0, lo - expand)
+        hi = np.minimum(np.array(prob.shape) - 1, hi + expand)
+        boxes.append([cid, lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]])
+        rec[f"bb/{cid}/volume_cc"] = np.array(cm.sum() * vcc)
+        rec[f"bb/{cid}/confidence"] = np.array(prob[cm].max())
+    rec["bb/prob"] = prob
+    rec["bb/boxes"] = np.array(boxes, dtype=np.int64).reshape(-1, 7)
+    np.savez_compressed(os.path.join(OUT, "lesion.npz"), **rec)
+    print("lesion.npz", len(rec), "arrays")
+
+
 def ragged_goldens():
     """Volumes the MI355X path once refused: D/H/W not divisible by 8 (the UpBlock pad branch,
     unet3d.py:130-138, fires at every decoder level) and planes above 64x64 (80x80)."""
@@ -254,6 +348,9 @@ if __name__ == "__main__":
     torch.set_num_threads(8)
     if sys.argv[1:] == ["variants"]:
         variant_goldens()
+        sys.exit(0)
+    if sys.argv[1:] == ["lesion"]:
+        lesion_goldens()
         sys.exit(0)
     if sys.argv[1:] == ["ragged"]:
         ragged_goldens()
@@ -268,4 +365,5 @@ if __name__ == "__main__":
     model_golden("model_b1_48.npz", (16, 32, 64, 128), (1, 1, 48, 48, 48), seed=43)
     model_golden("model_c32_b1_64.npz", (32, 64, 128, 256), (1, 1, 64, 64, 64), seed=44)
     ragged_goldens()
+    lesion_goldens()
     sliding_goldens()

@@ -1,0 +1,103 @@
+"""Device lesion post-processing (light_unet/lesion.py -> csrc/lesion.hip, l3u_ccl_*) against the
+reference's own outputs (tests/golden/lesion.npz, made by running light_unet/models/metrics.py)
+and against the pinned oracle (oracle/lesion_oracle.py) at larger sizes.  Integer work: labels,
+counts, matches and boxes bit-exact; the float metrics equal (same host arithmetic)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import lesion_oracle as L
+
+pytestmark = pytest.mark.gpu
+
+CC = ["rand30", "rand50", "sparse", "empty", "full", "single", "checker"]
+
+
+@pytest.mark.parametrize("name", CC)
+def test_labels_match_reference(cuda, golden, name):
+    from light_unet import lesion
+    z = golden("lesion.npz")
+    lab, n = lesion.get_connected_components(z[f"cc/{name}/mask"].astype(np.int32))
+    assert n == int(z[f"cc/{name}/num"]) and lab.dtype == np.int32
+    assert np.array_equal(lab, z[f"cc/{name}/labels"])
+    lab5, n5 = lesion.get_connected_components(z[f"cc/{name}/mask"], min_size=5)
+    assert n5 == int(z[f"cc/{name}/num_min5"])
+    assert np.array_equal(lab5, z[f"cc/{name}/labels_min5"])
+
+
+@pytest.mark.parametrize("i", range(4))
+def test_matching_and_metrics_match_reference(cuda, golden, i):
+    from light_unet import lesion
+    z = golden("lesion.npz")
+    pred, tgt = z[f"lm/{i}/pred"], z[f"lm/{i}/target"]
+    for thr in (0.3, 0.5):
+        m = lesion.calculate_lesion_metrics(pred, tgt, threshold=thr)
+        for k, v in m.items():
+            assert v == z[f"lm/{i}/thr{thr}/{k}"].item(), (thr, k)
+    m = lesion.calculate_lesion_metrics(pred[None, None], tgt[None, None], threshold=0.3,
+                                        min_size_voxels=6, iou_threshold=0.2,
+                                        distance_threshold_mm=6.0, spacing=(2.0, 3.0, 4.0))
+    for k, v in m.items():
+        assert v == z[f"lm/{i}/opts/{k}"].item(), k
+    pl, _ = lesion.get_connected_components(pred >= 0.3)
+    tl, _ = lesion.get_connected_components(tgt >= 0.5)
+    mt, up, ut = lesion.match_components(pl, tl)
+    assert np.array_equal(np.array(mt, np.int64).reshape(-1, 2), z[f"lm/{i}/matches"])
+    assert list(up) == z[f"lm/{i}/unmatched_pred"].tolist()
+    assert list(ut) == z[f"lm/{i}/unmatched_target"].tolist()
+
+
+def test_calculate_metrics_matches_reference(cuda, golden):
+    from light_unet import lesion
+    z = golden("lesion.npz")
+    preds = [z[f"lm/{i}/pred"] for i in range(4)]
+    tgts = [z[f"lm/{i}/target"] for i in range(4)]
+    agg = lesion.calculate_metrics(preds, tgts, threshold=0.3,
+                                   spacing=[(4.0, 4.0, 4.0), (2.0, 2.0, 2.0), (4.0, 4.0, 4.0), (3.0, 4.0, 5.0)])
+    for k, v in agg.items():
+        assert v == z[f"agg/{k}"].item(), k
+
+
+def test_bboxes_match_reference(cuda, golden):
+    from light_unet import lesion
+    z = golden("lesion.npz")
+    bb = lesion.extract_bboxes(z["bb/prob"], 0.3, 0.5, (4.0, 4.0, 4.0), expansion_voxels=2)
+    ref = z["bb/boxes"]
+    assert len(bb) == ref.shape[0] > 0
+    for b, r in zip(bb, ref):
+        assert [b["mask_id"]] + b["bbox_voxel"] == r.tolist()
+        assert b["bbox_mm"] == [float(v * 4.0) for v in r[1:]]
+        assert b["volume_cc"] == z[f"bb/{r[0]}/volume_cc"].item()
+        assert b["confidence"] == z[f"bb/{r[0]}/confidence"].item()
+
+
+@pytest.mark.parametrize("density", [0.1, 0.2, 0.3116, 0.5])
+def test_labels_match_oracle_64(cuda, density):
+    """64^3 random masks, incl. 3-D site percolation (p ~= 0.3116: components spanning the volume
+    through long chains, the worst case for the union-find's contention)."""
+    from light_unet import lesion
+    m = np.random.default_rng(int(density * 1e4)).random((64, 64, 64)) < density
+    lab, n = lesion.get_connected_components(m)
+    ref, nr = L.get_connected_components(m)
+    assert n == nr and np.array_equal(lab, ref)
+    lab2, _ = lesion.get_connected_components(m)
+    assert np.array_equal(lab, lab2)      # deterministic
+
+
+def test_bboxes_match_oracle_ragged(cuda):
+    from light_unet import lesion
+    rng = np.random.default_rng(3)
+    shape = (70, 90, 52)
+    zz, yy, xx = np.meshgrid(*[np.arange(s) for s in shape], indexing="ij")
+    p = (rng.random(shape) * 0.05).astype(np.float32)
+    for _ in range(30):
+        c = [rng.uniform(0, s) for s in shape]
+        r = rng.uniform(1.0, 5.0)
+        p = np.maximum(p, rng.uniform(0.3, 1.0) * np.exp(
+            -((zz - c[0]) ** 2 + (yy - c[1]) ** 2 + (xx - c[2]) ** 2) / (2 * r * r))).astype(np.float32)
+    got = lesion.extract_bboxes(torch.from_numpy(p).cuda(), 0.3, 0.5, (2.0, 2.0, 3.0), expansion_voxels=3)
+    ref = L.bboxes(p, 0.3, 0.5, (2.0, 2.0, 3.0), expansion_voxels=3)
+    assert len(got) == len(ref) > 5
+    for g, r in zip(got, ref):
+        for k in ("mask_id", "bbox_voxel", "volume_cc", "confidence"):
+            assert g[k] == r[k], k

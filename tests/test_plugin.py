@@ -18,6 +18,11 @@ def _standin(tmp_path):
     (base / "models" / "__init__.py").write_text(
         "from .unet3d import Lightweight3DUNet\nfrom .losses import FocalTverskyLoss, get_loss_function\n")
     (base / "models" / "unet3d.py").write_text("class Lightweight3DUNet:\n    origin = 'reference'\n")
+    (base / "models" / "metrics.py").write_text(
+        "def get_connected_components(mask, min_size=0):\n    return 'reference'\n"
+        "def match_components(*a, **k):\n    return 'reference'\n"
+        "def calculate_lesion_metrics(*a, **k):\n    return 'reference'\n"
+        "def calculate_metrics(*a, **k):\n    return 'reference'\n")
     (base / "models" / "losses.py").write_text(
         "class FocalTverskyLoss:\n    origin = 'reference'\n\n"
         "def get_loss_function(cfg):\n    return FocalTverskyLoss()\n")
@@ -26,7 +31,8 @@ def _standin(tmp_path):
     (base / "core" / "trainer.py").write_text(
         "from light_unet.models.unet3d import Lightweight3DUNet\n"
         "from light_unet.models.losses import get_loss_function\n"
-        "from light_unet.utils import sliding_window_inference_3d\n\n"
+        "from light_unet.utils import sliding_window_inference_3d\n"
+        "from light_unet.models.metrics import calculate_metrics\n\n"
         "class Trainer:\n"
         "    def train_epoch(self, epoch):\n        return 'reference'\n"
         "    def _train_epoch_step_based(self, epoch):\n        return 'reference'\n")
@@ -46,6 +52,11 @@ def test_install_binds_model_and_loss(tmp_path):
         assert trainer.get_loss_function.__module__ == "l3u_amd.models.losses"
         assert m.FocalTverskyLoss.__module__ == "l3u_amd.models.losses"
         assert trainer.sliding_window_inference_3d.__module__ == "l3u_amd.utils"
+        import light_unet.models.metrics as met
+        for n in ("get_connected_components", "match_components", "calculate_lesion_metrics",
+                  "calculate_metrics"):
+            assert getattr(met, n).__module__ == "l3u_amd.lesion", n
+        assert trainer.calculate_metrics.__module__ == "l3u_amd.lesion"
         assert sys.modules["light_unet"].__file__.startswith({str(tmp_path)!r})
         net = trainer.Lightweight3DUNet()
         assert net.count_parameters()["total"] == 217228
