@@ -242,6 +242,38 @@ int l3u_outconv_bwd_ftl(const float* p, const float* t, const float* ftl_part, i
                         float* dh, long long dh_nstride, double* part, float* loss, int N, int C,
                         int S, hipStream_t stream);
 
+/* ---- Training patches (light_unet/datasets/patch_dataset.py:114-220) -----------------------
+ * One record per patch: the case volume it is cut from (device pointers, [sd][sh][sw] fp32), the
+ * crop start (max(0, center - patch // 2), zero padded past the volume end), and the augmentation
+ * the host drew with the reference's RNG calls: flip axis (-1 none), rotation plane (rot_a0 < rot_a1,
+ * -1 none) with scipy.ndimage.rotate's matrix entries and offsets, zoom (zoomed shape zs, the
+ * out -> in factor zf = (in - 1) / (out - 1), the centre-crop start zst of the fit back to the
+ * patch), intensity shift, gaussian noise on / off (the float64 noise values come in `noise`,
+ * [B][pz][py][px], drawn by the host). */
+typedef struct l3u_aug_param {
+  const float* image;
+  const float* label;
+  int z0, y0, x0;
+  int sd, sh, sw;
+  int pz, py, px;
+  int flip;
+  int rot_a0, rot_a1;
+  double rot_c, rot_s, rot_off0, rot_off1;
+  int zoom;
+  int zs[3];
+  int zst[3];
+  double zf[3];
+  int shift_on;
+  float shift;
+  int noise_on;
+} l3u_aug_param;
+
+/* out_img / out_lab [B][pz][py][px] fp32 (the DataLoader batch, [B, 1, pz, py, px]); tmp_* the
+ * same size (the rotated patches the zoom interpolates from). */
+int l3u_aug_patches(const l3u_aug_param* params, int B, int pz, int py, int px, const double* noise,
+                    float* tmp_img, float* tmp_lab, float* out_img, float* out_lab,
+                    hipStream_t stream);
+
 /* ---- Lesion post-processing (light_unet/models/metrics.py:38-63,107-213;
  *      light_unet/core/inferencer.py:62-111) -------------------------------------------------
  * l3u_ccl_label: connected components of (src >= threshold) over the 6 face neighbours

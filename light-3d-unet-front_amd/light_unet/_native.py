@@ -72,6 +72,7 @@ _SIGS = {
     "l3u_cast_f32_bf16": [P, P, L, P],
     "l3u_box_copy": [P, L, I, I, I, P, L, I, I, I, I, I, I, I, I, P],
     "l3u_ccl_nchunks": [L],
+    "l3u_aug_patches": [P, I, I, I, I, P, P, P, P, P, P],
     "l3u_ccl_label": [P, F, P, P, P, I, I, I, P],
     "l3u_ccl_stats": [P, P, P, P, I, I, I, I, P],
     "l3u_ccl_pairs": [P, P, I, P, L, P],
@@ -107,6 +108,15 @@ class NormSrc(ctypes.Structure):
     record from.  Pass `norm_src_ptr(s)`; keep the object alive across the call."""
     _fields_ = [("stat_part", P), ("nsb", I), ("layer", I), ("gamma", P), ("beta", P),
                 ("drop_p", F), ("seed", U64), ("step", P), ("rec_out", P)]
+
+
+class AugParam(ctypes.Structure):
+    """struct l3u_aug_param (include/l3u.h): one training patch's crop and augmentation."""
+    _fields_ = [("image", P), ("label", P), ("z0", I), ("y0", I), ("x0", I), ("sd", I), ("sh", I),
+                ("sw", I), ("pz", I), ("py", I), ("px", I), ("flip", I), ("rot_a0", I),
+                ("rot_a1", I), ("rot_c", D), ("rot_s", D), ("rot_off0", D), ("rot_off1", D),
+                ("zoom", I), ("zs", I * 3), ("zst", I * 3), ("zf", D * 3), ("shift_on", I),
+                ("shift", F), ("noise_on", I)]
 
 
 def norm_src_ptr(s):
