@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-bf16", action="store_true", help="skip the bf16 (config 3) step timing")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in autograd step timing")
+    ap.add_argument("--no-data", action="store_true",
+                    help="skip the data-path timings (lesion post-processing, training patches)")
     ap.add_argument("--ftl-mode", default="exact", choices=["exact", "local"])
     ap.add_argument("--no-sliding", action="store_true", help="skip the config-4 inference timing")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (32->256, 64^3) timing")
@@ -421,6 +423,91 @@ def sliding_bench(model, device, size=256):
             "note": "includes the host->device upload and the prob-map copy back"}
 
 
+def lesion_bench(device, size=256, reps=5):
+    """SURVEY §8f rank 4, post-processing: on the config-4 synthetic PET volume (256^3, 20 hot
+    spheres) used as the probability map, Inferencer.extract_bboxes (threshold 0.3, 0.5 cc at 4 mm,
+    inferencer.py:62-111) and calculate_lesion_metrics against the spheres (threshold 0.5,
+    metrics.py:216-287) on the device (light_unet.lesion, the map already in HBM), beside the
+    reference's host path for the same calls (scipy.ndimage.label + the numpy matching, timed on
+    this host: the reference's own dependency, not the oracle)."""
+    from scipy import ndimage
+    from light_unet import lesion
+    vol = synthetic_pet(size)
+    tgt = (vol >= 0.6).astype(np.float32)
+    pv, tv = torch.from_numpy(vol).to(device), torch.from_numpy(tgt).to(device)
+    lesion.extract_bboxes(pv, 0.3, 0.5, (4.0, 4.0, 4.0), 2)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        boxes = lesion.extract_bboxes(pv, 0.3, 0.5, (4.0, 4.0, 4.0), 2)
+        met = lesion.calculate_lesion_metrics(pv, tv, threshold=0.5)
+    torch.cuda.synchronize()
+    dev_ms = 1000 * (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    lab, n = ndimage.label((vol >= 0.3).astype(np.int32))
+    sizes = np.bincount(lab.ravel())
+    small = sizes < 8
+    small[0] = False
+    lab[small[lab]] = 0
+    lab, n = ndimage.label(lab > 0)
+    objs = ndimage.find_objects(lab)
+    pl, npred = ndimage.label((vol >= 0.5).astype(np.int32))
+    tl, ntgt = ndimage.label(tgt.astype(np.int32))
+    ndimage.center_of_mass(np.ones_like(pl, dtype=np.float32), labels=pl, index=np.arange(1, npred + 1))
+    np.bincount(pl.ravel().astype(np.int64) * (ntgt + 1) + tl.ravel(), minlength=(npred + 1) * (ntgt + 1))
+    host_ms = 1000 * (time.perf_counter() - t0)
+    return {"volume": [size] * 3, "device_ms": round(dev_ms, 3), "components": len(boxes),
+            "lesion_metrics": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in met.items()},
+            "host_scipy_ms": round(host_ms, 1), "host_note": f"scipy.ndimage label x3 + min-size filter + "
+            f"find_objects + centres + pair counts, one pass ({len(objs)} boxes)"}
+
+
+def patches_bench(device, B=4, reps=20):
+    """SURVEY §8f rank 4, training patches: a bs-4 batch of 48^3 patches cut and augmented (the
+    reference config's flip / rotation / scale / shift / noise probabilities) from the 256^3
+    synthetic case resident in HBM (light_unet.patches), beside the reference's per-patch host
+    work for the same draws (numpy crop + scipy rotate / zoom, timed on this host)."""
+    from scipy import ndimage
+    from light_unet.patches import DevicePatchDataset
+    aug = {"gaussian_noise": {"enabled": True, "prob": 0.3, "sigma": 0.01},
+           "intensity_shift": {"enabled": True, "prob": 0.5, "shift_range": [-0.1, 0.1]},
+           "random_flip": {"enabled": True, "prob": 0.5, "axes": [0, 1, 2]},
+           "random_rotation": {"enabled": True, "prob": 0.5, "angle_range": [-15, 15],
+                               "axes": [[0, 1], [0, 2], [1, 2]]},
+           "random_scale": {"enabled": True, "prob": 0.3, "scale_range": [0.9, 1.1]}}
+    vol = synthetic_pet(256)
+    lab = (vol >= 0.6).astype(np.float32)
+    ds = DevicePatchDataset([(vol, lab)], (48, 48, 48), 0.5, aug, seed=42, device=device)
+    ds.sample_batch(B)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    draws = []
+    for _ in range(reps):
+        ds.sample_batch(B)
+        draws.extend(ds.last_draws)
+    torch.cuda.synchronize()
+    dev_ms = 1000 * (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for ci, c, d in draws[:8]:
+        z, y, x = (max(0, v - 24) for v in c)
+        img, lb = vol[z:z + 48, y:y + 48, x:x + 48], lab[z:z + 48, y:y + 48, x:x + 48]
+        pad = [(0, 48 - n) for n in img.shape]
+        img, lb = np.pad(img, pad), np.pad(lb, pad)
+        if d.flip_axis >= 0:
+            img = np.flip(img, d.flip_axis).copy()
+        if d.rot_axes is not None:
+            img = ndimage.rotate(img, d.angle, axes=d.rot_axes, reshape=False, order=1, mode="constant")
+            lb = ndimage.rotate(lb, d.angle, axes=d.rot_axes, reshape=False, order=0, mode="constant")
+        if d.scale is not None:
+            img = ndimage.zoom(img, d.scale, order=1, mode="constant")
+            lb = ndimage.zoom(lb, d.scale, order=0, mode="constant")
+    host_ms = 1000 * (time.perf_counter() - t0) / 8 * B
+    return {"batch": B, "patch": [48, 48, 48], "device_ms_per_batch": round(dev_ms, 3),
+            "host_scipy_ms_per_batch": round(host_ms, 1),
+            "note": "device: host RNG draws + one l3u_aug_patches launch pair; host: crop + scipy "
+                    "rotate / zoom of the same draws, single thread, per batch of the same size"}
+
+
 def config5_bench(device, world, rank, steps=20, warmup=5, bs=4, size=64, enc=(32, 64, 128, 256)):
     """encoder 32->64->128->256 (812,284 parameters), 64^3 patches, bs 4
     per GPU, the reference's step-based mixed-domain epoch (trainer.py:260-347) with
@@ -700,6 +787,8 @@ def main():
     grouped = grouped_bench(device) if (rank == 0 and not args.no_grouped) else None
     bf16 = bf16_bench(device, args, enc, world, rank, pool) if (args.dtype == "fp32" and not args.no_bf16) else None
     dropin = dropin_bench(device) if (rank == 0 and not args.no_dropin) else None
+    lesion_r = lesion_bench(device) if (rank == 0 and not args.no_data) else None
+    patches_r = patches_bench(device) if (rank == 0 and not args.no_data) else None
     fwd1 = fwd_ms_per_patch(model, 1, args.size, device) if rank == 0 else None
     fwd4 = fwd_ms_per_patch(model, args.batch, args.size, device) if rank == 0 else None
     out = None
@@ -736,6 +825,8 @@ def main():
             "grouped_1gpu": grouped,
             "bf16": bf16,
             "dropin": dropin,
+            "lesion_256": lesion_r,
+            "patches": patches_r,
             "launches_per_step": n_launch_calls,
             "roofline": {
                 "kernel": f"l3u_dw3_bwd [{N},{cdom},{args.size}^3] (up3.res_block.conv1.depthwise "
