@@ -96,6 +96,20 @@ int l3u_pw_fwd2(const float* xa, long long xa_nstride, const float* wa, float* y
                 long long ya_nstride, float* stat_a, const float* xb, long long xb_nstride,
                 const float* wb, float* yb, long long yb_nstride, float* stat_b, int N, int K,
                 int Nout, int S, hipStream_t stream);
+/* ---- fused depthwise-separable conv forward (one launch per DepthwiseSeparableConv3d) -------
+ * replaces DepthwiseSeparableConv3d.forward (unet3d.py:20-23: depthwise 3^3 then pointwise 1x1)
+ * and, with w_sc, the ResidualBlock's Conv1x1 shortcut on the same input (unet3d.py:70-73,80):
+ *   Z = dw3(A) (A = x, or lrelu(IN(x))*dropout when rec / src is given: unet3d.py:84-89),
+ *   y = w_pw . Z,  r = w_sc . x,  z (optional, may be NULL) = Z for the backward.
+ * y_stat / r_stat: InstanceNorm (count, mean, M2) partials in the l3u_pw_fwd format with
+ * l3u_dwpw_stat_nsb(...) partials per (n, c).  Supported shapes: l3u_dwpw_supported.          */
+int l3u_dwpw_supported(int K, int Nout, int D, int H, int W, int shortcut);
+int l3u_dwpw_stat_nsb(int K, int Nout, int D, int H, int W);
+int l3u_dwpw_fwd(const float* x, long long x_nstride, const float* w_dw, const float* rec,
+                 const l3u_norm_src* src, const float* w_pw, float* y, long long y_nstride,
+                 float* y_stat, const float* w_sc, float* r, long long r_nstride, float* r_stat,
+                 float* z, long long z_nstride, int N, int K, int Nout, int D, int H, int W,
+                 hipStream_t stream);
 /* weight gradient partials: part[N*nsc][J][K] = sum_s dY[n][j][s] X[n][k][s] per voxel chunk   */
 int l3u_pw_bwd_weight_nparts(int N, int S);
 int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
@@ -462,6 +476,11 @@ int l3u_in_bwd_apply_bf16(const float* dpre, long long dpre_nstride, const l3u_b
 int l3u_pw_fwd_bf16(const l3u_bf16* x, long long x_nstride, const float* w, int w_layout,
                     const float* bias, l3u_bf16* y, long long y_nstride, int accumulate,
                     float* stat_part, int N, int K, int Nout, int S, hipStream_t stream);
+int l3u_dwpw_fwd_bf16(const l3u_bf16* x, long long x_nstride, const float* w_dw, const float* rec,
+                      const l3u_norm_src* src, const float* w_pw, l3u_bf16* y, long long y_nstride,
+                      float* y_stat, const float* w_sc, l3u_bf16* r, long long r_nstride,
+                      float* r_stat, l3u_bf16* z, long long z_nstride, int N, int K, int Nout,
+                      int D, int H, int W, hipStream_t stream);
 int l3u_pw_fwd2_bf16(const l3u_bf16* xa, long long xa_nstride, const float* wa, l3u_bf16* ya,
                      long long ya_nstride, float* stat_a, const l3u_bf16* xb, long long xb_nstride,
                      const float* wb, l3u_bf16* yb, long long yb_nstride, float* stat_b, int N,

@@ -315,6 +315,11 @@ int pick_tz(int D) { return D <= 8 ? D : 4; }
 #define L3U_GW_SCALAR 1
 #endif
 
+// register prefetch depth (planes in flight) of the quad forward stencil
+#ifndef L3U_DWQ_PD
+#define L3U_DWQ_PD 2
+#endif
+
 // TZ = 24 slabs for D % 24 == 0 (two slabs at 48^3): measured variant switch
 #ifndef L3U_TZ24
 #define L3U_TZ24 0
@@ -505,7 +510,7 @@ L3U_DEV void pin(T& v) { asm volatile("" : "+v"(v)); }
 //            + shift (ep = the saved pre-IN activation), plus the fp64 IN-backward sums
 //            in_part[c][n][chunk] = {sum dpre, sum dpre*xhat}
 //   EPI = 2: backward data, y += conv^T(x)      EPI = 3: backward data, y = conv^T(x)
-template <typename T, typename TE, int XF, int EPI, int TZC>
+template <typename T, typename TE, int XF, int EPI, int TZC, int PD = 2>
 __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
     const T* __restrict__ x, long long xns, const float* __restrict__ w,
     const float* __restrict__ rec, l3u_norm_src src, int has_src, T* __restrict__ y,
@@ -530,9 +535,9 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
   // loop is fully unrolled, so the two staged registers never move (no back-edge copies that
   // would force a vmcnt(0) drain of the pipeline).  The first two planes are requested before
   // the InstanceNorm record is finalized (its partial-sum loads then overlap them).
-  QPre<T> p0, p1;
-  q_fetch(p0, xp + zc(b.z0 - 1), qm);
-  q_fetch(p1, xp + zc(b.z0), qm);
+  QPre<T> pf[PD];   // PD planes in flight (register staging depth)
+#pragma unroll
+  for (int i = 0; i < PD; ++i) q_fetch(pf[i], xp + zc(b.z0 - 1 + i), qm);
   float sc = 1.f, sh = 0.f, mu = 0.f, rstd = 1.f, kk = 1.f;
   if (XF || EPI == 1) {
     if (has_src) {
@@ -552,7 +557,7 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
     const int zi = b.z0 - 1 + t;
     float* buf = lds + (t & 1) * PP;
     q_commit<XF == 1>(pre, buf, qm, zi >= zlo && zi <= zhi, sc, mu, sh);
-    q_fetch(pre, xp + zc(zi + 2), qm);
+    q_fetch(pre, xp + zc(zi + PD), qm);
     const int zo = zi - 1;   // output plane zo has all three input planes after this step
     f4 e = {0.f, 0.f, 0.f, 0.f};
     if (EPI == 1 || EPI == 2) e = ldv4(epp + (long long)min(max(zo, 0), D - 1) * HW + qofs);
@@ -594,9 +599,10 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
     a2 = f4{0.f, 0.f, 0.f, 0.f};
   };
 #pragma unroll
-  for (int t = 0; t < TZC + 2; t += 2) {
-    step(t, p0);
-    step(t + 1, p1);
+  for (int t = 0; t < TZC + 2; t += PD) {
+#pragma unroll
+    for (int i = 0; i < PD; ++i)
+      if (t + i < TZC + 2) step(t + i, pf[i]);
   }
   if (EPI == 1) {   // fixed-order block reduction of the IN-backward sums
     __syncthreads();
@@ -1416,7 +1422,7 @@ int dw3_fwd_impl(const T* x, long long x_nstride, const float* w, const float* r
     size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
     if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);   // reduction scratch
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
-#define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<T, T, M_, 0, T_>), grid, block, lds, stream, x, \
+#define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<T, T, M_, 0, T_, L3U_DWQ_PD>), grid, block, lds, stream, x, \
       x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W, g.RB, g.RPW, \
       g.ny, g.TZ, g.nz)
     if (xf) { TZ24(DWQF(1, 24)) if (g.TZ == 16) DWQF(1, 16); else if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }

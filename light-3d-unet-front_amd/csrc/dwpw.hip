@@ -1,0 +1,417 @@
+// Fused depthwise-separable convolution forward: Y = Wpw . dw3(A) in ONE launch, where
+// A = X (conv1) or A = lrelu(IN1(X)) * dropout (conv2, the transform applied on load), with the
+// InstanceNorm statistics partials of Y in the epilogue and, for conv1 of a block with a Conv1x1
+// shortcut, the shortcut GEMM R = Wsc . X from the same staged X planes.
+// Replaces DepthwiseSeparableConv3d.forward (light_unet/models/unet3d.py:20-23: depthwise 3^3,
+// groups = C, then the 1x1 pointwise) and ResidualBlock's shortcut conv (unet3d.py:70-73,80).
+//
+// Why one launch: the depthwise output Z never makes the HBM round trip write -> read between
+// two launches (it is written once, for the backward's pointwise weight gradient, and read from
+// LDS by the GEMM), the GEMM's X stream and the stencil's X stream are one read, and a launch
+// boundary disappears per conv.
+//
+// Mapping (gfx950, 64-wide waves): a workgroup owns one sample n, a slab of TZ output z-planes and
+// a strip of RB rows (all W), for ALL K input channels: wave w runs the depthwise z-march of
+// channel(s) w*CPW .. w*CPW+CPW-1 exactly as dw3q_fwd does (its lanes own x-quads of the strip's
+// rows; x-neighbours by DPP, rolling accumulators over 3 kernel depths, planes staged through
+// registers into a per-channel LDS image).  After each plane step the waves drop their Z quads
+// into a [K][VP] LDS tile, and the GEMM runs on the MFMA from that tile: wave tau owns a
+// (64-voxel group, 16-output-channel block[, Y or R]) tile; lane (lr, lk) feeds the float4
+// Z[4ks+lk][64g + 4lr .. +3] to 4 v_mfma_f32_16x16x4f32 (the l3u_pw_fwd operand mapping, same
+// k order: Y is bit-identical to l3u_dw3_fwd followed by l3u_pw_fwd).
+// InstanceNorm partials: one (count, mean, M2) per (n, output channel, workgroup) from fp64
+// per-lane sums (the l3u_pw_fwd format; l3u_dwpw_stat_nsb partials per (n, c)).
+#include "common.h"
+using namespace l3u;
+
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+L3U_DEV f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+L3U_DEV float lane_prev(float v) {   // value of lane l-1 (DPP wave_shr:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+L3U_DEV float lane_next(float v) {   // value of lane l+1 (DPP wave_shl:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
+}
+
+template <typename T> struct Raw4 { typedef f4 type; };
+template <> struct Raw4<bf16> { typedef b4_t type; };
+L3U_DEV f4 widen(f4 v) { return v; }
+L3U_DEV f4 widen(b4_t v) { return __builtin_convertvector(v, f4); }
+template <typename T>
+L3U_DEV void pin(T& v) { asm volatile("" : "+v"(v)); }
+
+// fp64 sum over the 16 lanes of a DPP row (fixed order: deterministic), in every lane
+L3U_DEV double row_sum16d(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  return v;
+}
+
+// Wave-local staging map of one channel's (RB+2) x WQ quad strip image (<= 128 quads): lane l
+// stages quads l and l + 64; rows outside the volume are never written (stay zero).
+struct WMap {
+  int goff[2], loff[2];
+  bool ok[2];
+};
+
+L3U_DEV WMap w_map(int y0, int rows, int H, int W, int WQ, int l) {
+  WMap m;
+  const int nq = (rows + 2) * WQ;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = l + 64 * k;
+    const int qc = q < nq ? q : 0;
+    const int lr = qc / WQ, xq = (qc - lr * WQ) * 4, yy = y0 - 1 + lr;
+    m.ok[k] = q < nq && yy >= 0 && yy < H;
+    m.goff[k] = min(max(yy, 0), H - 1) * W + xq;
+    m.loff[k] = lr * W + xq;
+  }
+  return m;
+}
+
+template <typename T>
+struct Stage {
+  typename Raw4<T>::type v[2];
+};
+
+template <typename T>
+L3U_DEV void w_fetch(Stage<T>& p, const T* plane, const WMap& m) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) p.v[k] = *reinterpret_cast<const typename Raw4<T>::type*>(plane + m.goff[k]);
+}
+
+template <bool XF, typename T>
+L3U_DEV void w_commit(const Stage<T>& p, float* lplane, const WMap& m, bool in, float sc, float mu,
+                      float sh) {
+  const float keep = in ? 1.f : 0.f;
+  sc *= keep;
+  sh *= keep;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    f4 v = widen(p.v[k]);
+    if (XF) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(sc, v[i] - mu, sh));
+    } else {
+      v *= keep;
+    }
+    if (m.ok[k]) *reinterpret_cast<f4*>(lplane + m.loff[k]) = v;
+  }
+}
+
+// XF: IN-on-load input (conv2); CPW: channels per wave (K = 16 * CPW, 16 waves); NC: output
+// channel blocks of 16 (Nout = 16 * NC); SC: also the Conv1x1 shortcut R = Wsc . X (XF = 0);
+// TZC: output planes per slab.  Grid: N * nz * ny workgroups of 1024 threads.
+template <typename T, int XF, int CPW, int NC, int SC, int TZC>
+__global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
+    const T* __restrict__ x, long long xns, const float* __restrict__ wdw,
+    const float* __restrict__ rec, l3u_norm_src src, int has_src,
+    const float* __restrict__ wpw, T* __restrict__ y, long long yns, float* __restrict__ ystat,
+    const float* __restrict__ wsc, T* __restrict__ r, long long rns, float* __restrict__ rstat,
+    T* __restrict__ z, long long zns, int D, int H, int W, int RB, int ny, int nz) {
+  constexpr int K = 16 * CPW, NB = 2 + SC, NT = 4 * NC * (1 + SC);
+  // register budget (1024 threads: <= 128 VGPRs): two channels per wave stage one plane ahead
+  // and read their taps from LDS; one channel per wave stages two planes ahead, taps in SGPRs
+  constexpr int PD = CPW == 1 ? 2 : 1;
+  constexpr bool LTAP = CPW > 1;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int WQ = W >> 2, PP = (RB + 2) * W, HW = H * W, VP = 256;
+  const long long S = (long long)D * HW;
+  int t0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int yb = t0 % ny; t0 /= ny;
+  const int zb = t0 % nz;
+  const int n = t0 / nz;
+  const int z0 = zb * TZC, z1 = min(z0 + TZC, D), y0 = yb * RB, rows = min(RB, H - y0);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+  const int lr = l / WQ, qx = l - lr * WQ;
+  const bool own = lr < rows;
+  const int oy = own ? lr : 0, ox = 4 * qx;
+  const bool el = qx == 0, er = qx == WQ - 1;
+  float* planes = lds;                          // [K][NB][PP]
+  float* zt = lds + (size_t)K * NB * PP;        // [K][VP]
+  double* sred = reinterpret_cast<double*>(zt + K * VP);   // [NT][16 ch][2]
+  float* taps = reinterpret_cast<float*>(sred + NT * 16 * 2);   // [K][27] (LTAP)
+
+  // ---- per-channel setup: taps, InstanceNorm record, first two planes in flight
+  const T* xn = x + (long long)n * xns;
+  const WMap wm = w_map(y0, rows, H, W, WQ, l);
+  const int zlo = max(0, z0 - 1), zhi = min(D - 1, z1);
+  auto zc = [&](int zz) { return (long long)min(max(zz, zlo), zhi) * HW; };
+  Stage<T> st[CPW][PD];
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) {
+    const T* xc = xn + (long long)(wv * CPW + i) * S;
+#pragma unroll
+    for (int k = 0; k < PD; ++k) w_fetch(st[i][k], xc + zc(z0 - 1 + k), wm);
+  }
+  float sc[CPW], mu[CPW], sh[CPW];
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) {
+    sc[i] = 1.f; mu[i] = 0.f; sh[i] = 0.f;
+    if (XF) {
+      const int c = wv * CPW + i;
+      if (has_src) {
+        float rr[kRec];
+        finalize_record(src, n, c, K, rr);
+        mu[i] = rr[0]; sc[i] = rr[2]; sh[i] = rr[3];
+        if (zb == 0 && yb == 0 && l == 0 && src.rec_out) {
+          float* o = src.rec_out + ((long long)n * K + c) * kRec;
+#pragma unroll
+          for (int k = 0; k < kRec; ++k) o[k] = rr[k];
+        }
+      } else {
+        const float* rp = rec + ((long long)n * K + c) * kRec;
+        mu[i] = rp[0]; sc[i] = rp[2]; sh[i] = rp[3];
+      }
+    }
+  }
+  float wk[LTAP ? 1 : CPW][27];
+  if constexpr (LTAP) {
+    for (int i = threadIdx.x; i < K * 27; i += blockDim.x) taps[i] = wdw[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < CPW; ++i)
+#pragma unroll
+      for (int tp = 0; tp < 27; ++tp) wk[i][tp] = wdw[(wv * CPW + i) * 27 + tp];
+  }
+  for (int i = threadIdx.x; i < K * NB * PP + K * VP; i += blockDim.x) planes[i] = 0.f;   // + zt
+
+  // ---- GEMM role of this wave: tile tau = wv -> (voxel group g, channel block m, Y or R)
+  const bool mm = wv < NT;
+  const int g = wv & 3, m = (wv >> 2) % NC, which = wv / (4 * NC);
+  const int lrm = l & 15, lk = l >> 4;
+  float aw[K / 4];
+  {
+    const float* wsrc = (SC && which == 1) ? wsc : wpw;
+#pragma unroll
+    for (int ks = 0; ks < K / 4; ++ks) aw[ks] = mm ? wsrc[(16 * m + lrm) * K + 4 * ks + lk] : 0.f;
+  }
+  T* outp = (SC && which == 1) ? r + (long long)n * rns : y + (long long)n * yns;
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  const int v0 = 64 * g + 4 * lrm;                // this lane's voxel quad in the strip
+  const int vrow = v0 / W, vx = v0 - vrow * W;
+  const bool vok = vrow < rows;
+  __syncthreads();
+
+  f4 a0[CPW], a1[CPW], a2[CPW];
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) a0[i] = a1[i] = a2[i] = f4{0.f, 0.f, 0.f, 0.f};
+
+  auto step = [&](int t, int slot) {
+    const int zi = z0 - 1 + t, zo = zi - 1;
+    const int bi = t % NB;
+    // (a) commit this step's input plane of each own channel, request the plane PD = 2 ahead
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+      const int c = wv * CPW + i;
+      float* buf = planes + ((size_t)c * NB + bi) * PP;
+      w_commit<XF == 1>(st[i][slot], buf, wm, zi >= zlo && zi <= zhi, sc[i], mu[i], sh[i]);
+      w_fetch(st[i][slot], xn + (long long)c * S + zc(zi + PD), wm);
+    }
+    __syncthreads();   // B1: planes visible; the previous step's GEMM reads of zt are done
+    const bool fin = zo >= z0 && zo < z1;
+    // (b) the stencil of each own channel (dw3q_fwd's tap order), Z quad -> zt (and global)
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) {
+      const int c = wv * CPW + i;
+      const float* buf = planes + ((size_t)c * NB + bi) * PP;
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) {
+        const f4 mq = *reinterpret_cast<const f4*>(buf + (oy + rr) * W + ox);
+        const float lv = lane_prev(mq[3]), rv = lane_next(mq[0]);
+        const float v[6] = {el ? 0.f : lv, mq[0], mq[1], mq[2], mq[3], er ? 0.f : rv};
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const float* tw = LTAP ? taps + c * 27 : nullptr;   // re-read each step (LDS broadcast)
+          const float w0 = LTAP ? tw[rr * 3 + dx] : wk[LTAP ? 0 : i][rr * 3 + dx];
+          const float w1 = LTAP ? tw[9 + rr * 3 + dx] : wk[LTAP ? 0 : i][9 + rr * 3 + dx];
+          const float w2 = LTAP ? tw[18 + rr * 3 + dx] : wk[LTAP ? 0 : i][18 + rr * 3 + dx];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            a2[i][q] = fmaf(w0, v[q + dx], a2[i][q]);
+            a1[i][q] = fmaf(w1, v[q + dx], a1[i][q]);
+            a0[i][q] = fmaf(w2, v[q + dx], a0[i][q]);
+          }
+        }
+      }
+      pin(a1[i]);
+      pin(a2[i]);
+      if (fin) {
+        const f4 o = round_to(a0[i], (const T*)nullptr);   // Z at its storage precision
+        if (lr < RB)
+          *reinterpret_cast<f4*>(zt + c * VP + lr * W + ox) = own ? o : f4{0.f, 0.f, 0.f, 0.f};
+        if (z != nullptr && own)
+          stv4(z + (long long)n * zns + (long long)c * S + (long long)zo * HW + (long long)(y0 + oy) * W + ox, o);
+      }
+      a0[i] = a1[i];
+      a1[i] = a2[i];
+      a2[i] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (!fin) return;   // uniform over the workgroup
+    __syncthreads();   // B2: the Z tile of plane zo is complete
+    // (c) the channel GEMM on the MFMA: Y (or R) tile of 16 channels x 64 voxels
+    if (mm) {
+      const float* bsrc = (SC && which == 1) ? planes + W + (size_t)((t - 1) % NB) * PP + v0
+                                             : zt + v0;
+      const size_t kstr = (SC && which == 1) ? (size_t)NB * PP : (size_t)VP;
+      f4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int ks = 0; ks < K / 4; ++ks) {
+        const f4 b = *reinterpret_cast<const f4*>(bsrc + (size_t)(4 * ks + lk) * kstr);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = mfma4(aw[ks], b[q], acc[q]);
+      }
+      // lane (lrm, lk) holds channels 16m + 4lk + rr of the voxel quad v0 .. v0+3
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int co = 16 * m + 4 * lk + rr;
+        f4 o = f4{acc[0][rr], acc[1][rr], acc[2][rr], acc[3][rr]};
+        T* dst = outp + (long long)co * S + (long long)zo * HW + (long long)(y0 + vrow) * W + vx;
+        if (vok) stv4(dst, o);
+        o = round_to(o, dst);   // statistics of the stored values
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double dv = vok ? (double)o[q] : 0.0;
+          s1[rr] += dv;
+          s2[rr] = fma(dv, dv, s2[rr]);
+        }
+      }
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < TZC + 2; t += PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) step(t + k, k);
+  }
+
+  // ---- statistics partials: lanes of a row -> waves of the same (m, which) in g order
+  if (mm) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const double a = row_sum16d(s1[rr]), b = row_sum16d(s2[rr]);
+      if (lrm == 0) {
+        double* o = sred + ((size_t)wv * 16 + 4 * lk + rr) * 2;
+        o[0] = a;
+        o[1] = b;
+      }
+    }
+  }
+  __syncthreads();
+  const int nch = 16 * NC * (1 + SC);
+  if ((int)threadIdx.x < nch) {
+    const int wh = threadIdx.x / (16 * NC), cc = threadIdx.x % (16 * NC);
+    const int mb = cc >> 4, ci = cc & 15;
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const double* p = sred + ((size_t)((wh * NC + mb) * 4 + gg) * 16 + ci) * 2;
+      a += p[0];
+      b += p[1];
+    }
+    const double cnt = (double)(z1 - z0) * rows * W;
+    const double mean = a / cnt;
+    const double m2 = fmax(b - a * mean, 0.0);
+    float* st3 = (wh == 1 ? rstat : ystat);
+    if (st3 != nullptr) {
+      const int nsb = nz * ny;
+      float* o = st3 + (((long long)n * (16 * NC) + cc) * nsb + zb * ny + yb) * 3;
+      o[0] = (float)cnt;
+      o[1] = (float)mean;
+      o[2] = (float)m2;
+    }
+  }
+}
+
+struct DPGeom {
+  int RB, ny, TZ, nz;
+  bool ok;
+};
+
+// planes + Z tile + statistics scratch (16 tiles) + taps
+size_t dp_lds(int K, int NB, int RB, int W) {
+  return ((size_t)K * NB * (RB + 2) * W + (size_t)K * 256) * sizeof(float) +
+         (size_t)16 * 16 * 2 * sizeof(double) + (size_t)K * 27 * sizeof(float);
+}
+
+#ifndef L3U_DWPW_TZ
+#define L3U_DWPW_TZ 8
+#endif
+
+DPGeom dp_geom(int K, int Nout, int D, int H, int W, int sc) {
+  DPGeom g{};
+  g.ok = false;
+  // K = 32 (two channels per wave) exceeds the 128-VGPR budget of a 1024-thread workgroup
+  // (measured: 74-118 VGPRs spilled), so the fused path takes 16 input channels
+  if (K != 16 || !(Nout == 16 || Nout == 32)) return g;
+  if (W % 4 != 0 || W < 8 || W > 64 || H < 1 || D < 1) return g;
+  const int WQ = W / 4, RPW = 64 / WQ;
+  g.RB = min(RPW, H);
+  if (g.RB * W > 256) return g;                       // the Z tile holds <= 256 voxels
+  if ((g.RB + 2) * WQ > 128) return g;                // <= 2 staged quads per lane
+  if (sc && W + 256 > (g.RB + 2) * W) return g;       // shortcut B reads stay in the plane image
+  g.ny = (H + g.RB - 1) / g.RB;
+  g.TZ = L3U_DWPW_TZ;
+  g.nz = (D + g.TZ - 1) / g.TZ;
+  const int NB = 2 + sc;
+  if (dp_lds(K, NB, g.RB, W) > 160 * 1024) return g;
+  g.ok = true;
+  return g;
+}
+
+template <typename T>
+int dwpw_fwd_impl(const T* x, long long x_nstride, const float* w_dw, const float* rec,
+                  const l3u_norm_src* src, const float* w_pw, T* y, long long y_nstride,
+                  float* y_stat, const float* w_sc, T* r, long long r_nstride, float* r_stat,
+                  T* z, long long z_nstride, int N, int K, int Nout, int D, int H, int W,
+                  hipStream_t stream) {
+  const int sc = w_sc != nullptr ? 1 : 0;
+  const DPGeom g = dp_geom(K, Nout, D, H, W, sc);
+  L3U_REQUIRE(N > 0 && g.ok && x && w_dw && w_pw && y);
+  L3U_REQUIRE(!sc || (r != nullptr && rec == nullptr && src == nullptr));
+  L3U_REQUIRE(x_nstride % 4 == 0 && y_nstride % 4 == 0 && (!sc || r_nstride % 4 == 0) &&
+              (z == nullptr || z_nstride % 4 == 0));
+  const l3u_norm_src zs{};
+  const l3u_norm_src s = src ? *src : zs;
+  const int xf = (rec != nullptr || src != nullptr) ? 1 : 0;
+  const int NB = 2 + sc;
+  const size_t lds = dp_lds(K, NB, g.RB, W);
+  dim3 grid(N * g.nz * g.ny), block(1024);
+#define DPF(XF_, CPW_, NC_, SC_) hipLaunchKernelGGL((dwpw_fwd_kernel<T, XF_, CPW_, NC_, SC_, L3U_DWPW_TZ>), grid, \
+      block, lds, stream, x, x_nstride, w_dw, rec, s, src ? 1 : 0, w_pw, y, y_nstride, y_stat, w_sc, r, \
+      r_nstride, r_stat, z, z_nstride, D, H, W, g.RB, g.ny, g.nz)
+#define DPF_C(CPW_, NC_) do { if (sc) DPF(0, CPW_, NC_, 1); else if (xf) DPF(1, CPW_, NC_, 0); \
+                              else DPF(0, CPW_, NC_, 0); } while (0)
+  if (Nout == 16) DPF_C(1, 1);
+  else DPF_C(1, 2);
+#undef DPF_C
+#undef DPF
+  L3U_CHECK_LAUNCH();
+}
+
+}  // namespace
+
+extern "C" {
+
+int l3u_dwpw_supported(int K, int Nout, int D, int H, int W, int shortcut) {
+  return dp_geom(K, Nout, D, H, W, shortcut ? 1 : 0).ok ? 1 : 0;
+}
+
+int l3u_dwpw_stat_nsb(int K, int Nout, int D, int H, int W) {
+  const DPGeom g = dp_geom(K, Nout, D, H, W, 0);
+  return g.ok ? g.nz * g.ny : 0;
+}
+
+}  // extern "C"
+
+#define P_DPF(TT) (const TT* x, long long x_nstride, const float* w_dw, const float* rec,          \
+    const l3u_norm_src* src, const float* w_pw, TT* y, long long y_nstride, float* y_stat,        \
+    const float* w_sc, TT* r, long long r_nstride, float* r_stat, TT* z, long long z_nstride,      \
+    int N, int K, int Nout, int D, int H, int W, hipStream_t stream)
+L3U_TWIN(l3u_dwpw_fwd, P_DPF, dwpw_fwd_impl(bp(x), x_nstride, w_dw, rec, src, w_pw, bp(y), y_nstride,
+         y_stat, w_sc, bp(r), r_nstride, r_stat, bp(z), z_nstride, N, K, Nout, D, H, W, stream))

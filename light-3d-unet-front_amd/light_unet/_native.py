@@ -77,6 +77,9 @@ _SIGS = {
     "l3u_ccl_stats": [P, P, P, P, I, I, I, I, P],
     "l3u_ccl_pairs": [P, P, I, P, L, P],
     "l3u_cast_bf16_f32": [P, P, L, P],
+    "l3u_dwpw_supported": [I, I, I, I, I, I],
+    "l3u_dwpw_stat_nsb": [I, I, I, I, I],
+    "l3u_dwpw_fwd": [P, L, P, P, P, P, P, L, P, P, P, L, P, P, L, I, I, I, I, I, I, P],
 }
 # entry points with a _bf16 twin (same arguments; saved activations stored as bf16, gradients
 # fp32, include/l3u.h)
@@ -86,7 +89,7 @@ BF16_TWINS = ("l3u_dw3_fwd", "l3u_dw3_bwd", "l3u_pw_fwd", "l3u_pw_fwd2", "l3u_pw
               "l3u_norm_act_bwd_reduce", "l3u_norm_act_bwd_apply", "l3u_norm_act_bwd",
               "l3u_in_bwd_apply", "l3u_maxpool2_fwd", "l3u_outconv_fwd", "l3u_outconv_bwd",
               "l3u_outconv_bwd_ftl", "l3u_box_copy",
-              "l3u_front_fwd")
+              "l3u_front_fwd", "l3u_dwpw_fwd")
 for _n in BF16_TWINS:
     _SIGS[_n + "_bf16"] = _SIGS[_n]
 # query helpers that return a value instead of an error code
@@ -94,7 +97,7 @@ _QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_
             "l3u_pw_bwd_supported", "l3u_pw_bwd_nparts", "l3u_convt_bwd_fused_nparts",
             "l3u_norm_act_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks",
             "l3u_gconv3_nblocks", "l3u_gconv3_wgrad_nparts", "l3u_front_nblocks",
-            "l3u_ccl_nchunks"}
+            "l3u_ccl_nchunks", "l3u_dwpw_supported", "l3u_dwpw_stat_nsb"}
 
 _lib = None
 
@@ -136,7 +139,11 @@ def load():
             "(or __graft_entry__.build()).  The Light-3D-U-Net MI355X path has no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH)
     for name, args in _SIGS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None and os.environ.get("L3U_LIB"):
+            continue   # an older variant build (A/B tools): calls of newer entry points raise
+        if fn is None:
+            raise NativeError(f"{LIB_PATH} does not export {name}: rebuild the library")
         fn.argtypes = args
         fn.restype = I
     _lib = lib

@@ -31,6 +31,11 @@ _PAIR_PW = os.environ.get("L3U_PAIR_PW", "1") != "0"
 # block-tail backward inside the pointwise backwards (l3u_pw_bwd_tail); L3U_TAIL_FUSE=0 disables
 _TAIL_FUSE = os.environ.get("L3U_TAIL_FUSE", "1") != "0"
 _SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32").split(","))
+# conv2 (depthwise + pointwise, InstanceNorm1 on load) as one l3u_dwpw_fwd launch for volumes of
+# at least this many voxels (the 48^3 level; at 24^3 its 1024-thread slabs are too few to fill
+# the chip, tools/dwpw_bench.py); L3U_DWPW=0 disables
+_DWPW = os.environ.get("L3U_DWPW", "1") != "0"
+_DWPW_MIN_S = int(os.environ.get("L3U_DWPW_MIN_S", "65536"))
 
 
 class V:
@@ -481,12 +486,24 @@ class UNetEngine:
                        cout * S, 0, self.fwd_arena.ptr(s1), N, cin, cout, S, st)
             src1 = self._src(flat, pre + "norm1.", s1, nsb, rec1, drop, cptr, 1 + layer)
         z2 = e(N, cout, S)
-        self._call("l3u_dw3_fwd", y1.data_ptr(), cout * S, self._w(flat, pre + "conv2.depthwise.weight"),
-                   None, nat.norm_src_ptr(src1), z2.data_ptr(), cout * S, N, cout, d, h, w, st)
         y2 = e(N, cout, S)
-        s2 = self.fwd_arena.alloc(N * cout * nsb2 * 3)
-        self._call("l3u_pw_fwd", z2.data_ptr(), cout * S, self._w(flat, pre + "conv2.pointwise.weight"),
-                   0, None, y2.data_ptr(), cout * S, 0, self.fwd_arena.ptr(s2), N, cout, cout, S, st)
+        if _DWPW and S >= _DWPW_MIN_S and nat.query("l3u_dwpw_supported", cout, cout, d, h, w, 0):
+            # conv2 = depthwise (IN1 + LeakyReLU + Dropout3d on load) + pointwise in one launch
+            nsb2 = nat.query("l3u_dwpw_stat_nsb", cout, cout, d, h, w)
+            s2 = self.fwd_arena.alloc(N * cout * nsb2 * 3)
+            self._call("l3u_dwpw_fwd", y1.data_ptr(), cout * S,
+                       self._w(flat, pre + "conv2.depthwise.weight"), None, nat.norm_src_ptr(src1),
+                       self._w(flat, pre + "conv2.pointwise.weight"), y2.data_ptr(), cout * S,
+                       self.fwd_arena.ptr(s2), None, None, 0, None, z2.data_ptr(), cout * S, N, cout,
+                       cout, d, h, w, st)
+        else:
+            self._call("l3u_dw3_fwd", y1.data_ptr(), cout * S,
+                       self._w(flat, pre + "conv2.depthwise.weight"), None, nat.norm_src_ptr(src1),
+                       z2.data_ptr(), cout * S, N, cout, d, h, w, st)
+            s2 = self.fwd_arena.alloc(N * cout * nsb2 * 3)
+            self._call("l3u_pw_fwd", z2.data_ptr(), cout * S,
+                       self._w(flat, pre + "conv2.pointwise.weight"), 0, None, y2.data_ptr(), cout * S,
+                       0, self.fwd_arena.ptr(s2), N, cout, cout, S, st)
         src2 = self._src(flat, pre + "norm2.", s2, nsb2, rec2, 0.0, cptr, 0)
         if pool is None:
             self._call("l3u_norm_act_fwd", y2.data_ptr(), cout * S, None, nat.norm_src_ptr(src2),

@@ -14,7 +14,8 @@ import torch  # noqa: E402
 
 from light_unet import _native as nat  # noqa: E402
 
-SHAPES = [(4, 32, 48), (4, 16, 48), (4, 64, 24), (4, 32, 24), (4, 16, 24), (4, 128, 12), (4, 64, 12)]
+SHAPES = [tuple(int(v) for v in t.split(",")) for t in os.environ.get(
+    "KB_SHAPES", "4,32,48 4,16,48 4,64,24 4,32,24 4,16,24 4,128,12 4,64,12").split()]
 
 
 def timeit(fn, iters):
@@ -60,6 +61,23 @@ def main():
                     nat.call("l3u_dw3_bwd", dz.data_ptr(), C * S, x.data_ptr(), C * S, w.data_ptr(),
                              r, dx.data_ptr(), C * S, acc, dwp.data_ptr(),
                              inp.data_ptr() if r else None, N, C, D, H, W, st)
+            elif kind == "fwd1s":
+                # IN-fused forward with the record finalized in-kernel from GEMM partials, as in
+                # the step (nsb partials per (n, c) in the l3u_pw_fwd format)
+                nsb = nat.query("l3u_pw_stat_nsb", C, C, S)
+                part = torch.empty(N, C, nsb, 3, device=dev)
+                part[..., 0] = 64.0
+                part[..., 1] = torch.rand(N, C, nsb, device=dev)
+                part[..., 2] = 64.0 * torch.rand(N, C, nsb, device=dev)
+                gb = torch.rand(2, C, device=dev)
+                src = nat.NormSrc(part.data_ptr(), nsb, 1, gb[0].data_ptr(), gb[1].data_ptr(), 0.0,
+                                  0x5EED, None, None)
+                sp = nat.norm_src_ptr(src)
+                nb = 2 * u
+
+                def fn():
+                    nat.call("l3u_dw3_fwd", x.data_ptr(), C * S, w.data_ptr(), None, sp,
+                             dx.data_ptr(), C * S, N, C, D, H, W, st)
             else:
                 r = rec.data_ptr() if kind == "fwd1" else None
                 nb = 2 * u
