@@ -243,6 +243,12 @@ def call_bytes(name, a):
         N, ci, co, d, h, w = a[9:15]
         Si = d * h * w
         return "gemm", f"convt_bwd {ci}<-{co} [{N},{d}x{h}x{w}]", N * Si * (4 * 8 * co + e * ci + 4 * ci)
+    if base == "l3u_dwpw_fwd":    # (x, xns, wdw, rec, src, wpw, y, yns, ys, wsc, r, rns, rs, z, zns, N, K, J, D, H, W)
+        N, K, J, D, H, W = a[15:21]
+        S = D * H * W
+        sc = a[9] is not None
+        return ("dw", f"dwsep fwd (dw + pw{' + shortcut' if sc else ''}) [{N},{K}->{J},{D}x{H}x{W}]",
+                e * N * S * (K + J * (1 + sc) + (K if a[13] is not None else 0)) + 4 * K * (27 + J * (1 + sc)))
     if base == "l3u_front_fwd":   # (x, xns, wdw, wpw, wsc, z1, y1, r, s1, so, xc, N, cout, d, h, w)
         N, co, d, h, w = a[11:16]
         S = d * h * w

@@ -928,6 +928,97 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
   }
 }
 
+// ConvTranspose3d(k2, s2) data gradient in the x-PAIR layout (even W):
+//   dX[ci][z,y,x] = sum_{co,a,b,c} w[ci][co*8 + 4a+2b+c] dY[co][2z+a][2y+b][2x+c]
+// MFMA column j = input voxel PAIR q (x = 2xp, 2xp+1): for one (co, a, b) the four dY values of
+// the pair, (2x, c0) (2x, c1) (2x+1, c0) (2x+1, c1), are ONE contiguous float4 of an up-sampled row,
+// so lane (lr, lk) loads dY[co0 + lk][2z+a][2y+b][4xp .. 4xp+3] of pair q0 + lr (16 lanes: 256 B of
+// one row run, no gather, no redundant bytes) and feeds it to four MFMAs: elements 0/1 (c = 0/1)
+// into the even-voxel accumulator, 2/3 into the odd one, with the weights w[ci][co*8+4a+2b+c] as
+// the A operand.  KW waves split the co range (interleaved co quads) and combine through LDS in
+// wave order (deterministic).  Replaces the gathered-GEMM form for the model's decoder shapes.
+template <int NC, int KW>
+__global__ __launch_bounds__(64 * KW) void convt_dx_pair_kernel(
+    const float* __restrict__ dy, long long dyns, const float* __restrict__ w, float* __restrict__ dx,
+    long long dxns, int Ci, int Co, int D, int H, int W) {
+  __shared__ __attribute__((aligned(16))) float red[KW][NC * 2 * 4][64];
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
+  const int WP = W >> 1, P = D * H * WP;
+  const long long S = (long long)D * H * W, S8 = 8 * S;
+  const int q = blockIdx.x * 16 + lr, ci0 = blockIdx.y * 16 * NC, n = blockIdx.z;
+  const bool ok = q < P;
+  const int qq = ok ? q : 0;
+  const int xp = qq % WP, t = qq / WP, y = t % H, z = t / H;
+  const float* dyn = dy + (long long)n * dyns;
+  // row offsets of the four (a, b) up-sampled rows of this pair (within one co plane)
+  long long ro[4];
+#pragma unroll
+  for (int ab = 0; ab < 4; ++ab)
+    ro[ab] = ((long long)(2 * z + (ab >> 1)) * (2 * H) + (2 * y + (ab & 1))) * (2 * W) + 4 * xp;
+  f4 ae[NC], ao[NC];
+#pragma unroll
+  for (int m = 0; m < NC; ++m) ae[m] = ao[m] = f4{0.f, 0.f, 0.f, 0.f};
+  const int nq = (Co + 3) >> 2;
+  for (int cq = wave; cq < nq; cq += KW) {
+    const int co = 4 * cq + lk;
+    const bool cok = co < Co;
+    f4 v[4];
+#pragma unroll
+    for (int ab = 0; ab < 4; ++ab)
+      v[ab] = (ok && cok) ? *reinterpret_cast<const f4*>(dyn + (long long)co * S8 + ro[ab])
+                          : f4{0.f, 0.f, 0.f, 0.f};
+    float wv[NC][8];
+#pragma unroll
+    for (int m = 0; m < NC; ++m) {
+      const int ci = ci0 + 16 * m + lr;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wv[m][e] = (cok && ci < Ci) ? w[(long long)ci * Co * 8 + co * 8 + e] : 0.f;
+    }
+#pragma unroll
+    for (int ab = 0; ab < 4; ++ab)
+#pragma unroll
+      for (int m = 0; m < NC; ++m) {
+        ae[m] = mfma4(wv[m][2 * ab], v[ab][0], ae[m]);
+        ae[m] = mfma4(wv[m][2 * ab + 1], v[ab][1], ae[m]);
+        ao[m] = mfma4(wv[m][2 * ab], v[ab][2], ao[m]);
+        ao[m] = mfma4(wv[m][2 * ab + 1], v[ab][3], ao[m]);
+      }
+  }
+  if (KW > 1) {
+#pragma unroll
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[wave][(m * 2) * 4 + r][l] = ae[m][r];
+        red[wave][(m * 2 + 1) * 4 + r][l] = ao[m][r];
+      }
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float se = red[0][(m * 2) * 4 + r][l], so = red[0][(m * 2 + 1) * 4 + r][l];
+#pragma unroll
+        for (int wv2 = 1; wv2 < KW; ++wv2) {
+          se += red[wv2][(m * 2) * 4 + r][l];
+          so += red[wv2][(m * 2 + 1) * 4 + r][l];
+        }
+        ae[m][r] = se;
+        ao[m][r] = so;
+      }
+  }
+  if (!ok) return;
+  float* dxn = dx + (long long)n * dxns + ((long long)z * H + y) * W + 2 * xp;
+#pragma unroll
+  for (int m = 0; m < NC; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ci = ci0 + 16 * m + 4 * lk + r;
+      if (ci < Ci) *reinterpret_cast<f2_t*>(dxn + (long long)ci * S) = f2_t{ae[m][r], ao[m][r]};
+    }
+}
+
 #ifndef L3U_PW_SCH_MAX
 #define L3U_PW_SCH_MAX 512
 #endif
@@ -1062,6 +1153,9 @@ int pw_bwd_weight_launch(const TD* dy, long long dy_nstride, const TX* x, long l
   L3U_CHECK_LAUNCH();
 }
 
+#ifndef L3U_CONVT_PAIR
+#define L3U_CONVT_PAIR 1   // ConvTranspose3d data gradient in the x-pair layout (even W)
+#endif
 #ifndef L3U_CONVT_ONEPASS_ANYW
 #define L3U_CONVT_ONEPASS_ANYW 0   // 1: W % 4 != 0 (6^3) by scalar gathers (measured 8 us slower)
 #endif
@@ -1188,10 +1282,25 @@ int convt_bwd_impl(const float* dy, long long dy_nstride, const T* x, long long 
                    int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && Ci > 0 && Co > 0 && D > 0 && H > 0 && W > 0);
   const int S = D * H * W;
-  // dX[ci][s] = sum_{co,abc} w[ci][co*8+abc] dY[co][up(s, abc)]: the GEMM with X gathered (all
-  // gradients: fp32)
-  int rc = pw_launch<float>(dy, dy_nstride, w, 0, nullptr, dx, dx_nstride, 0, nullptr, N, Co * 8, Ci,
-                            S, 2, D, H, W, stream);
+  // dX[ci][s] = sum_{co,abc} w[ci][co*8+abc] dY[co][up(s, abc)] (all gradients: fp32): in the
+  // x-pair layout for even W (8-byte aligned rows), else the GEMM with X gathered
+  int rc;
+  if (L3U_CONVT_PAIR && W % 2 == 0 && dy_nstride % 4 == 0 && dx_nstride % 2 == 0 && al4<float>(dy) &&
+      ((uintptr_t)dx & 7) == 0) {
+    const int P = D * H * (W / 2);
+    const int NC = Ci % 32 == 0 && (long long)N * ((P + 15) / 16) * (Ci / 32) >= 256 ? 2 : 1;
+    const int KW = Co >= 16 ? 4 : (Co >= 8 ? 2 : 1);
+    dim3 grid((P + 15) / 16, (Ci + 16 * NC - 1) / (16 * NC), N), block(64 * KW);
+#define CTP(NC_, KW_) hipLaunchKernelGGL((convt_dx_pair_kernel<NC_, KW_>), grid, block, 0, stream, dy, \
+      dy_nstride, w, dx, dx_nstride, Ci, Co, D, H, W)
+    if (NC == 2) { if (KW == 4) CTP(2, 4); else if (KW == 2) CTP(2, 2); else CTP(2, 1); }
+    else { if (KW == 4) CTP(1, 4); else if (KW == 2) CTP(1, 2); else CTP(1, 1); }
+#undef CTP
+    rc = (int)hipGetLastError();
+  } else {
+    rc = pw_launch<float>(dy, dy_nstride, w, 0, nullptr, dx, dx_nstride, 0, nullptr, N, Co * 8, Ci, S,
+                          2, D, H, W, stream);
+  }
   if (rc != 0) return rc;
   // dW[ci][co*8+abc] = sum_s x[ci][s] dY[co][up(s, abc)] and, in the same launch,
   // db[co] = sum of dY over the up-sampled volume: bpart[N*nsc][Co]
