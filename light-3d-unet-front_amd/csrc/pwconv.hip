@@ -1019,6 +1019,117 @@ __global__ __launch_bounds__(64 * KW) void convt_dx_pair_kernel(
     }
 }
 
+// ConvTranspose3d(k2, s2) weight and bias gradients in the same x-pair layout (even W):
+//   part[chunk][ci][co*8 + 4a+2b+c] = sum_{s in chunk} x[ci][s] dY[co][2z+a][2y+b][2x+c]
+// The MFMA k-dimension is the voxel.  Lane (lr, lk) loads the float4 of up-sampled row
+// (co = 4g + lr/4, a, b = lr%4) at voxel pair lk of the step (both voxels of the pair, c = 0 / 1):
+// component (even, c) is B[k = lk][column lr] of the c-MFMA on the pair's even voxel, (odd, c) of
+// the one on its odd voxel, with A = x[ci][that voxel] (a float2 per lane).  Columns c = 0 and
+// c = 1 accumulate separately: acc[m][g][c] holds part[ci0+16m+4lk+r][(4g+lr/4)*8 + 2*(lr%4)+c].
+// Bias partial bsum[chunk][co] = sum of every dY value of co over the chunk's up-sampled voxels.
+// Same partial layout and chunking as pw_bwd_weight_kernel's GATHER form.
+template <typename T, int NJ, int NG>
+__global__ __launch_bounds__(256) void convt_dw_pair_kernel(
+    const T* __restrict__ x, long long xns, const float* __restrict__ dy, long long dyns,
+    float* __restrict__ part, float* __restrict__ bsum, int Ci, int Co, int D, int H, int W,
+    int SCH, int nsc) {
+  __shared__ __attribute__((aligned(16))) float red[4][NJ * NG * 2 * 4][64];
+  __shared__ float bred[4][NG * 4];
+  const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
+  const int WP = W >> 1;
+  const long long S = (long long)D * H * W, S8 = 8 * S;
+  const int sc = blockIdx.x % nsc, n = blockIdx.x / nsc;
+  const int ngb = (Co + 4 * NG - 1) / (4 * NG);
+  const int ci0 = (blockIdx.y / ngb) * 16 * NJ, g0 = (blockIdx.y % ngb) * NG;
+  const int p_lo = sc * (SCH / 2), p_hi = min((int)(S / 2), p_lo + SCH / 2);
+  const int ab = lr & 3, a_ = ab >> 1, b_ = ab & 1;
+  const float* dyn = dy + (long long)n * dyns;
+  const T* xn = x + (long long)n * xns;
+  f4 acc[NJ][NG][2];
+#pragma unroll
+  for (int m = 0; m < NJ; ++m)
+#pragma unroll
+    for (int g = 0; g < NG; ++g) acc[m][g][0] = acc[m][g][1] = f4{0.f, 0.f, 0.f, 0.f};
+  float bacc[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) bacc[g] = 0.f;
+  for (int pb = p_lo + 4 * wave; pb < p_hi; pb += 16) {
+    const int p = pb + lk;
+    const bool ok = p < p_hi;
+    const int pc = ok ? p : p_lo;
+    const int xp = pc % WP, t = pc / WP, y = t % H, z = t / H;
+    const long long ro = ((long long)(2 * z + a_) * (2 * H) + (2 * y + b_)) * (2 * W) + 4 * xp;
+    const long long xo = ((long long)z * H + y) * W + 2 * xp;
+    f4 v[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int co = 4 * (g0 + g) + (lr >> 2);
+      v[g] = (ok && co < Co) ? *reinterpret_cast<const f4*>(dyn + (long long)co * S8 + ro)
+                             : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    f2_t xv[NJ];
+#pragma unroll
+    for (int m = 0; m < NJ; ++m) {
+      const int ci = ci0 + 16 * m + lr;
+      xv[m] = (ok && ci < Ci) ? ldv2(xn + (long long)ci * S + xo) : f2_t{0.f, 0.f};
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      bacc[g] += (v[g][0] + v[g][1]) + (v[g][2] + v[g][3]);
+#pragma unroll
+      for (int m = 0; m < NJ; ++m) {
+        acc[m][g][0] = mfma4(xv[m][0], v[g][0], acc[m][g][0]);
+        acc[m][g][1] = mfma4(xv[m][0], v[g][1], acc[m][g][1]);
+        acc[m][g][0] = mfma4(xv[m][1], v[g][2], acc[m][g][0]);
+        acc[m][g][1] = mfma4(xv[m][1], v[g][3], acc[m][g][1]);
+      }
+    }
+  }
+  // fixed-order cross-wave reduction
+#pragma unroll
+  for (int m = 0; m < NJ; ++m)
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wave][((m * NG + g) * 2 + c) * 4 + r][l] = acc[m][g][c][r];
+  if (bsum != nullptr && ci0 == 0) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {   // lanes of one co: lr%4 (a, b) and lk, in a fixed xor order
+      float bv = bacc[g];
+      bv += __shfl_xor(bv, 1, 64);
+      bv += __shfl_xor(bv, 2, 64);
+      bv += __shfl_xor(bv, 16, 64);
+      bv += __shfl_xor(bv, 32, 64);
+      if (lk == 0 && ab == 0) bred[wave][g * 4 + (lr >> 2)] = bv;
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const int K = Co * 8;
+    float* o = part + (long long)blockIdx.x * Ci * K;
+#pragma unroll
+    for (int m = 0; m < NJ; ++m)
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = ((m * NG + g) * 2 + c) * 4 + r;
+            const float vsum = ((red[0][i][l] + red[1][i][l]) + red[2][i][l]) + red[3][i][l];
+            const int ci = ci0 + 16 * m + 4 * lk + r, co = 4 * (g0 + g) + (lr >> 2);
+            if (ci < Ci && co < Co) o[(long long)ci * K + co * 8 + 2 * ab + c] = vsum;
+          }
+    if (bsum != nullptr && ci0 == 0 && l < NG * 4) {
+      const int co = 4 * g0 + l;
+      if (co < Co)
+        bsum[(long long)blockIdx.x * Co + co] = ((bred[0][l] + bred[1][l]) + bred[2][l]) + bred[3][l];
+    }
+  }
+}
+
 #ifndef L3U_PW_SCH_MAX
 #define L3U_PW_SCH_MAX 512
 #endif
@@ -1155,6 +1266,9 @@ int pw_bwd_weight_launch(const TD* dy, long long dy_nstride, const TX* x, long l
 
 #ifndef L3U_CONVT_PAIR
 #define L3U_CONVT_PAIR 1   // ConvTranspose3d data gradient in the x-pair layout (even W)
+#endif
+#ifndef L3U_CTW_MIN_BLOCKS
+#define L3U_CTW_MIN_BLOCKS 512
 #endif
 #ifndef L3U_CONVT_ONEPASS_ANYW
 #define L3U_CONVT_ONEPASS_ANYW 0   // 1: W % 4 != 0 (6^3) by scalar gathers (measured 8 us slower)
@@ -1304,6 +1418,25 @@ int convt_bwd_impl(const float* dy, long long dy_nstride, const T* x, long long 
   if (rc != 0) return rc;
   // dW[ci][co*8+abc] = sum_s x[ci][s] dY[co][up(s, abc)] and, in the same launch,
   // db[co] = sum of dY over the up-sampled volume: bpart[N*nsc][Co]
+  if (L3U_CONVT_PAIR && W % 2 == 0 && x_nstride % 2 == 0 && dy_nstride % 4 == 0 && al4<float>(dy) &&
+      ((uintptr_t)x & (2 * sizeof(T) - 1)) == 0) {
+    const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
+    // as many (ci, co) tiles per workgroup as keep >= L3U_CTW_MIN_BLOCKS workgroups
+    int NJ = Ci % 32 == 0 ? 2 : 1, NG = Co % 16 == 0 ? 4 : (Co % 8 == 0 ? 2 : 1);
+    for (;;) {
+      const long long nb = (long long)N * nsc * ((Ci + 16 * NJ - 1) / (16 * NJ)) *
+                           ((Co + 4 * NG - 1) / (4 * NG));
+      if (nb >= L3U_CTW_MIN_BLOCKS || (NJ == 1 && NG == 1)) break;
+      if (NG > 1) NG >>= 1; else NJ >>= 1;
+    }
+    dim3 grid(N * nsc, ((Ci + 16 * NJ - 1) / (16 * NJ)) * ((Co + 4 * NG - 1) / (4 * NG))), block(256);
+#define CTW(NJ_, NG_) hipLaunchKernelGGL((convt_dw_pair_kernel<T, NJ_, NG_>), grid, block, 0, stream, x, \
+      x_nstride, dy, dy_nstride, wpart, bpart, Ci, Co, D, H, W, SCH, nsc)
+    if (NJ == 2) { if (NG == 4) CTW(2, 4); else if (NG == 2) CTW(2, 2); else CTW(2, 1); }
+    else { if (NG == 4) CTW(1, 4); else if (NG == 2) CTW(1, 2); else CTW(1, 1); }
+#undef CTW
+    L3U_CHECK_LAUNCH();
+  }
   return pw_bwd_weight_launch<T, float>(x, x_nstride, dy, dy_nstride, wpart, bpart, N, Ci, Co * 8, S,
                                         true, H, W, stream);
 }
