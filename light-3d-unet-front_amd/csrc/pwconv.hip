@@ -1265,8 +1265,11 @@ int pw_bwd_weight_launch(const TD* dy, long long dy_nstride, const TX* x, long l
 }
 
 #ifndef L3U_CONVT_PAIR
-#define L3U_CONVT_PAIR 1   // ConvTranspose3d data gradient in the x-pair layout (even W)
+#define L3U_CONVT_PAIR 1   // ConvTranspose3d backward in the x-pair layout (even W) ...
 #endif
+#ifndef L3U_CONVT_PAIR_MAX_S
+#define L3U_CONVT_PAIR_MAX_S 8192   // ... for input volumes up to this size (rocprof r2s: at 6^3
+#endif                              // 35.4 -> 19.8 us; at 24^3 34.3 -> 37.1 us, so not there)
 #ifndef L3U_CTW_MIN_BLOCKS
 #define L3U_CTW_MIN_BLOCKS 512
 #endif
@@ -1399,7 +1402,8 @@ int convt_bwd_impl(const float* dy, long long dy_nstride, const T* x, long long 
   // dX[ci][s] = sum_{co,abc} w[ci][co*8+abc] dY[co][up(s, abc)] (all gradients: fp32): in the
   // x-pair layout for even W (8-byte aligned rows), else the GEMM with X gathered
   int rc;
-  if (L3U_CONVT_PAIR && W % 2 == 0 && dy_nstride % 4 == 0 && dx_nstride % 2 == 0 && al4<float>(dy) &&
+  if (L3U_CONVT_PAIR && S <= L3U_CONVT_PAIR_MAX_S && W % 2 == 0 && dy_nstride % 4 == 0 &&
+      dx_nstride % 2 == 0 && al4<float>(dy) &&
       ((uintptr_t)dx & 7) == 0) {
     const int P = D * H * (W / 2);
     const int NC = Ci % 32 == 0 && (long long)N * ((P + 15) / 16) * (Ci / 32) >= 256 ? 2 : 1;
@@ -1418,7 +1422,8 @@ int convt_bwd_impl(const float* dy, long long dy_nstride, const T* x, long long 
   if (rc != 0) return rc;
   // dW[ci][co*8+abc] = sum_s x[ci][s] dY[co][up(s, abc)] and, in the same launch,
   // db[co] = sum of dY over the up-sampled volume: bpart[N*nsc][Co]
-  if (L3U_CONVT_PAIR && W % 2 == 0 && x_nstride % 2 == 0 && dy_nstride % 4 == 0 && al4<float>(dy) &&
+  if (L3U_CONVT_PAIR && S <= L3U_CONVT_PAIR_MAX_S && W % 2 == 0 && x_nstride % 2 == 0 &&
+      dy_nstride % 4 == 0 && al4<float>(dy) &&
       ((uintptr_t)x & (2 * sizeof(T) - 1)) == 0) {
     const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
     // as many (ci, co) tiles per workgroup as keep >= L3U_CTW_MIN_BLOCKS workgroups
