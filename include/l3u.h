@@ -139,6 +139,13 @@ int l3u_pw_bwd_tail(const float* dout, long long dout_nstride, const float* out,
                     const double* tail_part, int npart, int sel, const float* x,
                     long long x_nstride, const float* w, float* dx, long long dx_nstride,
                     int accumulate, float* part, int N, int J, int K, int S, hipStream_t stream);
+/* the same with a rank-1 dout[j] = dscale[j] * dz (dz one channel: l3u_outconv_bwd_dz)       */
+int l3u_pw_bwd_tail_r1(const float* dz, long long dz_nstride, const float* dscale,
+                       const float* out, long long out_nstride, const float* yr,
+                       long long yr_nstride, const float* rec, const double* tail_part, int npart,
+                       int sel, const float* x, long long x_nstride, const float* w, float* dx,
+                       long long dx_nstride, int accumulate, float* part, int N, int J, int K,
+                       int S, hipStream_t stream);
 
 int l3u_pw_bwd_nparts(int N, int J, int K, int S);
 int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long y_nstride,
@@ -180,6 +187,12 @@ int l3u_norm_act_bwd_reduce(const float* dout, long long dout_nstride, const flo
                             const float* rec2, const float* r, long long r_nstride,
                             const float* rec_r, double* part, int N, int C, int S,
                             hipStream_t stream);
+/* the same with a rank-1 dout[c] = dscale[c] * dz (dz one channel: l3u_outconv_bwd_dz)      */
+int l3u_norm_act_bwd_reduce_r1(const float* dz, long long dz_nstride, const float* dscale,
+                               const float* out, long long out_nstride, const float* y2,
+                               long long y2_nstride, const float* rec2, const float* r,
+                               long long r_nstride, const float* rec_r, double* part, int N, int C,
+                               int S, hipStream_t stream);
 int l3u_norm_act_bwd_apply(const float* dout, long long dout_nstride, const float* out,
                            long long out_nstride, const float* y2, long long y2_nstride,
                            const float* rec2, const float* r, long long r_nstride,
@@ -255,6 +268,20 @@ int l3u_outconv_bwd_ftl(const float* p, const float* t, const float* ftl_part, i
                         const float* gscale, const float* h, long long h_nstride, const float* w,
                         float* dh, long long dh_nstride, double* part, float* loss, int N, int C,
                         int S, hipStream_t stream);
+/* the two out_conv backward forms writing dz = d(pre-sigmoid) [N][S] (batch stride dh_nstride)
+ * into dh instead of dh[c] = w[c] * dz: out_conv (unet3d.py:201) is rank-1, so the last block's
+ * tail backward takes dz and w through the _r1 entry points below and the [N][C][S] output
+ * gradient is never stored (same values, bit for bit).                                       */
+int l3u_outconv_bwd_dz(const float* dp, const float* p, const float* t, const double* sums,
+                       double alpha, double beta, double gamma, double smooth, const float* gscale,
+                       const float* h, long long h_nstride, const float* w, float* dh,
+                       long long dh_nstride, double* part, float* loss, int N, int C, int S,
+                       hipStream_t stream);
+int l3u_outconv_bwd_ftl_dz(const float* p, const float* t, const float* ftl_part, int ftl_nparts,
+                           double alpha, double beta, double gamma, double smooth,
+                           const float* gscale, const float* h, long long h_nstride,
+                           const float* w, float* dh, long long dh_nstride, double* part,
+                           float* loss, int N, int C, int S, hipStream_t stream);
 
 /* ---- Training patches (light_unet/datasets/patch_dataset.py:114-220) -----------------------
  * One record per patch: the case volume it is cut from (device pointers, [sd][sh][sw] fp32), the
@@ -481,6 +508,28 @@ int l3u_dwpw_fwd_bf16(const l3u_bf16* x, long long x_nstride, const float* w_dw,
                       float* y_stat, const float* w_sc, l3u_bf16* r, long long r_nstride,
                       float* r_stat, l3u_bf16* z, long long z_nstride, int N, int K, int Nout,
                       int D, int H, int W, hipStream_t stream);
+int l3u_outconv_bwd_dz_bf16(const float* dp, const float* p, const float* t, const double* sums,
+                            double alpha, double beta, double gamma, double smooth,
+                            const float* gscale, const l3u_bf16* h, long long h_nstride,
+                            const float* w, float* dh, long long dh_nstride, double* part,
+                            float* loss, int N, int C, int S, hipStream_t stream);
+int l3u_outconv_bwd_ftl_dz_bf16(const float* p, const float* t, const float* ftl_part,
+                                int ftl_nparts, double alpha, double beta, double gamma,
+                                double smooth, const float* gscale, const l3u_bf16* h,
+                                long long h_nstride, const float* w, float* dh,
+                                long long dh_nstride, double* part, float* loss, int N, int C,
+                                int S, hipStream_t stream);
+int l3u_norm_act_bwd_reduce_r1_bf16(const float* dz, long long dz_nstride, const float* dscale,
+                                    const l3u_bf16* out, long long out_nstride, const l3u_bf16* y2,
+                                    long long y2_nstride, const float* rec2, const l3u_bf16* r,
+                                    long long r_nstride, const float* rec_r, double* part, int N,
+                                    int C, int S, hipStream_t stream);
+int l3u_pw_bwd_tail_r1_bf16(const float* dz, long long dz_nstride, const float* dscale,
+                            const l3u_bf16* out, long long out_nstride, const l3u_bf16* yr,
+                            long long yr_nstride, const float* rec, const double* tail_part,
+                            int npart, int sel, const l3u_bf16* x, long long x_nstride,
+                            const float* w, float* dx, long long dx_nstride, int accumulate,
+                            float* part, int N, int J, int K, int S, hipStream_t stream);
 int l3u_pw_fwd2_bf16(const l3u_bf16* xa, long long xa_nstride, const float* wa, l3u_bf16* ya,
                      long long ya_nstride, float* stat_a, const l3u_bf16* xb, long long xb_nstride,
                      const float* wb, l3u_bf16* yb, long long yb_nstride, float* stat_b, int N,

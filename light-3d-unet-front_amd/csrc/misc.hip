@@ -144,7 +144,7 @@ L3U_DEV FtlCoef ftl_coef(const double* sums, double alpha, double beta, double g
 // global sums (losses.py:30-54), fused so the loss gradient is never written out.
 template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void outconv_bwd_kernel(
-    const float* __restrict__ dp, const float* __restrict__ p, const float* __restrict__ t,
+    int dz_only, const float* __restrict__ dp, const float* __restrict__ p, const float* __restrict__ t,
     const double* __restrict__ sums, double alpha, double beta, double gamma, double smooth,
     const float* __restrict__ gscale, const T* __restrict__ h, long long hns,
     const float* __restrict__ w, float* __restrict__ dh, long long dhns,
@@ -199,6 +199,15 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
 #pragma unroll
   for (int c = 0; c < 33; ++c) acc[c] = 0.f;
   acc[32] = (dz[0] + dz[1]) + (dz[2] + dz[3]);
+  if (dz_only) {   // d(pre-sigmoid) only: the consumers form dh[c] = w[c] * dz on the fly
+    if (VEC) {
+      if (i0 < S) stv4(dhp + i0, dz);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (i0 + q < S) st1(dhp + i0 + q, dz[q]);
+    }
+  }
 #pragma unroll
   for (int c = 0; c < 32; ++c) {
     if (c < C) {
@@ -206,14 +215,14 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
         if (i0 < S) {
           const f4 hv = ldv4(hp + (long long)c * S + i0);
           acc[c] = fmaf(dz[0], hv[0], fmaf(dz[1], hv[1], fmaf(dz[2], hv[2], dz[3] * hv[3])));
-          stv4(dhp + (long long)c * S + i0, w[c] * dz);
+          if (!dz_only) stv4(dhp + (long long)c * S + i0, w[c] * dz);
         }
       } else {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (i0 + q < S) {
             acc[c] = fmaf(dz[q], ld1(hp + (long long)c * S + i0 + q), acc[c]);
-            st1(dhp + (long long)c * S + i0 + q, w[c] * dz[q]);
+            if (!dz_only) st1(dhp + (long long)c * S + i0 + q, w[c] * dz[q]);
           }
       }
     }
@@ -633,15 +642,15 @@ int outconv_bwd_impl(const float* dp, const float* p, const float* t, const doub
                      double alpha, double beta, double gamma, double smooth, const float* gscale,
                      const T* h, long long h_nstride, const float* w, float* dh, long long dh_nstride,
                      double* part, float* loss, int N, int C, int S, hipStream_t stream,
-                     const float* fpart = nullptr, int fnp = 0) {
+                     const float* fpart = nullptr, int fnp = 0, int dz_only = 0) {
   L3U_REQUIRE(N > 0 && C > 0 && C <= 32 && S > 0);
   L3U_REQUIRE(dp != nullptr || (t != nullptr && (sums != nullptr || (fpart != nullptr && fnp > 0))));
   const bool vec = S % 4 == 0 && h_nstride % 4 == 0 && dh_nstride % 4 == 0;
   dim3 grid((S + 1023) / 1024, N);
   size_t lds = 4 * (C + 1) * sizeof(double);
   if (fpart != nullptr && lds < 3 * 64 * sizeof(double)) lds = 3 * 64 * sizeof(double);
-  if (vec) hipLaunchKernelGGL((outconv_bwd_kernel<T, true>), grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S, fpart, fnp);
-  else hipLaunchKernelGGL((outconv_bwd_kernel<T, false>), grid, dim3(256), lds, stream, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S, fpart, fnp);
+  if (vec) hipLaunchKernelGGL((outconv_bwd_kernel<T, true>), grid, dim3(256), lds, stream, dz_only, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S, fpart, fnp);
+  else hipLaunchKernelGGL((outconv_bwd_kernel<T, false>), grid, dim3(256), lds, stream, dz_only, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S, fpart, fnp);
   L3U_CHECK_LAUNCH();
 }
 
@@ -691,6 +700,14 @@ L3U_TWIN(l3u_outconv_bwd, P_OCB, outconv_bwd_impl(dp, p, t, sums, alpha, beta, g
 L3U_TWIN(l3u_outconv_bwd_ftl, P_OCBF, outconv_bwd_impl((const float*)nullptr, p, t, (const double*)nullptr,
          alpha, beta, gamma, smooth, gscale, bp(h), h_nstride, w, dh, dh_nstride, part, loss, N, C, S,
          stream, ftl_part, ftl_nparts))
+// the same two forms writing dz = d(pre-sigmoid) [N][S] (batch stride dz_nstride) instead of dh:
+// out_conv is rank-1 (dh[c] = w[c] * dz), so the last block's tail consumers read dz (the _r1
+// entry points) and dh is never stored
+L3U_TWIN(l3u_outconv_bwd_dz, P_OCB, outconv_bwd_impl(dp, p, t, sums, alpha, beta, gamma, smooth, gscale,
+         bp(h), h_nstride, w, dh, dh_nstride, part, loss, N, C, S, stream, nullptr, 0, 1))
+L3U_TWIN(l3u_outconv_bwd_ftl_dz, P_OCBF, outconv_bwd_impl((const float*)nullptr, p, t,
+         (const double*)nullptr, alpha, beta, gamma, smooth, gscale, bp(h), h_nstride, w, dh, dh_nstride,
+         part, loss, N, C, S, stream, ftl_part, ftl_nparts, 1))
 template <typename T>
 int box_copy_impl(const T* src, long long sns, int sd, int sh, int sw, T* dst, long long dns, int dd,
                   int dh, int dw, int oz, int oy, int ox, int N, int C, hipStream_t stream) {

@@ -168,21 +168,24 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     const float* __restrict__ dout, long long dns, const T* __restrict__ out, long long ons,
     const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
     const T* __restrict__ r, long long rns, const float* __restrict__ recr,
-    double* __restrict__ part, int N, int C, int S) {
+    double* __restrict__ part, int N, int C, int S, const float* __restrict__ dscale = nullptr) {
   __shared__ double red[4];
   const int nc = blockIdx.y, c = nc % C, n = nc / C, nb = gridDim.x;
   const float m2 = rec2[(long long)nc * kRec + 0], rs2 = rec2[(long long)nc * kRec + 1];
   float mr = 0.f, rsr = 1.f;
   if (recr) { mr = recr[(long long)nc * kRec + 0]; rsr = recr[(long long)nc * kRec + 1]; }
   const long long co = (long long)c * S;
-  const float* dp = dout + (long long)n * dns + co;
+  // dscale: rank-1 dout = dscale[c] * dz (dz one channel, l3u_outconv_bwd_dz)
+  const float* dp = dout + (long long)n * dns + (dscale ? 0 : co);
+  const float dsc = dscale ? dscale[c] : 1.f;
   const T* op = out + (long long)n * ons + co;
   const T* yp = y2 + (long long)n * y2ns + co;
   const T* rp = r + (long long)n * rns + co;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
   if (VEC) {
     for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += nb * 1024) {
-      const f4 dv = ldv4(dp + i), ov = ldv4(op + i);
+      const f4 ov = ldv4(op + i);
+      const f4 dv = dscale ? dsc * ldv4(dp + i) : ldv4(dp + i);
       const f4 yv = ldv4(yp + i);
       f4 rv = f4{0.f, 0.f, 0.f, 0.f};
       if (recr) rv = ldv4(rp + i);
@@ -196,7 +199,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     }
   } else {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += nb * 256) {
-      const float g = ld1(dp + i) * lrelu_d(ld1(op + i));
+      const float g = (dscale ? dsc * ld1(dp + i) : ld1(dp + i)) * lrelu_d(ld1(op + i));
       s0 += g;
       s1 += (double)g * ((ld1(yp + i) - m2) * rs2);
       if (recr) s2 += (double)g * ((ld1(rp + i) - mr) * rsr);
@@ -458,13 +461,13 @@ int norm_act_bwd_reduce_impl(const float* dout, long long dout_nstride, const T*
                              long long out_nstride, const T* y2, long long y2_nstride,
                              const float* rec2, const T* r, long long r_nstride,
                              const float* rec_r, double* part, int N, int C, int S,
-                             hipStream_t stream) {
+                             hipStream_t stream, const float* dscale = nullptr) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
   const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
                    y2_nstride % 4 == 0 && r_nstride % 4 == 0;
   dim3 grid(elem_blocks(S), N * C);
-  if (vec) hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S);
-  else hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, false>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S);
+  if (vec) hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale);
+  else hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, false>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale);
   L3U_CHECK_LAUNCH();
 }
 
@@ -534,6 +537,13 @@ L3U_TWIN(l3u_norm_act_pool_fwd, P_NAP, norm_act_pool_fwd_impl(bp(y2), y2_nstride
     const float* rec_r, double* part, int N, int C, int S, hipStream_t stream)
 L3U_TWIN(l3u_norm_act_bwd_reduce, P_NBR, norm_act_bwd_reduce_impl(dout, dout_nstride, bp(out),
          out_nstride, bp(y2), y2_nstride, rec2, bp(r), r_nstride, rec_r, part, N, C, S, stream))
+// rank-1 output gradient dout[c] = dscale[c] * dz (dz: one channel, batch stride dz_nstride)
+#define P_NBR1(TT) (const float* dz, long long dz_nstride, const float* dscale, const TT* out,        \
+    long long out_nstride, const TT* y2, long long y2_nstride, const float* rec2, const TT* r,       \
+    long long r_nstride, const float* rec_r, double* part, int N, int C, int S, hipStream_t stream)
+L3U_TWIN(l3u_norm_act_bwd_reduce_r1, P_NBR1, dscale == nullptr ? (int)hipErrorInvalidValue :
+         norm_act_bwd_reduce_impl(dz, dz_nstride, bp(out), out_nstride, bp(y2), y2_nstride, rec2, bp(r),
+         r_nstride, rec_r, part, N, C, S, stream, dscale))
 #define P_NBA(TT) (const float* dout, long long dout_nstride, const TT* out, long long out_nstride,   \
     const TT* y2, long long y2_nstride, const float* rec2, const TT* r, long long r_nstride,        \
     const float* rec_r, const double* part, float* dy2, long long dy2_nstride, float* dr,          \

@@ -566,7 +566,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const T* __restrict__ x, long long xns, const float* __restrict__ w,
     float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part, int N, int J,
     int K, int S, int SCH, int nsc, const T* __restrict__ oin = nullptr, long long oins = 0,
-    int sel = 1) {
+    int sel = 1, const float* __restrict__ dscale = nullptr) {
   constexpr int TJ = 16 * NJ, TK = 16 * NK, JR = TJ / 4;
   constexpr int WS = TK + ((16 - TK) % 64 + 64) % 64;   // >= TK, = 16 mod 64
   constexpr int DS = 68;                                // dY tile row stride (floats)
@@ -592,7 +592,12 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   for (int jr = 0; jr < JR; ++jr) {
     const int j = 4 * jr + lk;
     g[jr] = f4{0.f, 0.f, 0.f, 0.f};
-    if (j < J && sd < s_hi) g[jr] = ldv4(dyn + (long long)j * S + sd);
+    if (j < J && sd < s_hi) {
+      if (PRO == 2 && dscale != nullptr)   // rank-1 dout[j] = dscale[j] * dz (l3u_outconv_bwd_dz)
+        g[jr] = dscale[j] * ldv4(dyn + sd);
+      else
+        g[jr] = ldv4(dyn + (long long)j * S + sd);
+    }
   }
   if (PRO == 2) {   // the block output (LeakyReLU mask of the tail)
     const T* on = oin + (long long)n * oins;
@@ -1298,7 +1303,7 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
                      const T* yr, long long yr_nstride, const float* rec, const double* tail_part,
                      int npart, int sel, const T* x, long long x_nstride, const float* w, float* dx,
                      long long dx_nstride, int accumulate, float* part, int N, int J, int K, int S,
-                     hipStream_t stream) {
+                     hipStream_t stream, const float* dscale = nullptr) {
   L3U_REQUIRE(N > 0 && l3u_pw_bwd_supported(J, K, S) && !pw_bwd_wide(J));
   L3U_REQUIRE(dout && out && yr && rec && tail_part && npart > 0 && (sel == 1 || sel == 2));
   L3U_REQUIRE(x && w && dx && part);
@@ -1315,7 +1320,7 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
 #define PWBT(A_, B_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2>), grid, block, 0, stream, \
       dout, dout_nstride, yr, yr_nstride, rec, tail_part, npart, x, x_nstride, w, dx, dx_nstride, \
-      accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel)
+      accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel, dscale)
   if (NJ == 1 && NK == 1) PWBT(1, 1);
   else if (NJ == 1 && NK == 2) PWBT(1, 2);
   else if (NJ == 1 && NK == 4) PWBT(1, 4);
@@ -1526,6 +1531,15 @@ L3U_TWIN(l3u_pw_bwd_weight, P_PBW, pw_bwd_weight_launch(dy, dy_nstride, bp(x), x
 L3U_TWIN(l3u_pw_bwd_tail, P_PBT, pw_bwd_tail_impl(dout, dout_nstride, bp(out), out_nstride, bp(yr),
          yr_nstride, rec, tail_part, npart, sel, bp(x), x_nstride, w, dx, dx_nstride, accumulate,
          part, N, J, K, S, stream))
+// rank-1 block-output gradient dout[j] = dscale[j] * dz (dz one channel, l3u_outconv_bwd_dz)
+#define P_PBT1(TT) (const float* dz, long long dz_nstride, const float* dscale, const TT* out,        \
+    long long out_nstride, const TT* yr, long long yr_nstride, const float* rec,                     \
+    const double* tail_part, int npart, int sel, const TT* x, long long x_nstride, const float* w,   \
+    float* dx, long long dx_nstride, int accumulate, float* part, int N, int J, int K, int S,        \
+    hipStream_t stream)
+L3U_TWIN(l3u_pw_bwd_tail_r1, P_PBT1, dscale == nullptr ? (int)hipErrorInvalidValue :
+         pw_bwd_tail_impl(dz, dz_nstride, bp(out), out_nstride, bp(yr), yr_nstride, rec, tail_part,
+         npart, sel, bp(x), x_nstride, w, dx, dx_nstride, accumulate, part, N, J, K, S, stream, dscale))
 #define P_PBD(TT) (const float* dy, long long dy_nstride, const TT* y, long long y_nstride,         \
     const float* rec, const double* in_part, int npart, const TT* x, long long x_nstride,           \
     const float* w, float* dx, long long dx_nstride, int accumulate, float* part, int N, int J,     \

@@ -36,14 +36,19 @@ _SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32").sp
 # the chip, tools/dwpw_bench.py); L3U_DWPW=0 disables
 _DWPW = os.environ.get("L3U_DWPW", "1") != "0"
 _DWPW_MIN_S = int(os.environ.get("L3U_DWPW_MIN_S", "65536"))
+# the out_conv backward hands the last block d(pre-sigmoid) and w (out_conv is rank-1) instead
+# of the [N, C, S] output gradient (l3u_outconv_bwd_dz + the _r1 tail kernels); L3U_RANK1=0
+# disables
+_RANK1 = os.environ.get("L3U_RANK1", "1") != "0"
 
 
 class V:
-    """A strided activation view: channel c of sample n at t[off + n*ns + c*S]."""
-    __slots__ = ("t", "off", "ns", "C")
+    """A strided activation view: channel c of sample n at t[off + n*ns + c*S].  scale (a device
+    pointer to C floats): a rank-1 gradient, channel c = scale[c] * the one stored channel."""
+    __slots__ = ("t", "off", "ns", "C", "scale")
 
-    def __init__(self, t, off, ns, C):
-        self.t, self.off, self.ns, self.C = t, off, ns, C
+    def __init__(self, t, off, ns, C, scale=None):
+        self.t, self.off, self.ns, self.C, self.scale = t, off, ns, C, scale
 
     @property
     def p(self):
@@ -624,14 +629,20 @@ class UNetEngine:
         A = self.bwd_arena
         # ---- out_conv + sigmoid (unet3d.py:220-221)
         h = sv["h"]
-        dh = e(N, c0, S[0])
+        up3 = sv["blk"]["up3.res_block."]
+        # rank-1 hand-off: the tail kernels of the last block form dout[c] = w[c] * dz themselves
+        r1 = _RANK1 and self.kinds["up3.res_block."][0][0] == "ds" and \
+            self._tail_fusable(up3, up3["x"].C, c0, S[0])
+        sfx = "_dz" if r1 else ""
+        dh = e(N, 1, S[0]) if r1 else e(N, c0, S[0])
+        dhns = S[0] if r1 else c0 * S[0]
         nb = nat.query("l3u_outconv_nblocks", S[0])
         po = A.alloc(2 * N * nb * (c0 + 1))          # fp64 partials
         loss_ptr = None
         if dp is not None:
             g = (dp.data_ptr(), None, None, 0.0, 0.0, 0.0, 0.0, None)
-            self._call("l3u_outconv_bwd", g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
-                       self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po),
+            self._call("l3u_outconv_bwd" + sfx, g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
+                       self._w(flat, "out_conv.weight"), dh.data_ptr(), dhns, A.ptr(po),
                        loss_ptr, N, c0, S[0], st)
         else:   # FocalTversky gradient formed inside the kernel from the global sums
             t, sums, (alpha, beta, gamma, smooth) = ftl[:3]
@@ -639,20 +650,20 @@ class UNetEngine:
                 loss_ptr = ftl[3].data_ptr()
             if sums is None:   # the sums reduced inside the launch from the forward's partials
                 fpart, fnp = ftl[4], ftl[5]
-                self._call("l3u_outconv_bwd_ftl", sv["p"].data_ptr(), t.data_ptr(), fpart.data_ptr(),
-                           fnp, alpha, beta, gamma, smooth, None, h.p, h.ns,
-                           self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po),
+                self._call("l3u_outconv_bwd_ftl" + sfx, sv["p"].data_ptr(), t.data_ptr(),
+                           fpart.data_ptr(), fnp, alpha, beta, gamma, smooth, None, h.p, h.ns,
+                           self._w(flat, "out_conv.weight"), dh.data_ptr(), dhns, A.ptr(po),
                            loss_ptr, N, c0, S[0], st)
             else:
-                self._call("l3u_outconv_bwd", None, sv["p"].data_ptr(), t.data_ptr(), sums.data_ptr(),
-                           alpha, beta, gamma, smooth, None, h.p, h.ns,
-                           self._w(flat, "out_conv.weight"), dh.data_ptr(), c0 * S[0], A.ptr(po),
+                self._call("l3u_outconv_bwd" + sfx, None, sv["p"].data_ptr(), t.data_ptr(),
+                           sums.data_ptr(), alpha, beta, gamma, smooth, None, h.p, h.ns,
+                           self._w(flat, "out_conv.weight"), dh.data_ptr(), dhns, A.ptr(po),
                            loss_ptr, N, c0, S[0], st)
         self._seg(po // 2, N * nb, c0 + 1, 1, c0, "out_conv.weight", f64=1)
         self._seg(po // 2 + c0, N * nb, c0 + 1, 1, 1, "out_conv.bias", f64=1)
         dcat3, dcat2, dcat1 = e(N, 2 * c0, S[0]), e(N, 2 * c1, S[1]), e(N, 2 * c2, S[2])
         dcats = {0: dcat3, 1: dcat2, 2: dcat1}
-        dout = V(dh, 0, c0 * S[0], c0)
+        dout = V(dh, 0, dhns, c0, self._w(flat, "out_conv.weight") if r1 else None)
         # ---- decoder (reverse order); up_specs = (prefix, Co, level, index into sv["ups"])
         up_specs = [("up3.", c0, 0, 2), ("up2.", c1, 1, 1), ("up1.", c2, 2, 0)]
         for up, co, lvl, uidx in up_specs:
@@ -746,9 +757,15 @@ class UNetEngine:
         if fused:
             self._seg(pnd + 2, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.weight", f64=1)
             self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.bias", f64=1)
-            self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(),
-                       cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S, st)
+            if dout.scale is not None:   # rank-1 dout (l3u_outconv_bwd_dz)
+                self._call("l3u_norm_act_bwd_reduce_r1", dout.p, dout.ns, dout.scale, out.p, out.ns,
+                           y2.data_ptr(), cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S,
+                           st)
+            else:
+                self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(),
+                           cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S, st)
             return pn, nb
+        assert dout.scale is None, "a rank-1 output gradient needs the fused block tail"
         dy2 = self._empty(N, cout, S, device=dev)
         if shortcut:
             dr = self._empty(N, cout, S, device=dev)
@@ -928,9 +945,14 @@ class UNetEngine:
         A = self.bwd_arena
         npw = nat.query("l3u_pw_bwd_nparts", N, J, K, S)
         part = A.alloc(npw * J * K)
-        self._call("l3u_pw_bwd_tail", dout.p, dout.ns, out.p, out.ns, yr.p, yr.ns, rec, A.ptr(pn),
-                   ntp, sel, x.p, x.ns, self._w(flat, name), dx.p, dx.ns, accumulate, A.ptr(part),
-                   N, J, K, S, st)
+        if dout.scale is not None:   # rank-1 dout (l3u_outconv_bwd_dz)
+            self._call("l3u_pw_bwd_tail_r1", dout.p, dout.ns, dout.scale, out.p, out.ns, yr.p, yr.ns,
+                       rec, A.ptr(pn), ntp, sel, x.p, x.ns, self._w(flat, name), dx.p, dx.ns,
+                       accumulate, A.ptr(part), N, J, K, S, st)
+        else:
+            self._call("l3u_pw_bwd_tail", dout.p, dout.ns, out.p, out.ns, yr.p, yr.ns, rec,
+                       A.ptr(pn), ntp, sel, x.p, x.ns, self._w(flat, name), dx.p, dx.ns, accumulate,
+                       A.ptr(part), N, J, K, S, st)
         self._seg(part, npw, J * K, 1, J * K, name)
 
     def _seg_dw(self, off, count, C, name):

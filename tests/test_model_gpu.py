@@ -294,3 +294,36 @@ def test_trainstep_data_parallel_two_ranks(cuda, tmp_path):
         np.testing.assert_array_equal(k0, ks[:k0.size])
     assert differ, "both ranks drew the same Dropout3d masks"
 
+
+
+def test_rank1_output_gradient_bitwise(cuda, golden):
+    """out_conv is rank-1 (unet3d.py:201): handing the last block d(pre-sigmoid) and the out_conv
+    weight (l3u_outconv_bwd_dz + the _r1 tail kernels) gives bitwise the gradients of the
+    materialised [N, C, S] output gradient, for the FocalTversky and the given-dL/dp forms."""
+    import light_unet.engine as E
+    from light_unet.models.unet3d import Lightweight3DUNet
+    from light_unet.train_step import TrainStep
+    z = golden("model_b2_32.npz")
+    sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w/")}
+    x = torch.from_numpy(z["x"]).to(cuda)
+    t = torch.from_numpy(z["target"]).to(cuda)
+    res = []
+    for r1 in (True, False):
+        E._RANK1 = r1
+        try:
+            m = Lightweight3DUNet(dropout_p=0.1)
+            m.load_state_dict(sd)
+            m = m.to(cuda).train()
+            ts = TrainStep(m)
+            p, sv, sums = ts._fwd(x, t)
+            ts._bwd(p, sv, t, sums)
+            g1 = ts.gflat.clone()
+            dp = torch.rand(p.shape, generator=torch.Generator().manual_seed(9)).to(cuda)
+            gg = torch.zeros_like(ts.gflat)
+            m.engine.backward(ts.flat, gg, sv, dp)
+            torch.cuda.synchronize()
+            res.append((g1, gg, ts.loss.clone()))
+        finally:
+            E._RANK1 = True
+    for name, a, b in zip(("ftl grad", "dp grad", "loss"), *res):
+        assert torch.equal(a, b), (name, (a - b).abs().max().item())
