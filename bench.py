@@ -232,6 +232,15 @@ def call_bytes(name, a):
         N, J, K, S = a[17:21]
         return ("gemm", f"pw_bwd_tail{a[9]} {J}->{K} [{N},{S}]",
                 N * S * (4 * J + 2 * e * J + e * K + 4 * K * (1 + a[15])))
+    if base == "l3u_pw_bwd_tail_r1":  # (dz, dzns, dscale, out, ons, yr, yns, rec, pn, ntp, sel, x, xns, w, dx, dxns, acc, part, N, J, K, S)
+        N, J, K, S = a[18:22]           # rank-1 dout: one fp32 channel
+        return ("gemm", f"pw_bwd_tail{a[10]} (rank-1 dout) {J}->{K} [{N},{S}]",
+                N * S * (4 + 2 * e * J + e * K + 4 * K * (1 + a[16])))
+    if base == "l3u_pw_bwd_tail_up":  # (dskip, dskns, dpool, dpns, idx, out, ons, yr, yns, rec, pn, ntp, sel, x, xns, w, dx, dxns, acc, part, N, J, K, D, H, W)
+        N, J, K, D, H, W = a[20:26]     # dout = skip gradient + unpooled dpool (+ argmax bytes)
+        S = D * H * W
+        return ("gemm", f"pw_bwd_tail{a[12]} (+maxpool bwd) {J}->{K} [{N},{S}]",
+                N * S * (4 * J + 4 * J / 8 + J / 8 + 2 * e * J + e * K + 4 * K * (1 + a[18])))
     if base == "l3u_pw_bwd_weight":  # (dy, dyns, x, xns, part, N, J, K, S)
         N, J, K, S = a[5:9]
         return "gemm", f"pw_bwd_weight {J}x{K} [{N},{S}]", N * S * (4 * J + e * K)

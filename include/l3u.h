@@ -146,6 +146,14 @@ int l3u_pw_bwd_tail_r1(const float* dz, long long dz_nstride, const float* dscal
                        int sel, const float* x, long long x_nstride, const float* w, float* dx,
                        long long dx_nstride, int accumulate, float* part, int N, int J, int K,
                        int S, hipStream_t stream);
+/* the same with dout = dskip + the next level's MaxPool3d backward (as l3u_norm_act_bwd_reduce_up) */
+int l3u_pw_bwd_tail_up(const float* dskip, long long dskip_nstride, const float* dpool,
+                       long long dpool_nstride, const unsigned char* idx, const float* out,
+                       long long out_nstride, const float* yr, long long yr_nstride,
+                       const float* rec, const double* tail_part, int npart, int sel,
+                       const float* x, long long x_nstride, const float* w, float* dx,
+                       long long dx_nstride, int accumulate, float* part, int N, int J, int K, int D,
+                       int H, int W, hipStream_t stream);
 
 int l3u_pw_bwd_nparts(int N, int J, int K, int S);
 int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long y_nstride,
@@ -193,6 +201,16 @@ int l3u_norm_act_bwd_reduce_r1(const float* dz, long long dz_nstride, const floa
                                long long y2_nstride, const float* rec2, const float* r,
                                long long r_nstride, const float* rec_r, double* part, int N, int C,
                                int S, hipStream_t stream);
+/* the same with dout = dskip + the MaxPool3d(2) backward of the next level (DownBlock,
+ * unet3d.py:104: l3u_maxpool2_bwd's expression applied on load, so the level-output gradient is
+ * never stored): dpool [N][C][S/8] (batch stride dpool_nstride), idx [N][C][S/8] as written by
+ * l3u_maxpool2_fwd; even D and H, W % 4 == 0.                                                 */
+int l3u_norm_act_bwd_reduce_up(const float* dskip, long long dskip_nstride, const float* dpool,
+                               long long dpool_nstride, const unsigned char* idx, const float* out,
+                               long long out_nstride, const float* y2, long long y2_nstride,
+                               const float* rec2, const float* r, long long r_nstride,
+                               const float* rec_r, double* part, int N, int C, int D, int H, int W,
+                               hipStream_t stream);
 int l3u_norm_act_bwd_apply(const float* dout, long long dout_nstride, const float* out,
                            long long out_nstride, const float* y2, long long y2_nstride,
                            const float* rec2, const float* r, long long r_nstride,
@@ -530,6 +548,20 @@ int l3u_pw_bwd_tail_r1_bf16(const float* dz, long long dz_nstride, const float* 
                             int npart, int sel, const l3u_bf16* x, long long x_nstride,
                             const float* w, float* dx, long long dx_nstride, int accumulate,
                             float* part, int N, int J, int K, int S, hipStream_t stream);
+int l3u_norm_act_bwd_reduce_up_bf16(const float* dskip, long long dskip_nstride,
+                                    const float* dpool, long long dpool_nstride,
+                                    const unsigned char* idx, const l3u_bf16* out,
+                                    long long out_nstride, const l3u_bf16* y2, long long y2_nstride,
+                                    const float* rec2, const l3u_bf16* r, long long r_nstride,
+                                    const float* rec_r, double* part, int N, int C, int D, int H,
+                                    int W, hipStream_t stream);
+int l3u_pw_bwd_tail_up_bf16(const float* dskip, long long dskip_nstride, const float* dpool,
+                            long long dpool_nstride, const unsigned char* idx, const l3u_bf16* out,
+                            long long out_nstride, const l3u_bf16* yr, long long yr_nstride,
+                            const float* rec, const double* tail_part, int npart, int sel,
+                            const l3u_bf16* x, long long x_nstride, const float* w, float* dx,
+                            long long dx_nstride, int accumulate, float* part, int N, int J, int K,
+                            int D, int H, int W, hipStream_t stream);
 int l3u_pw_fwd2_bf16(const l3u_bf16* xa, long long xa_nstride, const float* wa, l3u_bf16* ya,
                      long long ya_nstride, float* stat_a, const l3u_bf16* xb, long long xb_nstride,
                      const float* wb, l3u_bf16* yb, long long yb_nstride, float* stat_b, int N,

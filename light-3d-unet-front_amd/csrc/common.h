@@ -283,6 +283,33 @@ L3U_DEV void block_record2(const l3u_norm_src& a, const l3u_norm_src& b, bool ha
   __syncthreads();
 }
 
+// a / b for 0 <= a < 2^24, b > 0, with inv = 1.f / b: one float multiply and a correction step
+// (the float quotient is within 1 of the exact one) instead of an integer division
+L3U_DEV int fdiv(int a, int b, float inv) {
+  int q = (int)((float)a * inv);
+  const int r = a - q * b;
+  q += r < 0 ? -1 : (r >= b ? 1 : 0);
+  return q;
+}
+
+// MaxPool3d(2, 2) backward folded into a consumer's load (DownBlock, unet3d.py:104): the gradient
+// of the pooled level's input at the x-quad (z, y, x..x+3) (x % 4 == 0, even D / H, W % 4 == 0)
+// is v (the skip-connection gradient quad) plus dpool of the window's argmax (idx = 4dz + 2dy + dx
+// per pooled voxel, l3u_maxpool2_fwd's encoding) -- l3u_maxpool2_bwd's expression, bit for bit.
+// dpp / ipp: the (n, c) planes of dpool [Ho*Wo*Do] and idx; H, W: the fine level's plane.
+L3U_DEV f4_t unpool_add(f4_t v, const float* __restrict__ dpp, const unsigned char* __restrict__ ipp,
+                        int z, int y, int x, int H, int W) {
+  const long long o2 = ((long long)(z >> 1) * (H >> 1) + (y >> 1)) * (W >> 1) + (x >> 1);
+  const f2_t g = *reinterpret_cast<const f2_t*>(dpp + o2);
+  const int id = reinterpret_cast<const unsigned short*>(ipp)[o2 >> 1], i0 = id & 0xff, i1 = id >> 8;
+  const int j = 2 * (z & 1) + (y & 1);
+  v[0] += i0 == 2 * j ? g.x : 0.f;
+  v[1] += i0 == 2 * j + 1 ? g.x : 0.f;
+  v[2] += i1 == 2 * j ? g.y : 0.f;
+  v[3] += i1 == 2 * j + 1 ? g.y : 0.f;
+  return v;
+}
+
 // XCD-aware block remap (guide §5.5 T1, bijective form): blocks that share halo planes / weight
 // tiles are consecutive in the logical order, and consecutive logical ids land on one XCD.
 L3U_DEV int xcd_remap(int bid, int nblocks) {

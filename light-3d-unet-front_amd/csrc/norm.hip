@@ -168,7 +168,9 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     const float* __restrict__ dout, long long dns, const T* __restrict__ out, long long ons,
     const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
     const T* __restrict__ r, long long rns, const float* __restrict__ recr,
-    double* __restrict__ part, int N, int C, int S, const float* __restrict__ dscale = nullptr) {
+    double* __restrict__ part, int N, int C, int S, const float* __restrict__ dscale = nullptr,
+    const float* __restrict__ dpool = nullptr, long long dpns = 0,
+    const unsigned char* __restrict__ pidx = nullptr, int H = 0, int W = 0) {
   __shared__ double red[4];
   const int nc = blockIdx.y, c = nc % C, n = nc / C, nb = gridDim.x;
   const float m2 = rec2[(long long)nc * kRec + 0], rs2 = rec2[(long long)nc * kRec + 1];
@@ -185,7 +187,12 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
   if (VEC) {
     for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += nb * 1024) {
       const f4 ov = ldv4(op + i);
-      const f4 dv = dscale ? dsc * ldv4(dp + i) : ldv4(dp + i);
+      f4 dv = dscale ? dsc * ldv4(dp + i) : ldv4(dp + i);
+      if (dpool) {   // + the MaxPool3d backward of the next level (l3u_maxpool2_bwd folded in)
+        const int HW = H * W, z = fdiv(i, HW, 1.f / HW), rm = i - z * HW, y = fdiv(rm, W, 1.f / W);
+        dv = unpool_add(dv, dpool + (long long)n * dpns + (long long)c * (S / 8),
+                        pidx + (long long)nc * (S / 8), z, y, rm - y * W, H, W);
+      }
       const f4 yv = ldv4(yp + i);
       f4 rv = f4{0.f, 0.f, 0.f, 0.f};
       if (recr) rv = ldv4(rp + i);
@@ -461,12 +468,16 @@ int norm_act_bwd_reduce_impl(const float* dout, long long dout_nstride, const T*
                              long long out_nstride, const T* y2, long long y2_nstride,
                              const float* rec2, const T* r, long long r_nstride,
                              const float* rec_r, double* part, int N, int C, int S,
-                             hipStream_t stream, const float* dscale = nullptr) {
+                             hipStream_t stream, const float* dscale = nullptr,
+                             const float* dpool = nullptr, long long dpns = 0,
+                             const unsigned char* pidx = nullptr, int H = 0, int W = 0) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
   const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
                    y2_nstride % 4 == 0 && r_nstride % 4 == 0;
+  L3U_REQUIRE(dpool == nullptr || (vec && pidx && H % 2 == 0 && W % 4 == 0 && (S / (H * W)) % 2 == 0 &&
+                                   dpns % 2 == 0 && ((uintptr_t)dpool & 7) == 0));
   dim3 grid(elem_blocks(S), N * C);
-  if (vec) hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale);
+  if (vec) hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale, dpool, dpns, pidx, H, W);
   else hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, false>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale);
   L3U_CHECK_LAUNCH();
 }
@@ -541,6 +552,15 @@ L3U_TWIN(l3u_norm_act_bwd_reduce, P_NBR, norm_act_bwd_reduce_impl(dout, dout_nst
 #define P_NBR1(TT) (const float* dz, long long dz_nstride, const float* dscale, const TT* out,        \
     long long out_nstride, const TT* y2, long long y2_nstride, const float* rec2, const TT* r,       \
     long long r_nstride, const float* rec_r, double* part, int N, int C, int S, hipStream_t stream)
+// the block-output gradient = skip gradient + the next level's MaxPool3d backward, folded in
+#define P_NBRU(TT) (const float* dskip, long long dskip_nstride, const float* dpool,                  \
+    long long dpool_nstride, const unsigned char* idx, const TT* out, long long out_nstride,         \
+    const TT* y2, long long y2_nstride, const float* rec2, const TT* r, long long r_nstride,        \
+    const float* rec_r, double* part, int N, int C, int D, int H, int W, hipStream_t stream)
+L3U_TWIN(l3u_norm_act_bwd_reduce_up, P_NBRU, dpool == nullptr ? (int)hipErrorInvalidValue :
+         norm_act_bwd_reduce_impl(dskip, dskip_nstride, bp(out), out_nstride, bp(y2), y2_nstride, rec2,
+         bp(r), r_nstride, rec_r, part, N, C, D * H * W, stream, nullptr, dpool, dpool_nstride, idx, H,
+         W))
 L3U_TWIN(l3u_norm_act_bwd_reduce_r1, P_NBR1, dscale == nullptr ? (int)hipErrorInvalidValue :
          norm_act_bwd_reduce_impl(dz, dz_nstride, bp(out), out_nstride, bp(y2), y2_nstride, rec2, bp(r),
          r_nstride, rec_r, part, N, C, S, stream, dscale))

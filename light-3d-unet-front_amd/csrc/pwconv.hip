@@ -566,7 +566,8 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const T* __restrict__ x, long long xns, const float* __restrict__ w,
     float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part, int N, int J,
     int K, int S, int SCH, int nsc, const T* __restrict__ oin = nullptr, long long oins = 0,
-    int sel = 1, const float* __restrict__ dscale = nullptr) {
+    int sel = 1, const float* __restrict__ dscale = nullptr, const float* __restrict__ dpool = nullptr,
+    long long dpns = 0, const unsigned char* __restrict__ pidx = nullptr, int Hf = 0, int Wf = 0) {
   constexpr int TJ = 16 * NJ, TK = 16 * NK, JR = TJ / 4;
   constexpr int WS = TK + ((16 - TK) % 64 + 64) % 64;   // >= TK, = 16 mod 64
   constexpr int DS = 68;                                // dY tile row stride (floats)
@@ -597,6 +598,11 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
         g[jr] = dscale[j] * ldv4(dyn + sd);
       else
         g[jr] = ldv4(dyn + (long long)j * S + sd);
+      if (PRO == 2 && dpool != nullptr) {   // + the next level's MaxPool3d backward (folded)
+        const int HW = Hf * Wf, z = fdiv(sd, HW, 1.f / HW), rm = sd - z * HW, y = fdiv(rm, Wf, 1.f / Wf);
+        g[jr] = unpool_add(g[jr], dpool + (long long)n * dpns + (long long)j * (S / 8),
+                           pidx + ((long long)n * J + j) * (S / 8), z, y, rm - y * Wf, Hf, Wf);
+      }
     }
   }
   if (PRO == 2) {   // the block output (LeakyReLU mask of the tail)
@@ -1303,8 +1309,11 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
                      const T* yr, long long yr_nstride, const float* rec, const double* tail_part,
                      int npart, int sel, const T* x, long long x_nstride, const float* w, float* dx,
                      long long dx_nstride, int accumulate, float* part, int N, int J, int K, int S,
-                     hipStream_t stream, const float* dscale = nullptr) {
+                     hipStream_t stream, const float* dscale = nullptr, const float* dpool = nullptr,
+                     long long dpns = 0, const unsigned char* pidx = nullptr, int Hf = 0, int Wf = 0) {
   L3U_REQUIRE(N > 0 && l3u_pw_bwd_supported(J, K, S) && !pw_bwd_wide(J));
+  L3U_REQUIRE(dpool == nullptr || (pidx && Hf % 2 == 0 && Wf % 4 == 0 && (S / (Hf * Wf)) % 2 == 0 &&
+                                   dpns % 2 == 0 && ((uintptr_t)dpool & 7) == 0));
   L3U_REQUIRE(dout && out && yr && rec && tail_part && npart > 0 && (sel == 1 || sel == 2));
   L3U_REQUIRE(x && w && dx && part);
   const bool al = al4<float>(dout) && al4<T>(out) && al4<T>(yr) && al4<T>(x) && al4<float>(dx) &&
@@ -1320,7 +1329,7 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
 #define PWBT(A_, B_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2>), grid, block, 0, stream, \
       dout, dout_nstride, yr, yr_nstride, rec, tail_part, npart, x, x_nstride, w, dx, dx_nstride, \
-      accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel, dscale)
+      accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel, dscale, dpool, dpns, pidx, Hf, Wf)
   if (NJ == 1 && NK == 1) PWBT(1, 1);
   else if (NJ == 1 && NK == 2) PWBT(1, 2);
   else if (NJ == 1 && NK == 4) PWBT(1, 4);
@@ -1537,6 +1546,16 @@ L3U_TWIN(l3u_pw_bwd_tail, P_PBT, pw_bwd_tail_impl(dout, dout_nstride, bp(out), o
     const double* tail_part, int npart, int sel, const TT* x, long long x_nstride, const float* w,   \
     float* dx, long long dx_nstride, int accumulate, float* part, int N, int J, int K, int S,        \
     hipStream_t stream)
+// the block-output gradient = skip gradient + the next level's MaxPool3d backward, folded in
+#define P_PBTU(TT) (const float* dskip, long long dskip_nstride, const float* dpool,                  \
+    long long dpool_nstride, const unsigned char* idx, const TT* out, long long out_nstride,         \
+    const TT* yr, long long yr_nstride, const float* rec, const double* tail_part, int npart,         \
+    int sel, const TT* x, long long x_nstride, const float* w, float* dx, long long dx_nstride,     \
+    int accumulate, float* part, int N, int J, int K, int D, int H, int W, hipStream_t stream)
+L3U_TWIN(l3u_pw_bwd_tail_up, P_PBTU, dpool == nullptr ? (int)hipErrorInvalidValue :
+         pw_bwd_tail_impl(dskip, dskip_nstride, bp(out), out_nstride, bp(yr), yr_nstride, rec, tail_part,
+         npart, sel, bp(x), x_nstride, w, dx, dx_nstride, accumulate, part, N, J, K, D * H * W, stream,
+         nullptr, dpool, dpool_nstride, idx, H, W))
 L3U_TWIN(l3u_pw_bwd_tail_r1, P_PBT1, dscale == nullptr ? (int)hipErrorInvalidValue :
          pw_bwd_tail_impl(dz, dz_nstride, bp(out), out_nstride, bp(yr), yr_nstride, rec, tail_part,
          npart, sel, bp(x), x_nstride, w, dx, dx_nstride, accumulate, part, N, J, K, S, stream, dscale))

@@ -81,6 +81,9 @@ _SIGS = {
     "l3u_outconv_bwd_ftl_dz": [P, P, P, I, D, D, D, D, P, P, L, P, P, L, P, P, I, I, I, P],
     "l3u_norm_act_bwd_reduce_r1": [P, L, P, P, L, P, L, P, P, L, P, P, I, I, I, P],
     "l3u_pw_bwd_tail_r1": [P, L, P, P, L, P, L, P, P, I, I, P, L, P, P, L, I, P, I, I, I, I, P],
+    "l3u_norm_act_bwd_reduce_up": [P, L, P, L, P, P, L, P, L, P, P, L, P, P, I, I, I, I, I, P],
+    "l3u_pw_bwd_tail_up": [P, L, P, L, P, P, L, P, L, P, P, I, I, P, L, P, P, L, I, P, I, I, I, I, I, I,
+                           P],
     "l3u_dwpw_supported": [I, I, I, I, I, I],
     "l3u_dwpw_stat_nsb": [I, I, I, I, I],
     "l3u_dwpw_fwd": [P, L, P, P, P, P, P, L, P, P, P, L, P, P, L, I, I, I, I, I, I, P],
@@ -94,7 +97,8 @@ BF16_TWINS = ("l3u_dw3_fwd", "l3u_dw3_bwd", "l3u_pw_fwd", "l3u_pw_fwd2", "l3u_pw
               "l3u_in_bwd_apply", "l3u_maxpool2_fwd", "l3u_outconv_fwd", "l3u_outconv_bwd",
               "l3u_outconv_bwd_ftl", "l3u_box_copy",
               "l3u_front_fwd", "l3u_dwpw_fwd", "l3u_outconv_bwd_dz", "l3u_outconv_bwd_ftl_dz",
-              "l3u_norm_act_bwd_reduce_r1", "l3u_pw_bwd_tail_r1")
+              "l3u_norm_act_bwd_reduce_r1", "l3u_pw_bwd_tail_r1", "l3u_norm_act_bwd_reduce_up",
+              "l3u_pw_bwd_tail_up")
 for _n in BF16_TWINS:
     _SIGS[_n + "_bf16"] = _SIGS[_n]
 # query helpers that return a value instead of an error code

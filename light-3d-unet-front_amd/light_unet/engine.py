@@ -40,15 +40,20 @@ _DWPW_MIN_S = int(os.environ.get("L3U_DWPW_MIN_S", "65536"))
 # of the [N, C, S] output gradient (l3u_outconv_bwd_dz + the _r1 tail kernels); L3U_RANK1=0
 # disables
 _RANK1 = os.environ.get("L3U_RANK1", "1") != "0"
+# the encoder's MaxPool3d backward formed in the loads of the consuming block tail (no
+# l3u_maxpool2_bwd launch, no level-output gradient tensor); L3U_POOLFOLD=0 disables
+_POOLFOLD = os.environ.get("L3U_POOLFOLD", "1") != "0"
 
 
 class V:
     """A strided activation view: channel c of sample n at t[off + n*ns + c*S].  scale (a device
     pointer to C floats): a rank-1 gradient, channel c = scale[c] * the one stored channel."""
-    __slots__ = ("t", "off", "ns", "C", "scale")
+    __slots__ = ("t", "off", "ns", "C", "scale", "pool")
 
-    def __init__(self, t, off, ns, C, scale=None):
+    def __init__(self, t, off, ns, C, scale=None, pool=None):
         self.t, self.off, self.ns, self.C, self.scale = t, off, ns, C, scale
+        # pool = (dpool, idx, (D, H, W)): plus the next level's MaxPool3d backward, formed on load
+        self.pool = pool
 
     @property
     def p(self):
@@ -716,8 +721,15 @@ class UNetEngine:
                             st, dev)
             # d(level output) = maxpool_bwd(dpool) + d(skip) (upper half of dcat at this level)
             dcat = dcats[lvl]
-            dlev = e(N, cprev, S[lvl])
             d, hh, w = dims[lvl]
+            cons = ("init_conv.", "down1.res_block.", "down2.res_block.")[lvl]
+            csv = sv["blk"][cons]
+            if (_POOLFOLD and self.kinds[cons][0][0] == "ds" and d % 2 == 0 and hh % 2 == 0
+                    and w % 4 == 0 and self._tail_fusable(csv, csv["x"].C, cprev, S[lvl])):
+                # the consuming block tail forms it on load (l3u_*_up): no tensor, no launch
+                dout = V(dcat, cprev * S[lvl], 2 * cprev * S[lvl], cprev, pool=(dpool, idx, dims[lvl]))
+                continue
+            dlev = e(N, cprev, S[lvl])
             self._call("l3u_maxpool2_bwd", dpool.data_ptr(), cprev * S[lvl + 1], idx.data_ptr(),
                        dcat.data_ptr() + dcat.element_size() * cprev * S[lvl], 2 * cprev * S[lvl],
                        dlev.data_ptr(),
@@ -761,11 +773,17 @@ class UNetEngine:
                 self._call("l3u_norm_act_bwd_reduce_r1", dout.p, dout.ns, dout.scale, out.p, out.ns,
                            y2.data_ptr(), cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S,
                            st)
+            elif dout.pool is not None:   # skip gradient + the folded MaxPool3d backward
+                dpool, idx, (d, h, w) = dout.pool
+                self._call("l3u_norm_act_bwd_reduce_up", dout.p, dout.ns, dpool.data_ptr(),
+                           cout * (S // 8), idx.data_ptr(), out.p, out.ns, y2.data_ptr(), cout * S,
+                           rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, d, h, w, st)
             else:
                 self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(),
                            cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S, st)
             return pn, nb
-        assert dout.scale is None, "a rank-1 output gradient needs the fused block tail"
+        assert dout.scale is None and dout.pool is None, "a formed-on-load output gradient " \
+            "needs the fused block tail"
         dy2 = self._empty(N, cout, S, device=dev)
         if shortcut:
             dr = self._empty(N, cout, S, device=dev)
@@ -949,6 +967,12 @@ class UNetEngine:
             self._call("l3u_pw_bwd_tail_r1", dout.p, dout.ns, dout.scale, out.p, out.ns, yr.p, yr.ns,
                        rec, A.ptr(pn), ntp, sel, x.p, x.ns, self._w(flat, name), dx.p, dx.ns,
                        accumulate, A.ptr(part), N, J, K, S, st)
+        elif dout.pool is not None:   # skip gradient + the folded MaxPool3d backward
+            dpool, idx, (d, h, w) = dout.pool
+            self._call("l3u_pw_bwd_tail_up", dout.p, dout.ns, dpool.data_ptr(), J * (S // 8),
+                       idx.data_ptr(), out.p, out.ns, yr.p, yr.ns, rec, A.ptr(pn), ntp, sel, x.p,
+                       x.ns, self._w(flat, name), dx.p, dx.ns, accumulate, A.ptr(part), N, J, K, d, h,
+                       w, st)
         else:
             self._call("l3u_pw_bwd_tail", dout.p, dout.ns, out.p, out.ns, yr.p, yr.ns, rec,
                        A.ptr(pn), ntp, sel, x.p, x.ns, self._w(flat, name), dx.p, dx.ns, accumulate,

@@ -296,20 +296,26 @@ def test_trainstep_data_parallel_two_ranks(cuda, tmp_path):
 
 
 
-def test_rank1_output_gradient_bitwise(cuda, golden):
-    """out_conv is rank-1 (unet3d.py:201): handing the last block d(pre-sigmoid) and the out_conv
-    weight (l3u_outconv_bwd_dz + the _r1 tail kernels) gives bitwise the gradients of the
-    materialised [N, C, S] output gradient, for the FocalTversky and the given-dL/dp forms."""
+@pytest.mark.parametrize("switch,fixture", [("_RANK1", "model_b2_32.npz"),
+                                            ("_POOLFOLD", "model_b2_32.npz"),
+                                            ("_POOLFOLD", "model_b1_48.npz")])
+def test_formed_on_load_gradients_bitwise(cuda, golden, switch, fixture):
+    """Output gradients formed on load give bitwise the gradients of the materialised tensors,
+    for the FocalTversky and the given-dL/dp forms of the backward:
+    _RANK1: out_conv is rank-1 (unet3d.py:201), the last block gets d(pre-sigmoid) and the
+    out_conv weight (l3u_outconv_bwd_dz + the _r1 tail kernels);
+    _POOLFOLD: the encoder levels' MaxPool3d backward (unet3d.py:104) inside the consuming block
+    tail's loads (the _up tail kernels; at 48^3 the 48^3 and 24^3 levels)."""
     import light_unet.engine as E
     from light_unet.models.unet3d import Lightweight3DUNet
     from light_unet.train_step import TrainStep
-    z = golden("model_b2_32.npz")
+    z = golden(fixture)
     sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w/")}
     x = torch.from_numpy(z["x"]).to(cuda)
     t = torch.from_numpy(z["target"]).to(cuda)
     res = []
-    for r1 in (True, False):
-        E._RANK1 = r1
+    for on in (True, False):
+        setattr(E, switch, on)
         try:
             m = Lightweight3DUNet(dropout_p=0.1)
             m.load_state_dict(sd)
@@ -324,6 +330,6 @@ def test_rank1_output_gradient_bitwise(cuda, golden):
             torch.cuda.synchronize()
             res.append((g1, gg, ts.loss.clone()))
         finally:
-            E._RANK1 = True
+            setattr(E, switch, True)
     for name, a, b in zip(("ftl grad", "dp grad", "loss"), *res):
         assert torch.equal(a, b), (name, (a - b).abs().max().item())
