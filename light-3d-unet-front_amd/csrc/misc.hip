@@ -142,6 +142,18 @@ L3U_DEV FtlCoef ftl_coef(const double* sums, double alpha, double beta, double g
 // dz = dL/dp * p(1-p); dh[c] = w[c] * dz; part[n*nb + blk][0..C-1] = sum dz*h[c], [C] = sum dz.
 // dL/dp comes from dp, or (dp == NULL) from the FocalTversky closed form A t + B (1 - t) of the
 // global sums (losses.py:30-54), fused so the loss gradient is never written out.
+// The three FocalTversky sums over nb partials {p*t, p, t}: lane-strided fp64 sums, then a fixed
+// DPP wave reduction (every lane gets the totals); one 64-lane wave.  l3u_ftl_reduce and the
+// in-kernel reduce of l3u_outconv_bwd_ftl share it, so both give the same bits.
+L3U_DEV void ftl_lane_sums(const float* __restrict__ part, int nb, double& a, double& b, double& c) {
+  const int l = threadIdx.x & 63;
+  a = b = c = 0.0;
+  for (int i = l; i < nb; i += 64) { a += part[i * 3]; b += part[i * 3 + 1]; c += part[i * 3 + 2]; }
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  c = wave_sum_d(c);
+}
+
 template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     int dz_only, const float* __restrict__ dp, const float* __restrict__ p, const float* __restrict__ t,
@@ -159,16 +171,9 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
       // the FocalTversky sums from the out_conv forward's partials, in ftl_sums_kernel's order
       // (bit-identical to l3u_ftl_reduce): lane-strided fp64 sums, then the 64 lanes in order
       if (threadIdx.x < 64) {
-        const int l = threadIdx.x;
-        double a = 0, b = 0, c = 0;
-        for (int i = l; i < fnp; i += 64) { a += fpart[i * 3]; b += fpart[i * 3 + 1]; c += fpart[i * 3 + 2]; }
-        redd[l] = a; redd[64 + l] = b; redd[128 + l] = c;
-      }
-      __syncthreads();
-      if (threadIdx.x < 3) {
-        double t = 0;
-        for (int i = 0; i < 64; ++i) t += redd[threadIdx.x * 64 + i];
-        fsum[threadIdx.x] = t;
+        double a, b, c;
+        ftl_lane_sums(fpart, fnp, a, b, c);
+        if (threadIdx.x == 0) { fsum[0] = a; fsum[1] = b; fsum[2] = c; }
       }
       __syncthreads();
       sums = fsum;
@@ -269,17 +274,9 @@ __global__ __launch_bounds__(256) void ftl_partials_kernel(const float* __restri
 
 // sums[0..2] (double) = fixed-order sum of the partials
 __global__ void ftl_sums_kernel(const float* __restrict__ part, int nb, double* __restrict__ sums) {
-  __shared__ double red[3][64];
-  const int l = threadIdx.x;   // 64 threads
-  double a = 0, b = 0, c = 0;
-  for (int i = l; i < nb; i += 64) { a += part[i * 3]; b += part[i * 3 + 1]; c += part[i * 3 + 2]; }
-  red[0][l] = a; red[1][l] = b; red[2][l] = c;
-  __syncthreads();
-  if (l < 3) {
-    double s = 0;
-    for (int i = 0; i < 64; ++i) s += red[l][i];
-    sums[l] = s;
-  }
+  double a, b, c;
+  ftl_lane_sums(part, nb, a, b, c);
+  if (threadIdx.x == 0) { sums[0] = a; sums[1] = b; sums[2] = c; }
 }
 
 __global__ void ftl_loss_kernel(const double* __restrict__ sums, double alpha, double beta,
@@ -349,6 +346,9 @@ __global__ __launch_bounds__(256) void adamw_tick_kernel(float* __restrict__ p, 
 __global__ void counter_add_kernel(int* c, int v) { c[0] += v; }
 
 // ---------------------------------------------------------------- segmented partial reduction
+#ifndef L3U_SEG_BATCH
+#define L3U_SEG_BATCH 8   // measured: 8 < 16 < 32 us/step
+#endif
 // item (8 x int64): src_off, count, istride, tstride, len, dst_off, accumulate, unused
 // dst[dst_off + t] (+)= sum_{i<count} src[src_off + i*istride + t*tstride], t < len (<= 256)
 __global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __restrict__ src,
@@ -369,24 +369,25 @@ __global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __res
     const long long base = it[0] + o * it[3];
     const long long stp = is * TP;
     long long i = k;
+    constexpr int B = L3U_SEG_BATCH;   // loads in flight per thread
     if (it[7]) {
       const double* sd = reinterpret_cast<const double*>(src) + base;
-      for (; i + 15 * TP < cnt; i += 16 * TP) {
-        double v[16];
+      for (; i + (B - 1) * TP < cnt; i += B * TP) {
+        double v[B];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = sd[i * is + u * stp];
+        for (int u = 0; u < B; ++u) v[u] = sd[i * is + u * stp];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) s += v[u];
+        for (int u = 0; u < B; ++u) s += v[u];
       }
       for (; i < cnt; i += TP) s += sd[i * is];
     } else {
       const float* sf = src + base;
-      for (; i + 15 * TP < cnt; i += 16 * TP) {
-        float v[16];
+      for (; i + (B - 1) * TP < cnt; i += B * TP) {
+        float v[B];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = sf[i * is + u * stp];
+        for (int u = 0; u < B; ++u) v[u] = sf[i * is + u * stp];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) s += v[u];
+        for (int u = 0; u < B; ++u) s += v[u];
       }
       for (; i < cnt; i += TP) s += sf[i * is];
     }

@@ -305,6 +305,9 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
   }
 }
 
+#ifndef L3U_PWKS_UNROLL
+#define L3U_PWKS_UNROLL 4
+#endif
 // Small-volume variant (per-sample S < 8192: the 12^3 / 6^3 levels): the 4 waves of a workgroup
 // share ONE 64-voxel tile and split the reduction dimension K (k-steps interleaved by wave), then
 // combine through LDS in a fixed order; weights are read straight from L2 (they are tiny and
@@ -334,7 +337,7 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
   for (int m = 0; m < NC; ++m)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[m][q] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
+#pragma unroll L3U_PWKS_UNROLL
   for (int ks = wave; ks < ksteps; ks += 4) {
     const int kk = 4 * ks + lk;
     const f4 a = load_x4<VEC, XM == 2>(xn, kk, K, s, S, S, Hq, Wq);
