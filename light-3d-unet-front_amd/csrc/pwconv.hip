@@ -579,7 +579,9 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   __shared__ __attribute__((aligned(16))) float w_l[TJ * WS];
   __shared__ __attribute__((aligned(16))) float coef[PRO ? TJ * 8 : 1];
   __shared__ double psum[PRO ? TJ * PS * 2 : 1];
-  __shared__ __attribute__((aligned(16))) float dyt[8][TJ * DS];
+  // the waves' dY tiles, sized by the launch for the block's wave count (a static [8] array held
+  // 70 KB at TJ = 32 for 4-wave blocks: two workgroups per CU instead of four)
+  extern __shared__ __attribute__((aligned(16))) float dyt_lds[];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const int nthr = blockDim.x, nwv = nthr >> 6;         // one sweep: SCH == 64 * nwv
   const int sc = blockIdx.x % nsc, n = blockIdx.x / nsc, k0 = blockIdx.y * TK;
@@ -689,7 +691,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       for (int q = 0; q < 4; ++q) g[jr][q] = ok ? f * (g[jr][q] - M1 - (yv[jr][q] - mu) * rs * M2) : 0.f;
     }
   }
-  float* tile = dyt[wave];
+  float* tile = dyt_lds + (size_t)wave * TJ * DS;
 #pragma unroll
   for (int jr = 0; jr < JR; ++jr)
     *reinterpret_cast<f4*>(tile + (4 * jr + lk) * DS + 4 * lr) = g[jr];
@@ -744,7 +746,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   // 6. fixed-order cross-wave reduction (reuses the dY tiles): every wave parks its partial
   // tile, wave 0 adds them in wave order
   __syncthreads();
-  float* red = &dyt[0][0];
+  float* red = dyt_lds;
 #pragma unroll
   for (int a = 0; a < NJ; ++a)
 #pragma unroll
@@ -1330,7 +1332,8 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
-#define PWBT(A_, B_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2>), grid, block, 0, stream, \
+  const size_t dlds = (size_t)nwv * 16 * NJ * 68 * sizeof(float);   // dY tiles (DS = 68)
+#define PWBT(A_, B_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2>), grid, block, dlds, stream, \
       dout, dout_nstride, yr, yr_nstride, rec, tail_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel, dscale, dpool, dpns, pidx, Hf, Wf)
   if (NJ == 1 && NK == 1) PWBT(1, 1);
@@ -1372,10 +1375,11 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);   // one sweep of the chunk per workgroup
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
-#define PWBF(A_, B_) do { if (y) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 1>), grid, block, 0, \
+  const size_t dlds = (size_t)nwv * 16 * NJ * 68 * sizeof(float);   // dY tiles (DS = 68)
+#define PWBF(A_, B_) do { if (y) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 1>), grid, block, dlds, \
       stream, dy, dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, N, J, K, S, SCH, nsc); \
-    else hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 0>), grid, block, 0, stream, dy, dy_nstride, \
+    else hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 0>), grid, block, dlds, stream, dy, dy_nstride, \
       y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, accumulate, part, N, J, K, \
       S, SCH, nsc); } while (0)
   if (NJ == 1 && NK == 1) PWBF(1, 1);
