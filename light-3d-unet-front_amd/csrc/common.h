@@ -106,6 +106,14 @@ L3U_DEV double dpp_d(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xf, 0xf, false);
   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
+// fp64 sum over the 16 lanes of a DPP row (fixed order: deterministic), in every lane
+L3U_DEV double row_sum16d(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  return v;
+}
 L3U_DEV double swap_sum_d(double v, bool row16) {
   const unsigned long long u = __double_as_longlong(v);
   const unsigned lo = (unsigned)(u & 0xffffffffu), hi = (unsigned)(u >> 32);

@@ -44,15 +44,6 @@ L3U_DEV f4 widen(b4_t v) { return __builtin_convertvector(v, f4); }
 template <typename T>
 L3U_DEV void pin(T& v) { asm volatile("" : "+v"(v)); }
 
-// fp64 sum over the 16 lanes of a DPP row (fixed order: deterministic), in every lane
-L3U_DEV double row_sum16d(double v) {
-  v += dpp_d<0xB1>(v);
-  v += dpp_d<0x4E>(v);
-  v += dpp_d<0x141>(v);
-  v += dpp_d<0x140>(v);
-  return v;
-}
-
 // Wave-local staging map of one channel's (RB+2) x WQ quad strip image (<= 128 quads): lane l
 // stages quads l and l + 64; rows outside the volume are never written (stay zero).
 struct WMap {
