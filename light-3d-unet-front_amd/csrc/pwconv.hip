@@ -1163,6 +1163,9 @@ int pw_sch(int S) {
 // still launch enough workgroups (>= 4 per CU at one sample)
 int pw_nsw(int NC) { const int n = 4 / NC; return n < L3U_PW_NSW_MAX ? n : L3U_PW_NSW_MAX; }
 
+#ifndef L3U_PW_MIN_BLOCKS
+#define L3U_PW_MIN_BLOCKS 1024   // measured: 0 / 512 / 1024 within 2 us, 1024 best
+#endif
 #ifndef L3U_PW_KS_MIN_K
 #define L3U_PW_KS_MIN_K 0
 #endif
@@ -1214,7 +1217,11 @@ int pw_launch(const T* x, long long x_nstride, const float* w, int w_layout, con
 #undef PWK
     L3U_CHECK_LAUNCH();
   }
-  const int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
+  int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
+  // narrower output tiles while the grid is short of L3U_PW_MIN_BLOCKS workgroups (the 24^3 ->
+  // 48^3 ConvTranspose3d: 432 -> 864)
+  while (CO_BLK > 16 && (long long)((S + 255) / 256) * ((Nout + CO_BLK - 1) / CO_BLK) * NZ <
+                        L3U_PW_MIN_BLOCKS) CO_BLK >>= 1;
   const int NC = CO_BLK / 16, NSW = pw_nsw(NC), TSB = 256 * NSW;
   const int nsb = (S + TSB - 1) / TSB;
   const int WS = (CO_BLK % 32 == 16) ? CO_BLK : CO_BLK + 16;
