@@ -358,23 +358,44 @@ def cpu_baseline(args, enc):
     x = torch.from_numpy(rng.random((bs, 1, size, size, size), dtype=np.float32))
     t = torch.from_numpy((rng.random((bs, 1, size, size, size)) > 0.97).astype(np.float32))
 
+    # Dropout3d(p) after norm1 of every ResidualBlock, as the GPU step runs it (unet3d.py:84-88):
+    # one Bernoulli(1-p) keep flag per (sample, channel), fresh every step
+    drop_p = args.dropout
+    blocks = [k[:-len("norm1.weight")] for k in sd if k.endswith("norm1.weight")]
+
     def step():
-        out = U.unet_forward(sd, x)
+        masks = {b: (torch.rand(bs, sd[b + "norm1.weight"].shape[0], generator=g) >= drop_p).float()
+                 for b in blocks} if drop_p > 0 else None
+        out = U.unet_forward(sd, x, drop_masks=masks, drop_p=drop_p)
         loss = U.focal_tversky(out, t)
         opt.zero_grad()
         loss.backward()
         opt.step()
 
-    step()
+    warm = 3
+    for _ in range(warm):
+        step()
     t0 = time.perf_counter()
     for _ in range(args.cpu_steps):
         step()
     dt = time.perf_counter() - t0
     return {"value": round(args.cpu_steps * bs / dt, 3), "unit": "patches/s",
-            "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{args.cpu_steps} train steps (fwd+FocalTversky+bwd+AdamW, dropout 0) of "
-                      f"bs={bs} {size}^3 fp32 after 1 warm-up, oracle/unet_oracle.py (aten CPU)",
+            "cores": torch.get_num_threads(), "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"{args.cpu_steps} train steps (fwd+FocalTversky+bwd+AdamW, Dropout3d "
+                      f"p={drop_p}) of bs={bs} {size}^3 fp32 after {warm} warm-ups, "
+                      f"oracle/unet_oracle.py (aten CPU)",
             "ms_per_step": round(1000 * dt / args.cpu_steps, 1)}
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def fwd_ms_per_patch(model, bs, size, device, iters=20):

@@ -155,3 +155,18 @@ def test_window_positions_edge_cases():
     assert S.window_positions(50, 48, 24) == [0, 2]
     with pytest.raises(ValueError):
         S.sliding_window(np.zeros((4, 4)), lambda a: a)
+
+
+def test_cpu_baseline_equivalence_recorded():
+    """the oracle step (bench.py's cpu_baseline leg) was timed against the
+    reference's own model on the same cores and inputs (tests/fixtures/make_cpu_ratio.py);
+    the record holds outputs within 1e-3 and a time ratio near 1, so the CPU baseline is the
+    reference's speed, not a slower restatement's."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "fixtures", "cpu_ratio.json")) as f:
+        rec = json.load(f)
+    assert rec["parity_dropout0"]["max_abs_out"] <= 1e-3
+    assert rec["parity_dropout0"]["grad_rel_l2"] <= 1e-3
+    assert 0.8 <= rec["ratio_oracle_over_reference"] <= 1.25
+    assert "p=0.1" in rec["workload"] and rec["cpu_model"]
