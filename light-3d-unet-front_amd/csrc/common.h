@@ -183,6 +183,9 @@ L3U_DEV unsigned long long splitmix64(unsigned long long z) {
   return z ^ (z >> 31);
 }
 
+L3U_DEV void record_from(const l3u_norm_src& s, int n, int c, int C, float cn, float mu, float m2,
+                         float r[kRec]);
+
 // Merge the (count, mean, M2) partials of one (n, c) with the 64 lanes of the calling wave
 // (lane-strided Chan merges, then a fixed xor tree) and build the 8-float record.  Every caller
 // for the same (n, c) gets bit-identical values.  Must be called by a full wave; returns the
@@ -216,6 +219,13 @@ L3U_DEV void finalize_record(const l3u_norm_src& s, int n, int c, int C, float r
       chan_merge(cn, mu, m2, cb, mb, vb);
     }
   }
+  record_from(s, n, c, C, cn, mu, m2, r);
+}
+
+// The record of (n, c) from its merged (count, mean, M2): rstd, the affine parameters and the
+// Dropout3d keep scale of (step, layer, n*C + c).
+L3U_DEV void record_from(const l3u_norm_src& s, int n, int c, int C, float cn, float mu, float m2,
+                         float r[kRec]) {
   const float var = cn > 0.f ? m2 / cn : 0.f;
   const float rstd = 1.0f / sqrtf(var + kEps);
   const float g = s.gamma ? s.gamma[c] : 1.f, b = s.beta ? s.beta[c] : 0.f;

@@ -71,7 +71,8 @@ def test_bf16_twins_mirror_fp32_entry_points():
             if x != y:
                 assert x.replace("float*", "l3u_bf16*") == y, (t, x, y)
                 nb += 1
-        assert nb >= 1, t
+        # the args-struct entry points (void* activations) differ only in the name
+        assert nb >= 1 or "_args*" in a32[0], t
 
 
 def test_host_queries_without_gpu():

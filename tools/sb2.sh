@@ -1,0 +1,8 @@
+#!/bin/bash
+# sblock tests, then the step launch list and the A/B against L3U_SBLOCK=0
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_sblock_gpu.py -q -x --timeout 120 --timeout-method thread -rf > gpurun_out/sb_test.log 2>&1
+rc=$?; echo "sblock tests rc=$rc"; tail -15 gpurun_out/sb_test.log
+[ $rc -eq 0 ] || exit $rc
+bash tools/sbp.sh ${1:-sbp}
