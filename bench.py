@@ -295,13 +295,18 @@ def gemm_mfma_evidence(top=5):
     (tools/pmc_step.sh + tools/pmc_gemm.sh -> tools/pmc_launch_json.py -> profiles/*_pmc_step.json)."""
     import glob
     files = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r2*_pmc_step.json")))]
-    if not files:
+    items, src = [], None
+    for fn in reversed(files):   # the newest pass that carries the MFMA counters
+        with open(fn) as f:
+            rec = json.load(f)
+        items = [i for i in rec.get("items", []) if "mfma_util" in i and i.get("mfma_busy_cycles", 0) > 0]
+        if items:
+            src = fn
+            break
+    if not items:
         return None
-    with open(files[-1]) as f:
-        rec = json.load(f)
-    items = [i for i in rec["items"] if "mfma_util" in i and i["mfma_busy_cycles"] > 0]
     items.sort(key=lambda i: -i["pmc_dur_us"])
-    return {"source": os.path.relpath(files[-1], ROOT),
+    return {"source": os.path.relpath(src, ROOT),
             "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)",
             "ceiling_note": "fp32 MFMA at the HBM roofline: 5.5 flop/B x 8 TB/s = 44 TFLOP/s = 0.28 of "
                             "the 157 TFLOP/s fp32 matrix peak",
