@@ -954,14 +954,14 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
 // the A operand.  KW waves split the co range (interleaved co quads) and combine through LDS in
 // wave order (deterministic).  Replaces the gathered-GEMM form for the model's decoder shapes.
 template <int NC, int KW>
-__global__ __launch_bounds__(64 * KW) void convt_dx_pair_kernel(
+L3U_DEV void convt_dx_pair_body(int bx, int by, int bz,
     const float* __restrict__ dy, long long dyns, const float* __restrict__ w, float* __restrict__ dx,
     long long dxns, int Ci, int Co, int D, int H, int W) {
   __shared__ __attribute__((aligned(16))) float red[KW][NC * 2 * 4][64];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const int WP = W >> 1, P = D * H * WP;
   const long long S = (long long)D * H * W, S8 = 8 * S;
-  const int q = blockIdx.x * 16 + lr, ci0 = blockIdx.y * 16 * NC, n = blockIdx.z;
+  const int q = bx * 16 + lr, ci0 = by * 16 * NC, n = bz;
   const bool ok = q < P;
   const int qq = ok ? q : 0;
   const int xp = qq % WP, t = qq / WP, y = t % H, z = t / H;
@@ -1035,6 +1035,13 @@ __global__ __launch_bounds__(64 * KW) void convt_dx_pair_kernel(
     }
 }
 
+template <int NC, int KW>
+__global__ __launch_bounds__(64 * KW) void convt_dx_pair_kernel(
+    const float* __restrict__ dy, long long dyns, const float* __restrict__ w, float* __restrict__ dx,
+    long long dxns, int Ci, int Co, int D, int H, int W) {
+  convt_dx_pair_body<NC, KW>(blockIdx.x, blockIdx.y, blockIdx.z, dy, dyns, w, dx, dxns, Ci, Co, D, H, W);
+}
+
 // ConvTranspose3d(k2, s2) weight and bias gradients in the same x-pair layout (even W):
 //   part[chunk][ci][co*8 + 4a+2b+c] = sum_{s in chunk} x[ci][s] dY[co][2z+a][2y+b][2x+c]
 // The MFMA k-dimension is the voxel.  Lane (lr, lk) loads the float4 of up-sampled row
@@ -1045,7 +1052,7 @@ __global__ __launch_bounds__(64 * KW) void convt_dx_pair_kernel(
 // Bias partial bsum[chunk][co] = sum of every dY value of co over the chunk's up-sampled voxels.
 // Same partial layout and chunking as pw_bwd_weight_kernel's GATHER form.
 template <typename T, int NJ, int NG>
-__global__ __launch_bounds__(256) void convt_dw_pair_kernel(
+L3U_DEV void convt_dw_pair_body(int bx, int by,
     const T* __restrict__ x, long long xns, const float* __restrict__ dy, long long dyns,
     float* __restrict__ part, float* __restrict__ bsum, int Ci, int Co, int D, int H, int W,
     int SCH, int nsc) {
@@ -1054,9 +1061,9 @@ __global__ __launch_bounds__(256) void convt_dw_pair_kernel(
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
   const int WP = W >> 1;
   const long long S = (long long)D * H * W, S8 = 8 * S;
-  const int sc = blockIdx.x % nsc, n = blockIdx.x / nsc;
+  const int sc = bx % nsc, n = bx / nsc;
   const int ngb = (Co + 4 * NG - 1) / (4 * NG);
-  const int ci0 = (blockIdx.y / ngb) * 16 * NJ, g0 = (blockIdx.y % ngb) * NG;
+  const int ci0 = (by / ngb) * 16 * NJ, g0 = (by % ngb) * NG;
   const int p_lo = sc * (SCH / 2), p_hi = min((int)(S / 2), p_lo + SCH / 2);
   const int ab = lr & 3, a_ = ab >> 1, b_ = ab & 1;
   const float* dyn = dy + (long long)n * dyns;
@@ -1124,7 +1131,7 @@ __global__ __launch_bounds__(256) void convt_dw_pair_kernel(
   __syncthreads();
   if (wave == 0) {
     const int K = Co * 8;
-    float* o = part + (long long)blockIdx.x * Ci * K;
+    float* o = part + (long long)bx * Ci * K;
 #pragma unroll
     for (int m = 0; m < NJ; ++m)
 #pragma unroll
@@ -1141,8 +1148,37 @@ __global__ __launch_bounds__(256) void convt_dw_pair_kernel(
     if (bsum != nullptr && ci0 == 0 && l < NG * 4) {
       const int co = 4 * g0 + l;
       if (co < Co)
-        bsum[(long long)blockIdx.x * Co + co] = ((bred[0][l] + bred[1][l]) + bred[2][l]) + bred[3][l];
+        bsum[(long long)bx * Co + co] = ((bred[0][l] + bred[1][l]) + bred[2][l]) + bred[3][l];
     }
+  }
+}
+
+template <typename T, int NJ, int NG>
+__global__ __launch_bounds__(256) void convt_dw_pair_kernel(
+    const T* __restrict__ x, long long xns, const float* __restrict__ dy, long long dyns,
+    float* __restrict__ part, float* __restrict__ bsum, int Ci, int Co, int D, int H, int W,
+    int SCH, int nsc) {
+  convt_dw_pair_body<T, NJ, NG>(blockIdx.x, blockIdx.y, x, xns, dy, dyns, part, bsum, Ci, Co, D, H, W,
+                                SCH, nsc);
+}
+
+// Both pair-layout ConvTranspose3d backward halves in ONE launch (the 6^3 decoder input, where
+// each is a ~10 us latency-bound launch): workgroups [0, nA) take the data gradient (grid gx x
+// gy x gz of convt_dx_pair_kernel<NC, 4>), the rest the weight / bias partials (grid gwx x gwy
+// of convt_dw_pair_kernel).  The two read the same dY and are independent; per-workgroup work and
+// results are those of the two launches, bit for bit.
+template <typename T, int NC, int NJ, int NG>
+__global__ __launch_bounds__(256) void convt_pair_bwd_kernel(
+    const float* __restrict__ dy, long long dyns, const float* __restrict__ w, float* __restrict__ dx,
+    long long dxns, const T* __restrict__ x, long long xns, float* __restrict__ part,
+    float* __restrict__ bsum, int Ci, int Co, int D, int H, int W, int SCH, int nsc, int gx, int gy,
+    int nA, int gwx) {
+  const int b = blockIdx.x;
+  if (b < nA) {
+    convt_dx_pair_body<NC, 4>(b % gx, (b / gx) % gy, b / (gx * gy), dy, dyns, w, dx, dxns, Ci, Co, D, H, W);
+  } else {
+    const int k = b - nA;
+    convt_dw_pair_body<T, NJ, NG>(k % gwx, k / gwx, x, xns, dy, dyns, part, bsum, Ci, Co, D, H, W, SCH, nsc);
   }
 }
 
@@ -1290,6 +1326,9 @@ int pw_bwd_weight_launch(const TD* dy, long long dy_nstride, const TX* x, long l
 #ifndef L3U_CONVT_PAIR
 #define L3U_CONVT_PAIR 1   // ConvTranspose3d backward in the x-pair layout (even W) ...
 #endif
+#ifndef L3U_CONVT_PAIR1
+#define L3U_CONVT_PAIR1 1   // both pair-layout halves as one launch (convt_pair_bwd_kernel)
+#endif
 #ifndef L3U_CONVT_PAIR_MAX_S
 #define L3U_CONVT_PAIR_MAX_S 8192   // ... for input volumes up to this size (rocprof r2s: at 6^3
 #endif                              // 35.4 -> 19.8 us; at 24^3 34.3 -> 37.1 us, so not there)
@@ -1427,6 +1466,36 @@ int convt_bwd_impl(const float* dy, long long dy_nstride, const T* x, long long 
                    int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && Ci > 0 && Co > 0 && D > 0 && H > 0 && W > 0);
   const int S = D * H * W;
+  const bool pdx = L3U_CONVT_PAIR && S <= L3U_CONVT_PAIR_MAX_S && W % 2 == 0 && dy_nstride % 4 == 0 &&
+                   dx_nstride % 2 == 0 && al4<float>(dy) && ((uintptr_t)dx & 7) == 0;
+  const bool pdw = L3U_CONVT_PAIR && S <= L3U_CONVT_PAIR_MAX_S && W % 2 == 0 && x_nstride % 2 == 0 &&
+                   dy_nstride % 4 == 0 && al4<float>(dy) && ((uintptr_t)x & (2 * sizeof(T) - 1)) == 0;
+  if (L3U_CONVT_PAIR1 && pdx && pdw && Co >= 16) {
+    // one launch for both halves (same tile choices as the two launches below)
+    const int P = D * H * (W / 2);
+    const int NC = Ci % 32 == 0 && (long long)N * ((P + 15) / 16) * (Ci / 32) >= 256 ? 2 : 1;
+    const int gx = (P + 15) / 16, gy = (Ci + 16 * NC - 1) / (16 * NC), nA = gx * gy * N;
+    const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
+    int NJ = Ci % 32 == 0 ? 2 : 1, NG = Co % 16 == 0 ? 4 : (Co % 8 == 0 ? 2 : 1);
+    for (;;) {
+      const long long nb = (long long)N * nsc * ((Ci + 16 * NJ - 1) / (16 * NJ)) *
+                           ((Co + 4 * NG - 1) / (4 * NG));
+      if (nb >= L3U_CTW_MIN_BLOCKS || (NJ == 1 && NG == 1)) break;
+      if (NG > 1) NG >>= 1; else NJ >>= 1;
+    }
+    const int gwx = N * nsc, gwy = ((Ci + 16 * NJ - 1) / (16 * NJ)) * ((Co + 4 * NG - 1) / (4 * NG));
+    dim3 grid(nA + gwx * gwy), block(256);
+#define CPB(NC_, NJ_, NG_) hipLaunchKernelGGL((convt_pair_bwd_kernel<T, NC_, NJ_, NG_>), grid, block, 0, \
+      stream, dy, dy_nstride, w, dx, dx_nstride, x, x_nstride, wpart, bpart, Ci, Co, D, H, W, SCH, nsc, \
+      gx, gy, nA, gwx)
+#define CPB_G(NC_, NJ_) do { if (NG == 4) CPB(NC_, NJ_, 4); else if (NG == 2) CPB(NC_, NJ_, 2); \
+                             else CPB(NC_, NJ_, 1); } while (0)
+    if (NC == 2) { if (NJ == 2) CPB_G(2, 2); else CPB_G(2, 1); }
+    else { if (NJ == 2) CPB_G(1, 2); else CPB_G(1, 1); }
+#undef CPB_G
+#undef CPB
+    L3U_CHECK_LAUNCH();
+  }
   // dX[ci][s] = sum_{co,abc} w[ci][co*8+abc] dY[co][up(s, abc)] (all gradients: fp32): in the
   // x-pair layout for even W (8-byte aligned rows), else the GEMM with X gathered
   int rc;
