@@ -311,6 +311,7 @@ __global__ __launch_bounds__(256) void ftl_bwd_kernel(
 // One launch: the update, and the step counter(s) advanced by the LAST workgroup to finish (ticket
 // order): every workgroup has read *step by the time it takes its ticket, so the increment
 // cannot race a read, and the separate one-thread launch disappears.  The ticket is reset.
+template <bool VEC>
 __global__ __launch_bounds__(256) void adamw_tick_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                          float* __restrict__ m, float* __restrict__ v,
                                                          long long numel, const float* __restrict__ lr,
@@ -323,17 +324,44 @@ __global__ __launch_bounds__(256) void adamw_tick_kernel(float* __restrict__ p, 
   const float bc2s = sqrtf(1.f - powf(beta2, (float)t));
   const float step_size = lrv / bc1;
   const float decay = 1.f - lrv * wd;
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < numel; i += (long long)gridDim.x * 256) {
-    const float gv = g[i] * gscale;
-    float pv = p[i] * decay;
-    float mv = m[i];
+  auto upd = [&](float& pv, float gv, float& mv, float& vv) {
+    gv *= gscale;
+    pv *= decay;
     mv = mv + (1.f - beta1) * (gv - mv);                 // exp_avg.lerp_(grad, 1 - beta1)
-    const float vv = v[i] * beta2 + (1.f - beta2) * gv * gv;
+    vv = vv * beta2 + (1.f - beta2) * gv * gv;
     const float denom = sqrtf(vv) / bc2s + eps;
     pv = pv - step_size * (mv / denom);
-    p[i] = pv;
-    m[i] = mv;
-    v[i] = vv;
+  };
+  const long long st = (long long)gridDim.x * 256;
+  if (VEC) {
+    // float4 per thread: the four arrays' loads of a thread are one memory round trip (the scalar
+    // grid-stride loop issued four dependent rounds); same per-element arithmetic
+    const long long n4 = numel >> 2;
+    for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += st) {
+      f4 pv = ldv4(p + 4 * i), mv = ldv4(m + 4 * i), vv = ldv4(v + 4 * i);
+      const f4 gv = ldv4(g + 4 * i);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float a = pv[q], b = mv[q], c = vv[q];
+        upd(a, gv[q], b, c);
+        pv[q] = a; mv[q] = b; vv[q] = c;
+      }
+      stv4(p + 4 * i, pv);
+      stv4(m + 4 * i, mv);
+      stv4(v + 4 * i, vv);
+    }
+    const long long i = 4 * n4 + threadIdx.x;
+    if (blockIdx.x == 0 && i < numel) {
+      float pv = p[i], mv = m[i], vv = v[i];
+      upd(pv, g[i], mv, vv);
+      p[i] = pv; m[i] = mv; v[i] = vv;
+    }
+  } else {
+    for (long long i = blockIdx.x * 256ll + threadIdx.x; i < numel; i += st) {
+      float pv = p[i], mv = m[i], vv = v[i];
+      upd(pv, g[i], mv, vv);
+      p[i] = pv; m[i] = mv; v[i] = vv;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0 && atomicAdd(ticket, 1) == (int)gridDim.x - 1) {
@@ -787,9 +815,15 @@ int l3u_adamw_tick(float* p, const float* g, float* m, float* v, long long numel
                    float beta1, float beta2, float eps, float weight_decay, int* step,
                    float grad_scale, int* ticket, int* counter2, hipStream_t stream) {
   L3U_REQUIRE(numel > 0 && step && ticket);
-  hipLaunchKernelGGL(adamw_tick_kernel, dim3(grid_for(numel, 1024, 1024)), dim3(256), 0, stream, p, g,
-                     m, v, numel, lr, beta1, beta2, eps, weight_decay, step, grad_scale, ticket,
-                     counter2);
+  const bool vec = ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0;
+  if (vec)
+    hipLaunchKernelGGL(adamw_tick_kernel<true>, dim3(grid_for(numel, 1024, 1024)), dim3(256), 0, stream,
+                       p, g, m, v, numel, lr, beta1, beta2, eps, weight_decay, step, grad_scale, ticket,
+                       counter2);
+  else
+    hipLaunchKernelGGL(adamw_tick_kernel<false>, dim3(grid_for(numel, 1024, 1024)), dim3(256), 0, stream,
+                       p, g, m, v, numel, lr, beta1, beta2, eps, weight_decay, step, grad_scale, ticket,
+                       counter2);
   L3U_CHECK_LAUNCH();
 }
 
