@@ -148,7 +148,22 @@ L3U_DEV FtlCoef ftl_coef(const double* sums, double alpha, double beta, double g
 L3U_DEV void ftl_lane_sums(const float* __restrict__ part, int nb, double& a, double& b, double& c) {
   const int l = threadIdx.x & 63;
   a = b = c = 0.0;
-  for (int i = l; i < nb; i += 64) { a += part[i * 3]; b += part[i * 3 + 1]; c += part[i * 3 + 2]; }
+  // 8 strided partials in flight per lane (one L2 round trip instead of eight), added in the same
+  // i order; out-of-range slots add +0.0, which leaves a (never -0.0) unchanged: same bits
+  constexpr int B = 8;
+  for (int i = l; i < nb; i += B * 64) {
+    float va[B], vb[B], vc[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int j = i + u * 64;
+      const bool ok = j < nb;
+      va[u] = ok ? part[j * 3] : 0.f;
+      vb[u] = ok ? part[j * 3 + 1] : 0.f;
+      vc[u] = ok ? part[j * 3 + 2] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < B; ++u) { a += va[u]; b += vb[u]; c += vc[u]; }
+  }
   a = wave_sum_d(a);
   b = wave_sum_d(b);
   c = wave_sum_d(c);
@@ -162,41 +177,51 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     const float* __restrict__ w, float* __restrict__ dh, long long dhns,
     double* __restrict__ part, float* __restrict__ loss, int C, int S,
     const float* __restrict__ fpart = nullptr, int fnp = 0) {
-  extern __shared__ double redd[];   // [4][C+1]; fpart: [3][64]
-  __shared__ float coef[2];
-  __shared__ double fsum[3];
+  extern __shared__ double redd[];   // [4][C+1]
   const int n = blockIdx.y, nb = gridDim.x;
-  if (dp == nullptr) {
-    if (fpart != nullptr) {
-      // the FocalTversky sums from the out_conv forward's partials, in ftl_sums_kernel's order
-      // (bit-identical to l3u_ftl_reduce): lane-strided fp64 sums, then the 64 lanes in order
-      if (threadIdx.x < 64) {
-        double a, b, c;
-        ftl_lane_sums(fpart, fnp, a, b, c);
-        if (threadIdx.x == 0) { fsum[0] = a; fsum[1] = b; fsum[2] = c; }
-      }
-      __syncthreads();
-      sums = fsum;
-    }
-    if (threadIdx.x == 0) {
-      const FtlCoef r = ftl_coef(sums, alpha, beta, gamma, smooth);
-      const double s = gscale ? (double)gscale[0] : 1.0;
-      coef[0] = (float)(r.A * s);
-      coef[1] = (float)(r.B * s);
-      if (loss && blockIdx.x == 0 && blockIdx.y == 0) loss[0] = (float)r.loss;
-    }
-    __syncthreads();
-  }
   const T* hp = h + (long long)n * hns;
   float* dhp = dh + (long long)n * dhns;
   const long long o = (long long)n * S;
   const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  // VEC: the streamed operands (p, t or dp, the C channels of h) are requested first, so their
+  // latency overlaps the FocalTversky prologue below
+  f4 pv4 = {0.f, 0.f, 0.f, 0.f}, gv4 = {0.f, 0.f, 0.f, 0.f};
+  f4 hv[VEC ? 32 : 1];
+  if (VEC) {
+    if (i0 < S) {
+      pv4 = ldv4(p + o + i0);
+      gv4 = ldv4((dp ? dp : t) + o + i0);
+    }
+#pragma unroll
+    for (int c = 0; c < 32; ++c) {
+      hv[c] = f4{0.f, 0.f, 0.f, 0.f};
+      if (c < C && i0 < S) hv[c] = ldv4(hp + (long long)c * S + i0);
+    }
+  }
+  float cA = 0.f, cB = 0.f;
+  if (dp == nullptr) {
+    // every wave forms the coefficients itself (no LDS hand-off, no barrier).  fpart: the
+    // FocalTversky sums from the out_conv forward's partials in ftl_sums_kernel's order
+    // (bit-identical to l3u_ftl_reduce; wave_sum_d leaves the same total in every lane)
+    double sm[3];
+    if (fpart != nullptr) {
+      ftl_lane_sums(fpart, fnp, sm[0], sm[1], sm[2]);
+    } else {
+      sm[0] = sums[0]; sm[1] = sums[1]; sm[2] = sums[2];
+    }
+    const FtlCoef r = ftl_coef(sm, alpha, beta, gamma, smooth);
+    const double s = gscale ? (double)gscale[0] : 1.0;
+    cA = (float)(r.A * s);
+    cB = (float)(r.B * s);
+    if (loss && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) loss[0] = (float)r.loss;
+  }
   f4 dz = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     if (i0 + q < S) {
-      const float pv = p[o + i0 + q];
-      const float g = dp ? dp[o + i0 + q] : fmaf(coef[0] - coef[1], t[o + i0 + q], coef[1]);
+      const float pv = VEC ? pv4[q] : p[o + i0 + q];
+      const float gs = VEC ? gv4[q] : (dp ? dp[o + i0 + q] : t[o + i0 + q]);
+      const float g = dp ? gs : fmaf(cA - cB, gs, cB);
       dz[q] = g * pv * (1.f - pv);
     }
   }
@@ -218,8 +243,8 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     if (c < C) {
       if (VEC) {
         if (i0 < S) {
-          const f4 hv = ldv4(hp + (long long)c * S + i0);
-          acc[c] = fmaf(dz[0], hv[0], fmaf(dz[1], hv[1], fmaf(dz[2], hv[2], dz[3] * hv[3])));
+          const f4 hc = hv[VEC ? c : 0];
+          acc[c] = fmaf(dz[0], hc[0], fmaf(dz[1], hc[1], fmaf(dz[2], hc[2], dz[3] * hc[3])));
           if (!dz_only) stv4(dhp + (long long)c * S + i0, w[c] * dz);
         }
       } else {
@@ -676,8 +701,7 @@ int outconv_bwd_impl(const float* dp, const float* p, const float* t, const doub
   L3U_REQUIRE(dp != nullptr || (t != nullptr && (sums != nullptr || (fpart != nullptr && fnp > 0))));
   const bool vec = S % 4 == 0 && h_nstride % 4 == 0 && dh_nstride % 4 == 0;
   dim3 grid((S + 1023) / 1024, N);
-  size_t lds = 4 * (C + 1) * sizeof(double);
-  if (fpart != nullptr && lds < 3 * 64 * sizeof(double)) lds = 3 * 64 * sizeof(double);
+  const size_t lds = 4 * (C + 1) * sizeof(double);
   if (vec) hipLaunchKernelGGL((outconv_bwd_kernel<T, true>), grid, dim3(256), lds, stream, dz_only, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S, fpart, fnp);
   else hipLaunchKernelGGL((outconv_bwd_kernel<T, false>), grid, dim3(256), lds, stream, dz_only, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S, fpart, fnp);
   L3U_CHECK_LAUNCH();
