@@ -83,9 +83,15 @@ __global__ __launch_bounds__(256) void outconv_fwd_kernel(
   const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4;
   f4 z = {bv, bv, bv, bv};
   if (VEC) {
-    if (i0 < S) {
-      for (int c = 0; c < C; ++c) z += w[c] * ldv4(hp + (long long)c * S + i0);
-    }
+    // every channel's float4 requested before the first use (C <= 32; the runtime-C loop issued
+    // one load per round trip), then added in channel order as before
+    f4 hv[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c)
+      if (c < C && i0 < S) hv[c] = ldv4(hp + (long long)c * S + i0);
+#pragma unroll
+    for (int c = 0; c < 32; ++c)
+      if (c < C && i0 < S) z += w[c] * hv[c];
   } else {
     for (int c = 0; c < C; ++c)
 #pragma unroll
@@ -684,7 +690,7 @@ int outconv_fwd_impl(const T* h, long long h_nstride, const float* w, const floa
                      const float* t, float* ftl_part, int N, int C, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
   L3U_REQUIRE(t == nullptr || ftl_part != nullptr);
-  const bool vec = S % 4 == 0 && h_nstride % 4 == 0;
+  const bool vec = S % 4 == 0 && h_nstride % 4 == 0 && C <= 32;   // the vector form holds <= 32 channels
   dim3 grid((S + 1023) / 1024, N);
   if (vec) hipLaunchKernelGGL((outconv_fwd_kernel<T, true>), grid, dim3(256), 0, stream, h, h_nstride, w, b, p, t, ftl_part, C, S);
   else hipLaunchKernelGGL((outconv_fwd_kernel<T, false>), grid, dim3(256), 0, stream, h, h_nstride, w, b, p, t, ftl_part, C, S);
