@@ -1199,19 +1199,39 @@ bool use_volume(int D, int H, int W) { return (long long)(D + 2) * (H + 2) * (W 
 #define L3U_DWV_FUSED 1   // whole-volume backward as one launch (data + weight gradient)
 #endif
 
-// load volume `src` (transformed if XF) into the padded LDS image; the halo is zero
-template <bool XF, typename T>
-L3U_DEV void v_load(float* L, const T* __restrict__ src, int D, int H, int W, float sc, float mu,
-                    float sh) {
+// The padded LDS image of volume `src` (transformed if XF; the halo is zero) for the 256-thread
+// whole-volume kernels (padded volume <= L3U_VOL_MAX), in two phases: v_fetch issues every load
+// of the thread's slots at once (raw values; it does not wait on the InstanceNorm record, so it
+// goes before the record merge), v_put transforms and writes them.
+constexpr int kVR = (L3U_VOL_MAX + 255) / 256;
+template <typename T>
+L3U_DEV void v_fetch(float (&raw)[kVR], const T* __restrict__ src, int D, int H, int W) {
   const int PW = W + 2, PH = H + 2, PV = (D + 2) * PH * PW;
-  for (int i = threadIdx.x; i < PV; i += blockDim.x) {
+#pragma unroll
+  for (int r = 0; r < kVR; ++r) {
+    const int i = threadIdx.x + 256 * r;
     const int x = i % PW - 1, t = i / PW, y = t % PH - 1, z = t / PH - 1;
-    float v = 0.f;
-    if (x >= 0 && x < W && y >= 0 && y < H && z >= 0 && z < D) {
-      v = ld1(src + ((long long)z * H + y) * W + x);
-      if (XF) v = lrelu(fmaf(sc, v - mu, sh));
+    raw[r] = 0.f;
+    if (i < PV && x >= 0 && x < W && y >= 0 && y < H && z >= 0 && z < D)
+      raw[r] = ld1(src + ((long long)z * H + y) * W + x);
+  }
+}
+template <bool XF>
+L3U_DEV void v_put(float* L, const float (&raw)[kVR], int D, int H, int W, float sc, float mu,
+                   float sh) {
+  const int PW = W + 2, PH = H + 2, PV = (D + 2) * PH * PW;
+#pragma unroll
+  for (int r = 0; r < kVR; ++r) {
+    const int i = threadIdx.x + 256 * r;
+    if (i < PV) {
+      const int x = i % PW - 1, t = i / PW, y = t % PH - 1, z = t / PH - 1;
+      float v = 0.f;
+      if (x >= 0 && x < W && y >= 0 && y < H && z >= 0 && z < D) {
+        v = raw[r];
+        if (XF) v = lrelu(fmaf(sc, v - mu, sh));
+      }
+      L[i] = v;
     }
-    L[i] = v;
   }
 }
 
@@ -1227,6 +1247,8 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int nc = blockIdx.x, c = nc % C, n = nc / C;
   const long long HW = (long long)H * W, S = D * HW, cofs = (long long)c * S;
+  float raw[kVR];
+  v_fetch(raw, x + (long long)n * xns + cofs, D, H, W);
   float wk[27];
 #pragma unroll
   for (int t = 0; t < 27; ++t) wk[t] = w[c * 27 + (FLIP ? 26 - t : t)];
@@ -1242,7 +1264,7 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
       mu = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];
     }
   }
-  v_load<XF == 1>(lds, x + (long long)n * xns + cofs, D, H, W, sc, mu, sh);
+  v_put<XF == 1>(lds, raw, D, H, W, sc, mu, sh);
   __syncthreads();
   const int PW = W + 2, PHW = (H + 2) * PW;
   T* yp = y + (long long)n * yns + cofs;
@@ -1299,6 +1321,10 @@ __global__ __launch_bounds__(256) void dwv_bwd_kernel(
   const int nc = blockIdx.x, c = nc % C, n = nc / C;
   const long long HW = (long long)H * W, S = D * HW, cofs = (long long)c * S;
   const int PW = W + 2, PHW = (H + 2) * PW, PV = (D + 2) * PHW;
+  // both volumes' loads in flight together, ahead of the weights and the IN record
+  float rz[kVR], ra[kVR];
+  v_fetch(rz, dz + (long long)n * dzns + cofs, D, H, W);
+  v_fetch(ra, x + (long long)n * xns + cofs, D, H, W);
   float wk[27];
 #pragma unroll
   for (int t = 0; t < 27; ++t) wk[t] = w[c * 27 + 26 - t];
@@ -1309,8 +1335,8 @@ __global__ __launch_bounds__(256) void dwv_bwd_kernel(
   }
   float* dzl = lds;
   float* al = lds + PV;
-  v_load<false>(dzl, dz + (long long)n * dzns + cofs, D, H, W, 1.f, 0.f, 0.f);
-  v_load<MODE == 1>(al, x + (long long)n * xns + cofs, D, H, W, sc, mu, sh);
+  v_put<false>(dzl, rz, D, H, W, 1.f, 0.f, 0.f);
+  v_put<MODE == 1>(al, ra, D, H, W, sc, mu, sh);
   __syncthreads();
   const T* xp = x + (long long)n * xns + cofs;
   float* dxp = dx + (long long)n * dxns + cofs;
