@@ -294,6 +294,61 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
   const T* yp = y2 + (long long)n * y2ns + co;
   const T* rp = r + (long long)n * rns + co;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  float* d2 = dy2 + (long long)n * dy2ns + co;
+  float* drp = dr + (long long)n * drns + co;
+  constexpr int NI = 2;   // S <= NI * 1024 (the 12^3 and 6^3 levels): operands held in registers
+  if (VEC && S <= NI * 1024) {
+    // every tile requested at once, one load phase; the apply reuses the registers (same
+    // per-thread order and expressions as the looped form below: same bits)
+    f4 dv[NI], ov[NI], yv[NI], rv[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const int i = threadIdx.x * 4 + k * 1024;
+      dv[k] = ov[k] = yv[k] = rv[k] = f4{0.f, 0.f, 0.f, 0.f};
+      if (i < S) {
+        dv[k] = ldv4(dp + i);
+        ov[k] = ldv4(op + i);
+        yv[k] = ldv4(yp + i);
+        if (recr) rv[k] = ldv4(rp + i);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      if (threadIdx.x * 4 + k * 1024 < S) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float g = dv[k][q] * lrelu_d(ov[k][q]);
+          s0 += g;
+          s1 += (double)g * ((yv[k][q] - m2) * rs2);
+          if (recr) s2 += (double)g * ((rv[k][q] - mr) * rsr);
+        }
+      }
+    }
+    s0 = block_sum256d(s0, red);
+    s1 = block_sum256d(s1, red);
+    s2 = block_sum256d(s2, red);
+    if (threadIdx.x == 0) {
+      double* o = part + ((long long)c * N + n) * 3;
+      o[0] = s0; o[1] = s1; o[2] = s2;
+    }
+    const float M0 = (float)((0.0 + s0) / S), M1 = (float)((0.0 + s1) / S), M2 = (float)((0.0 + s2) / S);
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const int i = threadIdx.x * 4 + k * 1024;
+      if (i < S) {
+        f4 o2, orr;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float g = dv[k][q] * lrelu_d(ov[k][q]);
+          o2[q] = f2 * (g - M0 - (yv[k][q] - m2) * rs2 * M1);
+          orr[q] = recr ? fr * (g - M0 - (rv[k][q] - mr) * rsr * M2) : g;
+        }
+        stv4(d2 + i, o2);
+        stv4(drp + i, orr);
+      }
+    }
+    return;
+  }
   if (VEC) {
     for (int i = threadIdx.x * 4; i < S; i += 1024) {
       const f4 dv = ldv4(dp + i), ov = ldv4(op + i);
@@ -324,8 +379,6 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
     o[0] = s0; o[1] = s1; o[2] = s2;
   }
   const float M0 = (float)((0.0 + s0) / S), M1 = (float)((0.0 + s1) / S), M2 = (float)((0.0 + s2) / S);
-  float* d2 = dy2 + (long long)n * dy2ns + co;
-  float* drp = dr + (long long)n * drns + co;
   if (VEC) {
     for (int i = threadIdx.x * 4; i < S; i += 1024) {
       const f4 dv = ldv4(dp + i), ov = ldv4(op + i);
