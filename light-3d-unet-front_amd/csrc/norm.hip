@@ -163,6 +163,9 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
 }
 
 // partials per (c, n, block): [sum g, sum g*xhat2, sum g*xhat_r],  g = dout * lrelu'(out)
+#ifndef L3U_NABR_U
+#define L3U_NABR_U 2
+#endif
 template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     const float* __restrict__ dout, long long dns, const T* __restrict__ out, long long ons,
@@ -185,23 +188,39 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
   const T* rp = r + (long long)n * rns + co;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
   if (VEC) {
-    for (int i = (blockIdx.x * 256 + threadIdx.x) * 4; i < S; i += nb * 1024) {
-      const f4 ov = ldv4(op + i);
-      f4 dv = dscale ? dsc * ldv4(dp + i) : ldv4(dp + i);
-      if (dpool) {   // + the MaxPool3d backward of the next level (l3u_maxpool2_bwd folded in)
-        const int HW = H * W, z = fdiv(i, HW, 1.f / HW), rm = i - z * HW, y = fdiv(rm, W, 1.f / W);
-        dv = unpool_add(dv, dpool + (long long)n * dpns + (long long)c * (S / 8),
-                        pidx + (long long)nc * (S / 8), z, y, rm - y * W, H, W);
-      }
-      const f4 yv = ldv4(yp + i);
-      f4 rv = f4{0.f, 0.f, 0.f, 0.f};
-      if (recr) rv = ldv4(rp + i);
+    // U grid-stride tiles per round: all their loads in flight before the first use, the sums
+    // still taken tile by tile in index order (same bits as one tile per round)
+    constexpr int U = L3U_NABR_U;
+    const int step = nb * 1024;
+    for (int i0 = (blockIdx.x * 256 + threadIdx.x) * 4; i0 < S; i0 += U * step) {
+      f4 ov[U], dv[U], yv[U], rv[U];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float g = dv[q] * lrelu_d(ov[q]);
-        s0 += g;
-        s1 += (double)g * ((yv[q] - m2) * rs2);
-        if (recr) s2 += (double)g * ((rv[q] - mr) * rsr);
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * step;
+        ov[u] = dv[u] = yv[u] = rv[u] = f4{0.f, 0.f, 0.f, 0.f};
+        if (i < S) {
+          ov[u] = ldv4(op + i);
+          dv[u] = dscale ? dsc * ldv4(dp + i) : ldv4(dp + i);
+          if (dpool) {   // + the MaxPool3d backward of the next level (l3u_maxpool2_bwd folded in)
+            const int HW = H * W, z = fdiv(i, HW, 1.f / HW), rm = i - z * HW, y = fdiv(rm, W, 1.f / W);
+            dv[u] = unpool_add(dv[u], dpool + (long long)n * dpns + (long long)c * (S / 8),
+                               pidx + (long long)nc * (S / 8), z, y, rm - y * W, H, W);
+          }
+          yv[u] = ldv4(yp + i);
+          if (recr) rv[u] = ldv4(rp + i);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i0 + u * step < S) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float g = dv[u][q] * lrelu_d(ov[u][q]);
+            s0 += g;
+            s1 += (double)g * ((yv[u][q] - m2) * rs2);
+            if (recr) s2 += (double)g * ((rv[u][q] - mr) * rsr);
+          }
+        }
       }
     }
   } else {
