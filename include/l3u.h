@@ -110,37 +110,6 @@ int l3u_dwpw_fwd(const float* x, long long x_nstride, const float* w_dw, const f
                  float* y_stat, const float* w_sc, float* r, long long r_nstride, float* r_stat,
                  float* z, long long z_nstride, int N, int K, int Nout, int D, int H, int W,
                  hipStream_t stream);
-/* ---- whole ResidualBlock forward at small volumes (S <= 256: the 6^3 level) in ONE launch ----
- * replaces ResidualBlock.forward (unet3d.py:77-93) with depthwise-separable convs: shortcut
- * Conv1x1 + InstanceNorm (or identity), conv1, norm1 + LeakyReLU + Dropout3d, conv2, norm2, the
- * residual add and the final LeakyReLU.  Workgroup (n, g) owns output channels 16g..16g+15 of
- * sample n; the G = Cout/16 workgroups of a sample meet at two barriers (the pointwise
- * contractions read every channel).  Every intermediate the backward reads is stored:
- *   z1 [N][Cin][S], y1 / z2 / y2 / r [N][Cout][S], records rec_r / rec1 / rec2 [N][Cout][8].
- * Activation pointers are T* of the entry point's storage type (fp32, or bf16 for _bf16).
- * sync: [N + 1] unsigned, zero once before the first use of this (block, N) and never reset
- * (monotonic barrier counters); sync[N] != 0 afterwards flags a barrier that timed out.
- * Needs every workgroup resident at once: l3u_sblock_supported checks N * Cout/16 against the
- * device's compute units.                                                                     */
-typedef struct l3u_sblock_fwd_args {
-  const void* x;  long long x_nstride;          /* block input [N][Cin][S] */
-  const float* w_dw1; const float* w_pw1;       /* [Cin][27], [Cout][Cin] */
-  const float* w_sc; const float* g_sc; const float* b_sc;   /* NULL: identity (Cin == Cout) */
-  const float* g1; const float* b1;             /* norm1 affine */
-  const float* w_dw2; const float* w_pw2;       /* [Cout][27], [Cout][Cout] */
-  const float* g2; const float* b2;             /* norm2 affine */
-  float drop_p; int layer1;                     /* Dropout3d of norm1: stream id as l3u_norm_src */
-  unsigned long long seed; const int* step;
-  void* z1; void* y1; void* z2; void* y2; void* r;
-  void* out;  long long out_nstride;
-  float* rec_r; float* rec1; float* rec2;
-  unsigned* sync;
-} l3u_sblock_fwd_args;
-int l3u_sblock_supported(int N, int Cin, int Cout, int D, int H, int W, int shortcut);
-int l3u_sblock_fwd(const l3u_sblock_fwd_args* a, int N, int Cin, int Cout, int D, int H, int W,
-                   hipStream_t stream);
-int l3u_sblock_fwd_bf16(const l3u_sblock_fwd_args* a, int N, int Cin, int Cout, int D, int H,
-                        int W, hipStream_t stream);
 /* weight gradient partials: part[N*nsc][J][K] = sum_s dY[n][j][s] X[n][k][s] per voxel chunk   */
 int l3u_pw_bwd_weight_nparts(int N, int S);
 int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, long long x_nstride,

@@ -87,8 +87,6 @@ _SIGS = {
     "l3u_dwpw_supported": [I, I, I, I, I, I],
     "l3u_dwpw_stat_nsb": [I, I, I, I, I],
     "l3u_dwpw_fwd": [P, L, P, P, P, P, P, L, P, P, P, L, P, P, L, I, I, I, I, I, I, P],
-    "l3u_sblock_supported": [I, I, I, I, I, I, I],
-    "l3u_sblock_fwd": [P, I, I, I, I, I, I, P],
 }
 # entry points with a _bf16 twin (same arguments; saved activations stored as bf16, gradients
 # fp32, include/l3u.h)
@@ -100,7 +98,7 @@ BF16_TWINS = ("l3u_dw3_fwd", "l3u_dw3_bwd", "l3u_pw_fwd", "l3u_pw_fwd2", "l3u_pw
               "l3u_outconv_bwd_ftl", "l3u_box_copy",
               "l3u_front_fwd", "l3u_dwpw_fwd", "l3u_outconv_bwd_dz", "l3u_outconv_bwd_ftl_dz",
               "l3u_norm_act_bwd_reduce_r1", "l3u_pw_bwd_tail_r1", "l3u_norm_act_bwd_reduce_up",
-              "l3u_pw_bwd_tail_up", "l3u_sblock_fwd")
+              "l3u_pw_bwd_tail_up")
 for _n in BF16_TWINS:
     _SIGS[_n + "_bf16"] = _SIGS[_n]
 # query helpers that return a value instead of an error code
@@ -108,8 +106,7 @@ _QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_
             "l3u_pw_bwd_supported", "l3u_pw_bwd_nparts", "l3u_convt_bwd_fused_nparts",
             "l3u_norm_act_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks",
             "l3u_gconv3_nblocks", "l3u_gconv3_wgrad_nparts", "l3u_front_nblocks",
-            "l3u_ccl_nchunks", "l3u_dwpw_supported", "l3u_dwpw_stat_nsb",
-            "l3u_sblock_supported"}
+            "l3u_ccl_nchunks", "l3u_dwpw_supported", "l3u_dwpw_stat_nsb"}
 
 _lib = None
 
@@ -123,16 +120,6 @@ class NormSrc(ctypes.Structure):
     record from.  Pass `norm_src_ptr(s)`; keep the object alive across the call."""
     _fields_ = [("stat_part", P), ("nsb", I), ("layer", I), ("gamma", P), ("beta", P),
                 ("drop_p", F), ("seed", U64), ("step", P), ("rec_out", P)]
-
-
-class SblockFwdArgs(ctypes.Structure):
-    """struct l3u_sblock_fwd_args (include/l3u.h): operands of the one-launch small-volume
-    ResidualBlock forward.  Pass ctypes.pointer(a); keep `a` alive across the call."""
-    _fields_ = [("x", P), ("x_nstride", L), ("w_dw1", P), ("w_pw1", P), ("w_sc", P), ("g_sc", P),
-                ("b_sc", P), ("g1", P), ("b1", P), ("w_dw2", P), ("w_pw2", P), ("g2", P), ("b2", P),
-                ("drop_p", F), ("layer1", I), ("seed", U64), ("step", P), ("z1", P), ("y1", P),
-                ("z2", P), ("y2", P), ("r", P), ("out", P), ("out_nstride", L), ("rec_r", P),
-                ("rec1", P), ("rec2", P), ("sync", P)]
 
 
 class AugParam(ctypes.Structure):

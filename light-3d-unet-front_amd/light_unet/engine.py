@@ -14,7 +14,6 @@ Partial sums (IN statistics, weight-gradient split-K partials) live in a per-sha
 layout is fixed by a dry run on first use; one l3u_reduce_segments launch at the end of backward
 turns all weight-gradient partials into the flat gradient buffer in a fixed order.
 """
-import ctypes
 import math
 import os
 
@@ -44,11 +43,6 @@ _RANK1 = os.environ.get("L3U_RANK1", "1") != "0"
 # the encoder's MaxPool3d backward formed in the loads of the consuming block tail (no
 # l3u_maxpool2_bwd launch, no level-output gradient tensor); L3U_POOLFOLD=0 disables
 _POOLFOLD = os.environ.get("L3U_POOLFOLD", "1") != "0"
-# a whole ResidualBlock forward at small volumes (S <= 256: the 6^3 level) as one launch
-# (l3u_sblock_fwd: per-sample workgroup barriers instead of five latency-bound launches).
-# Opt-in (L3U_SBLOCK=1): measured 36-40 us per block against ~30 us for the five launches it
-# replaces (32 workgroups run every stage serially; DESIGN.md §4, tools/sbprof.py)
-_SBLOCK = os.environ.get("L3U_SBLOCK", "0") == "1"
 
 
 class V:
@@ -199,7 +193,6 @@ class UNetEngine:
         # parameters, records and partial sums stay fp32 either way
         self.act_dtype = torch.float32
         self._grad_phase = False   # backward: gradient buffers are fp32 in either storage mode
-        self._sync = {}            # l3u_sblock_fwd barrier counters per (block, N, device)
 
     # ------------------------------------------------------------------ helpers
     @property
@@ -435,9 +428,6 @@ class UNetEngine:
         cout = out.C
         e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
         shortcut = self._has(pre + "shortcut.0.weight")
-        if (_SBLOCK and pool is None and S <= 256
-                and nat.query("l3u_sblock_supported", N, cin, cout, d, h, w, 1 if shortcut else 0)):
-            return self._block_fwd_small(flat, pre, layer, x, out, dims, drop, cptr, st, dev)
         nsb = nat.query("l3u_pw_stat_nsb", cin, cout, S)      # pw1 / shortcut (K = cin)
         nsb2 = nat.query("l3u_pw_stat_nsb", cout, cout, S)    # pw2 (K = cout)
         recs = self._f32(3, N * cout, 8, device=dev)
@@ -537,36 +527,6 @@ class UNetEngine:
                        idx.data_ptr(), N, cout, d, h, w, st)
         sv.update(z1=z1, y1=y1, z2=z2, y2=y2, dims=dims, shortcut=shortcut)
         return sv
-
-    def _block_fwd_small(self, flat, pre, layer, x, out, dims, drop, cptr, st, dev):
-        """ResidualBlock.forward (unet3d.py:77-93) as ONE l3u_sblock_fwd launch (S <= 256): the
-        same saved tensors and records as _block_fwd, so the backward is unchanged."""
-        N = x.t.shape[0]
-        d, h, w = dims
-        S = d * h * w
-        cin, cout = x.C, out.C
-        e = lambda *s: self._empty(*s, device=dev)  # noqa: E731
-        shortcut = self._has(pre + "shortcut.0.weight")
-        recs = self._f32(3, N * cout, 8, device=dev)
-        z1, y1, z2, y2 = e(N, cin, S), e(N, cout, S), e(N, cout, S), e(N, cout, S)
-        r = e(N, cout, S) if shortcut else None
-        key = (pre, N, str(dev))
-        sync = self._sync.get(key)
-        if sync is None:   # monotonic counters: zeroed once, never reset (include/l3u.h)
-            sync = self._sync[key] = torch.zeros(N + 1, dtype=torch.int32, device=dev)
-        wp = lambda nm: self._w(flat, pre + nm) if self._has(pre + nm) else None  # noqa: E731
-        a = nat.SblockFwdArgs(
-            x.p, x.ns, wp("conv1.depthwise.weight"), wp("conv1.pointwise.weight"),
-            wp("shortcut.0.weight"), wp("shortcut.1.weight"), wp("shortcut.1.bias"),
-            wp("norm1.weight"), wp("norm1.bias"), wp("conv2.depthwise.weight"),
-            wp("conv2.pointwise.weight"), wp("norm2.weight"), wp("norm2.bias"), float(drop),
-            1 + layer, self.seed, cptr or None, z1.data_ptr(), y1.data_ptr(), z2.data_ptr(),
-            y2.data_ptr(), r.data_ptr() if shortcut else None, out.p, out.ns,
-            recs[0].data_ptr(), recs[1].data_ptr(), recs[2].data_ptr(), sync.data_ptr())
-        self._call("l3u_sblock_fwd", ctypes.pointer(a), N, cin, cout, d, h, w, st)
-        return {"x": x, "out": out, "recs": recs, "z1": z1, "y1": y1, "z2": z2, "y2": y2,
-                "dims": dims, "shortcut": shortcut,
-                "r": V(r, 0, cout * S, cout) if shortcut else None}
 
     def _conv_w(self, flat, pre, which):
         kind = self.kinds[pre][which - 1]

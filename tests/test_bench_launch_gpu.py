@@ -1,0 +1,56 @@
+"""bench.py's own multi-rank launcher: a plain `python bench.py --gpus N` (no WORLD_SIZE in the
+environment, the driver's command form) starts the N ranks itself through torch.distributed.run
+and relays rank 0's JSON line."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_launcher_command_without_world_size(monkeypatch):
+    """CPU: with WORLD_SIZE unset and --gpus 2 the parent only spawns the launcher child (it never
+    reaches a torch.cuda call) and exits with the child's return code."""
+    sys.path.insert(0, ROOT)
+    import bench
+    seen = {}
+
+    class R:
+        returncode = 7
+
+    def fake_run(cmd, env=None, **kw):
+        seen["cmd"], seen["env"] = cmd, env
+        return R()
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 7
+    cmd = seen["cmd"]
+    assert cmd[0] == sys.executable and cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "2", "--steps", "3"]
+    assert cmd[-5].endswith("bench.py")
+
+
+@pytest.mark.gpu
+def test_bench_self_launches_two_ranks(cuda):
+    """GPU: `python bench.py --gpus 2 --dist-backend gloo --one-device` (both ranks on this GPU)
+    prints one JSON line with n_gpus 2, dp2 and a finite loss."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--dist-backend", "gloo", "--one-device", "--no-cpu-baseline",
+           "--no-config5", "--no-sliding", "--no-grouped", "--no-bf16", "--no-dropin", "--no-data"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 8
+    assert out["value"] > 0 and out["final_loss"] == out["final_loss"]
