@@ -62,6 +62,10 @@ def parse():
     # multi-rank rehearsal on a one-GPU box: every rank on cuda:0, collectives over gloo
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--one-device", action="store_true")
+    ap.add_argument("--dump-calls", default=None,
+                    help="write the recorded step's C-ABI calls (name, family, label, algorithmic "
+                         "bytes) in launch order to this JSON file (tools/instep.py aligns them "
+                         "with a rocprofv3 kernel trace of the graph-replayed step)")
     return ap.parse_args()
 
 
@@ -810,6 +814,10 @@ def main():
     dom_ms = StepRecorder.time_calls(orig, dom_calls[:1], reps=50)[0] if dom_calls else None
     fams = family_rooflines(orig, rec.calls) if rank == 0 else None
     n_launch_calls = len(rec.calls)
+    if args.dump_calls and rank == 0:
+        with open(args.dump_calls, "w") as f:
+            json.dump([dict(zip(("name", "family", "label", "bytes"),
+                                (n,) + (call_bytes(n, a) or (None, None, None)))) for n, a in rec.calls], f)
     rec = None   # releases the recorded step's buffers
 
     if args.no_graph:

@@ -49,11 +49,29 @@ def load():
     importlib.import_module(ALIAS + ".utils")
     importlib.import_module(ALIAS + ".fast_trainer")
     importlib.import_module(ALIAS + ".lesion")
+    importlib.import_module(ALIAS + ".patches")
     return mod
 
 
 LESION = ("get_connected_components", "match_components", "calculate_lesion_metrics",
           "calculate_metrics")
+
+
+def _lesion_entry(device_fn, reference_fn, batched_error):
+    """The device function, except for inputs it does not define: batched [B, D, H, W] volumes
+    (B > 1), which scipy.ndimage.label connects across the batch axis (4D connectivity), go to
+    the reference's own host function unchanged (the device kernels label 3D volumes)."""
+    reference_fn = getattr(reference_fn, "_l3u_reference", reference_fn)   # install() twice
+
+    def entry(*args, **kwargs):
+        try:
+            return device_fn(*args, **kwargs)
+        except batched_error:
+            return reference_fn(*args, **kwargs)
+    entry.__name__, entry.__doc__ = device_fn.__name__, device_fn.__doc__
+    entry.__module__, entry.__wrapped__ = device_fn.__module__, device_fn
+    entry._l3u_reference = reference_fn
+    return entry
 
 
 def _bind_lesion(done):
@@ -68,16 +86,18 @@ def _bind_lesion(done):
     except ImportError:
         return
     names = [n for n in LESION if hasattr(metrics, n)]
+    bound = {n: _lesion_entry(getattr(les, n), getattr(metrics, n), les.BatchedVolumeError)
+             for n in names}
     for n in names:
-        setattr(metrics, n, getattr(les, n))
+        setattr(metrics, n, bound[n])
     done["light_unet.models.metrics"] = names
     for modname in ("light_unet.models", "light_unet.core.trainer", "light_unet.core.inferencer"):
         mod = sys.modules.get(modname)
         if mod is None:
             continue
-        hit = [n for n in LESION if n in vars(mod)]
+        hit = [n for n in names if n in vars(mod)]
         for n in hit:
-            setattr(mod, n, getattr(les, n))
+            setattr(mod, n, bound[n])
         if hit:
             done.setdefault(modname, []).extend(hit)
     inf = sys.modules.get("light_unet.core.inferencer")
@@ -89,7 +109,24 @@ def _bind_lesion(done):
         done.setdefault("light_unet.core.inferencer", []).append("Inferencer.extract_bboxes")
 
 
-def install(fast_step=False, lesion=True):
+def _bind_device_patches(done):
+    """The training loaders of light_unet.datasets.loader (get_data_loader, loader.py:99-113)
+    on device patches: loader._create_train_loader (loader.py:9-10, called by the standard,
+    step-based and probabilistic factories) returns a DevicePatchLoader over the device twin of
+    the PatchDataset / MixedPatchDataset the factory just built (its cases read once into HBM,
+    its sampled locations kept; l3u_amd.patches).  Validation loaders are unchanged."""
+    loader = importlib.import_module("light_unet.datasets.loader")
+    patches = sys.modules[ALIAS + ".patches"]
+    ref = getattr(loader._create_train_loader, "_l3u_reference", loader._create_train_loader)
+
+    def _create_train_loader(dataset, batch_size, shuffle=True):
+        return patches.device_loader(dataset, batch_size)
+    _create_train_loader._l3u_reference = ref
+    loader._create_train_loader = _create_train_loader
+    done["light_unet.datasets.loader"] = ["_create_train_loader"]
+
+
+def install(fast_step=False, lesion=True, device_patches=False):
     """Bind this build's model and loss into the already-importable reference package.
     Returns {module: [names]} of what was replaced.  Raises ImportError when the reference's
     light_unet.models.{unet3d,losses} cannot be imported (nothing is half-installed).
@@ -101,7 +138,13 @@ def install(fast_step=False, lesion=True):
 
     lesion=True (default) also binds the device lesion post-processing (connected components,
     matching, lesion / voxel metrics, bounding boxes: light_unet/lesion.py) where the reference's
-    metrics module imports."""
+    metrics module imports.
+
+    device_patches=True also makes get_data_loader's training loaders cut
+    and augment their patches on the device (light_unet/patches.py; num_workers = 0 draw
+    semantics, DevicePatchLoader), so the graph-replayed step never waits on host workers or a
+    PCIe copy.  Needs light_unet.datasets.loader (and its NIfTI reader)."""
+
     amd = load()
     trainer_mod = importlib.import_module("light_unet.core.trainer") if fast_step else None
     src = {
@@ -125,6 +168,8 @@ def install(fast_step=False, lesion=True):
         fast = importlib.import_module(ALIAS + ".fast_trainer")
         fast.bind(trainer_mod.Trainer)
         done["light_unet.core.trainer"] = ["Trainer.train_epoch", "Trainer._train_epoch_step_based"]
+    if device_patches:
+        _bind_device_patches(done)
     if lesion:
         _bind_lesion(done)
     amd.installed_into = done

@@ -14,14 +14,32 @@ samples patches at random regardless of the index (patch_dataset.py:114-124), so
 data pipeline per rank (experiment.seed + rank) is the sharding; the global batch is
 batch_size * world.  The step's exchange (exchange.py) keeps the global-batch FocalTversky
 (`--ftl-mode exact`, default) or plain DDP averaging (`local`).  Rank 0 keeps the configured
-output directories; rank r > 0 writes its logs / TensorBoard / checkpoints under `<dir>_rank<r>`.
-Unlike scripts/train.py:55 the config file is never rewritten.
+output directories; rank r > 0 writes its logs / TensorBoard under `<dir>_rank<r>`.
+Validation (sliding-window inference + lesion metrics, trainer.py:349-458) runs on rank 0 only;
+its result is broadcast, so every rank takes the same model-selection, scheduler and
+early-stopping decisions (trainer.py:505-541) and the ranks' collectives stay in step.  Only
+rank 0 writes checkpoints (the weights are identical on every rank after each step's gradient
+all-reduce).  Unlike scripts/train.py:55 the config file is never rewritten.
 """
 import argparse
 import os
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def share_validation(trainer, rank, dist):
+    """Trainer.validate on rank 0 only, its (val_loss, metrics) broadcast to every rank; no
+    checkpoint files from ranks > 0."""
+    ref_validate = trainer.validate
+
+    def validate(epoch):
+        out = [ref_validate(epoch) if rank == 0 else None]
+        dist.broadcast_object_list(out, src=0)
+        return out[0]
+    trainer.validate = validate
+    if rank > 0:
+        trainer.save_checkpoint = lambda epoch, is_best=False: None
 
 
 def main(argv=None):
@@ -31,6 +49,9 @@ def main(argv=None):
     ap.add_argument("--splits_dir", default=None)
     ap.add_argument("--ftl-mode", default="exact", choices=["exact", "local"])
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--device-patches", action="store_true",
+                    help="cut and augment training patches on the device (l3u_amd.patches; "
+                         "num_workers = 0 draw semantics, per-rank RNG streams)")
     a = ap.parse_args(argv)
 
     import torch
@@ -48,7 +69,7 @@ def main(argv=None):
     if _HERE not in sys.path:
         sys.path.insert(0, _HERE)
     import l3u_plugin
-    l3u_plugin.install(fast_step=True)
+    l3u_plugin.install(fast_step=True, device_patches=a.device_patches)
     from light_unet.core.config import ConfigManager
     from light_unet.core.trainer import Trainer
 
@@ -64,10 +85,14 @@ def main(argv=None):
     trainer = Trainer(config)
     trainer.l3u_ftl_mode = a.ftl_mode
     if world > 1:   # per-rank data streams (the model is broadcast from rank 0 by FastLoop)
+        import random
         import numpy as np
         seed = int(config["experiment"]["seed"]) + rank
+        random.seed(seed)
         np.random.seed(seed)
         torch.manual_seed(seed)
+    if world > 1:
+        share_validation(trainer, rank, dist)
     trainer.train()
     if world > 1:
         dist.barrier()

@@ -33,16 +33,51 @@ def _device():
     return torch.device("cuda", torch.cuda.current_device())
 
 
-def _volume(a, dev):
-    """[D, H, W] float32 on the device from a numpy array / tensor ([1, D, H, W] accepted)."""
+class BatchedVolumeError(ValueError):
+    """A labelled or thresholded input with more than three non-unit axes ([B, D, H, W], B > 1).
+    scipy.ndimage.label connects such arrays across the leading axis (4D connectivity); the
+    device kernels label 3D volumes only, so l3u_plugin hands these calls back to the reference's
+    own host function (the contract of this module is 3D)."""
+
+
+def _volume(a, dev, keep_f64=False):
+    """[D, H, W] float32 on the device from a numpy array / tensor ([1, D, H, W] accepted).
+    keep_f64: a float64 input stays float64 (the reference thresholds float64 maps in float64)."""
     t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(np.asarray(a)))
     while t.dim() > 3 and t.shape[0] == 1:
         t = t[0]
+    if t.dim() > 3:
+        raise BatchedVolumeError(f"expected a 3D volume [D, H, W], got shape {tuple(t.shape)}")
     if t.dim() != 3:
         raise ValueError(f"expected a 3D volume [D, H, W], got shape {tuple(t.shape)}")
     if t.dtype == torch.bool:
         t = t.to(torch.uint8)
-    return t.to(device=dev, dtype=torch.float32).contiguous()
+    dt = torch.float64 if (keep_f64 and t.dtype == torch.float64) else torch.float32
+    return t.to(device=dev, dtype=dt).contiguous()
+
+
+def _require_3d(*arrays):
+    """Raise BatchedVolumeError for an input with more than three non-unit leading axes, before
+    any device work (shape only)."""
+    for a in arrays:
+        if a is None or isinstance(a, Components):
+            continue
+        shape = tuple(a.shape) if hasattr(a, "shape") else np.shape(a)
+        while len(shape) > 3 and shape[0] == 1:
+            shape = shape[1:]
+        if len(shape) > 3:
+            raise BatchedVolumeError(f"expected a 3D volume [D, H, W], got shape {tuple(shape)}")
+
+
+def _foreground(vol, threshold, dev):
+    """(volume, threshold) for l3u_ccl_label, which compares in float32.  A float64 map is
+    compared in float64 on the device first (`vol >= threshold` as metrics.py:245 /
+    inferencer.py:64 evaluate it in numpy), so values between float32(threshold) and threshold
+    classify as the reference classifies them; the kernel then labels the 0/1 mask."""
+    v = _volume(vol, dev, keep_f64=True)
+    if v.dtype == torch.float64:
+        return (v >= float(threshold)).to(torch.float32), 0.5
+    return v, threshold
 
 
 class Components:
@@ -51,6 +86,7 @@ class Components:
 
     def __init__(self, labels, num, stats):
         self.labels, self.num, self.stats = labels, int(num), stats
+        self.pmax64 = None   # float64 per-component maxima of a float64 prob map (label(prob=))
 
     def sizes(self):
         return self.stats[:, _SIZE].astype(np.int64)
@@ -71,7 +107,7 @@ def label(vol, threshold=0.5, min_size=0, prob=None):
     ndimage.label of the survivors is the order-preserving rank).  prob: optional volume whose
     per-component maximum lands in stats[:, 10] (float32 bits)."""
     dev = _device()
-    v = _volume(vol, dev)
+    v, threshold = _foreground(vol, threshold, dev)
     D, H, W = v.shape
     n = v.numel()
     st = nat.stream()
@@ -84,9 +120,14 @@ def label(vol, threshold=0.5, min_size=0, prob=None):
     num = int(cnt[nch].item())
     if num == 0:
         return Components(lab, 0, np.zeros((0, 12), dtype=np.uint64))
-    pv = _volume(prob, dev) if prob is not None else None
+    pv = _volume(prob, dev, keep_f64=True) if prob is not None else None
     if pv is not None and tuple(pv.shape) != (D, H, W):
         raise ValueError("prob must have the labelled volume's shape")
+    pv64 = None
+    if pv is not None and pv.dtype == torch.float64:
+        # the kernel's per-component maximum is float32; a float64 map keeps its own maximum
+        # (float(prob_map[component_mask].max()) in inferencer.py:98), taken below
+        pv64, pv = pv, None
     stats = torch.empty(num * 12, dtype=torch.int64, device=dev)
     nat.call("l3u_ccl_stats", lab.data_ptr(), None, pv.data_ptr() if pv is not None else None,
              stats.data_ptr(), num, D, H, W, st)
@@ -107,11 +148,17 @@ def label(vol, threshold=0.5, min_size=0, prob=None):
             nat.call("l3u_ccl_stats", lab.data_ptr(), rm.data_ptr(),
                      pv.data_ptr() if pv is not None else None, stats.data_ptr(), num, D, H, W, st)
             s = stats.view(num, 12).cpu().numpy().view(np.uint64)
-    return Components(lab, num, s)
+    c = Components(lab, num, s)
+    if pv64 is not None:
+        m = torch.full((num + 1,), -math.inf, dtype=torch.float64, device=dev)
+        m.scatter_reduce_(0, lab.reshape(-1).long(), pv64.reshape(-1), "amax")
+        c.pmax64 = m[1:].cpu().numpy()
+    return c
 
 
 def get_connected_components(mask, min_size=0):
     """metrics.py:38-63: (labeled int32 [D, H, W] numpy, num_components); foreground = mask != 0."""
+    _require_3d(mask)
     m = np.asarray(mask) if not isinstance(mask, torch.Tensor) else mask
     fg = (m != 0)
     c = label(fg.astype(np.float32) if isinstance(fg, np.ndarray) else fg.float(), 0.5, min_size)
@@ -124,6 +171,10 @@ def _as_components(lab_or_comp):
     dev = _device()
     t = lab_or_comp if isinstance(lab_or_comp, torch.Tensor) else torch.from_numpy(
         np.ascontiguousarray(np.asarray(lab_or_comp)))
+    while t.dim() > 3 and t.shape[0] == 1:
+        t = t[0]
+    if t.dim() != 3:
+        raise BatchedVolumeError(f"expected a labelled 3D volume [D, H, W], got shape {tuple(t.shape)}")
     t = t.to(device=dev, dtype=torch.int32).contiguous()
     num = int(t.max().item()) if t.numel() else 0
     if num == 0:
@@ -152,6 +203,7 @@ def match_components(pred_labeled, target_labeled, iou_threshold=0.1, distance_t
                      spacing=(4.0, 4.0, 4.0)):
     """metrics.py:127-213: greedy matching of predicted to target components by IoU or centre
     distance.  Labelled volumes (numpy / device) or Components."""
+    _require_3d(pred_labeled, target_labeled)
     pc, tc = _as_components(pred_labeled), _as_components(target_labeled)
     num_pred, num_target = pc.num, tc.num
     if num_pred == 0 or num_target == 0:
@@ -202,6 +254,7 @@ def calculate_lesion_metrics(pred, target, threshold=0.5, min_size_voxels=0, iou
                              distance_threshold_mm=10.0, spacing=(4.0, 4.0, 4.0)):
     """metrics.py:216-287: lesion-wise recall / precision / f1 and tp / fp / fn counts."""
     pred, target = _squeeze(pred), _squeeze(target)
+    _require_3d(pred, target)
     pc = label(pred, threshold, min_size_voxels)
     tc = label(target, 0.5, min_size_voxels)
     if tc.num == 0:
@@ -222,6 +275,8 @@ def calculate_metrics(predictions, labels, threshold=0.5, spacing=(4.0, 4.0, 4.0
     voxel counts come from the same device labelling (foreground sizes and overlaps)."""
     pred_list, label_list = _case_list(predictions, "predictions"), _case_list(labels, "labels")
     spacings = _spacing_per_case(spacing, len(pred_list))
+    for pred, target in zip(pred_list, label_list):
+        _require_3d(_squeeze(np.asarray(pred)), _squeeze(np.asarray(target)))
     smooth = 1e-6
     tot_tp = tot_fp = tot_fn = 0
     inter_sum = union_sum = 0.0
@@ -300,7 +355,8 @@ def extract_bboxes(prob_map, threshold=0.3, min_volume_cc=0.5, spacing=(4.0, 4.0
         zl, zh = max(0, zmin - e), min(shape[0] - 1, zmax + e)
         yl, yh = max(0, ymin - e), min(shape[1] - 1, ymax + e)
         xl, xh = max(0, xmin - e), min(shape[2] - 1, xmax + e)
-        conf = np.array([int(s[_PMAX])], dtype=np.uint32).view(np.float32)[0]
+        conf = (c.pmax64[cid - 1] if c.pmax64 is not None
+                else np.array([int(s[_PMAX])], dtype=np.uint32).view(np.float32)[0])
         out.append({"mask_id": cid,
                     "bbox_voxel": [zl, zh, yl, yh, xl, xh],
                     "bbox_mm": [float(zl * spacing[0]), float(zh * spacing[0]), float(yl * spacing[1]),

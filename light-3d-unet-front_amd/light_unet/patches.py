@@ -56,7 +56,16 @@ def draw_augmentation(aug, patch):
 
 
 def _cosdg_sindg(angle):
-    """scipy.special.cosdg / sindg: exact at multiples of 90 degrees."""
+    """scipy.ndimage.rotate's rotation constants, `special.cosdg(angle), special.sindg(angle)`
+    (the cephes degree functions, the reference's own dependency).  Without scipy: exact at
+    multiples of 90 degrees, np.cos / np.sin of the radians otherwise (may differ in the last
+    ulp)."""
+    try:
+        from scipy import special
+    except ImportError:
+        special = None
+    if special is not None:
+        return float(special.cosdg(angle)), float(special.sindg(angle))
     if angle % 90 == 0:
         k = int(angle // 90) % 4
         return [1.0, 0.0, -1.0, 0.0][k], [0.0, 1.0, 0.0, -1.0][k]
@@ -104,18 +113,21 @@ class DevicePatchDataset:
 
     cases: list of (image, label[, body_mask]) numpy volumes (the NIfTI contents the reference
     loads per item).  Seeding, location sampling (_sample_locations, :74-100) and the per-item
-    draws follow the reference; sample_batch(B) returns device tensors [B, 1, *patch_size]."""
+    draws follow the reference; sample_batch(B) returns device tensors [B, 1, *patch_size].
+    from_reference() takes a constructed reference PatchDataset instead: its sampled locations
+    are kept as they are and each case is read once."""
 
     def __init__(self, cases, patch_size=(48, 48, 48), lesion_patch_ratio=0.5, augmentation=None,
-                 seed=42, device=None):
+                 seed=42, device=None, locations=None):
         if not torch.cuda.is_available():
             raise nat.NativeError("DevicePatchDataset needs the ROCm device (no CPU fallback)")
         self.dev = device or torch.device("cuda", torch.cuda.current_device())
         self.patch_size = tuple(int(v) for v in patch_size)
         self.lesion_patch_ratio = lesion_patch_ratio
         self.augmentation = augmentation
-        random.seed(seed)
-        np.random.seed(seed)
+        if locations is None:
+            random.seed(seed)
+            np.random.seed(seed)
         self.vols = []
         for case in cases:
             img, lab = np.asarray(case[0], np.float32), np.asarray(case[1], np.float32)
@@ -123,8 +135,28 @@ class DevicePatchDataset:
                 raise ValueError("image and label must be matching 3D volumes")
             self.vols.append((torch.from_numpy(np.ascontiguousarray(img)).to(self.dev),
                               torch.from_numpy(np.ascontiguousarray(lab)).to(self.dev)))
-        self.lesion_locations, self.background_locations = self._sample_locations(cases)
+        if locations is None:
+            locations = self._sample_locations(cases)
+        self.lesion_locations, self.background_locations = locations
         self.last_draws = []
+
+    @classmethod
+    def from_reference(cls, ds, read=None, device=None):
+        """The device twin of a constructed reference PatchDataset `ds`: the same cases,
+        locations (ds.lesion_locations / background_locations, drawn by its __init__), patch
+        size, lesion ratio and augmentation config.  Each case is read ONCE with
+        read(path) -> float32 volume (default: `nib.load(path).get_fdata().astype(np.float32)`
+        through the nibabel module the reference module imported, patch_dataset.py:129-130)
+        and stays in HBM.  Consumes no random numbers."""
+        if read is None:
+            import sys
+            nib = sys.modules[type(ds).__module__].nib
+
+            def read(path):
+                return nib.load(path).get_fdata().astype(np.float32)
+        cases = [(read(c["image_path"]), read(c["label_path"])) for c in ds.cases]
+        return cls(cases, ds.patch_size, ds.lesion_patch_ratio, ds.augmentation, device=device,
+                   locations=(list(ds.lesion_locations), list(ds.background_locations)))
 
     @staticmethod
     def _sample_locations(cases):
@@ -153,29 +185,124 @@ class DevicePatchDataset:
             return self.background_locations[np.random.randint(len(self.background_locations))]
         return self.lesion_locations[np.random.randint(len(self.lesion_locations))]
 
+    def draw_item(self):
+        """One __getitem__'s random draws (location, then _augment's), in the reference's order:
+        ((case index, centre, AugDraw), its l3u_aug_param record)."""
+        case_idx, center = self._draw_location()
+        d = draw_augmentation(self.augmentation, self.patch_size)
+        img_t, lab_t = self.vols[case_idx]
+        return (case_idx, tuple(int(v) for v in center), d), aug_param(img_t, lab_t, center,
+                                                                      self.patch_size, d)
+
     def sample_batch(self, B):
-        draws, params = [], []
-        for _ in range(B):
-            case_idx, center = self._draw_location()
-            d = draw_augmentation(self.augmentation, self.patch_size)
-            draws.append((case_idx, tuple(int(v) for v in center), d))
-            img_t, lab_t = self.vols[case_idx]
-            params.append(aug_param(img_t, lab_t, center, self.patch_size, d))
-        self.last_draws = draws
-        arr = (nat.AugParam * B)(*params)
-        prm = torch.frombuffer(bytearray(arr), dtype=torch.uint8).to(self.dev)
-        pz, py, px = self.patch_size
-        P = pz * py * px
-        noise = None
-        if any(d.noise is not None for _, _, d in draws):
-            nz = np.zeros((B, P), np.float64)
-            for k, (_, _, d) in enumerate(draws):
-                if d.noise is not None:
-                    nz[k] = d.noise.reshape(-1)
-            noise = torch.from_numpy(nz).to(self.dev)
-        tmp = torch.empty(2, B, P, dtype=torch.float32, device=self.dev)
-        out = torch.empty(2, B, 1, pz, py, px, dtype=torch.float32, device=self.dev)
-        nat.call("l3u_aug_patches", prm.data_ptr(), B, pz, py, px,
-                 noise.data_ptr() if noise is not None else None, tmp[0].data_ptr(),
-                 tmp[1].data_ptr(), out[0].data_ptr(), out[1].data_ptr(), nat.stream())
-        return out[0], out[1]
+        """B consecutive __getitem__ draws, cut and augmented on the device in one launch pair."""
+        items = [self.draw_item() for _ in range(B)]
+        self.last_draws = [i[0] for i in items]
+        return cut_patches(items, self.patch_size, self.dev)
+
+
+def cut_patches(items, patch, dev):
+    """One l3u_aug_patches launch pair over [(draw, AugParam)] (the records may point into
+    different datasets' volumes): device tensors images, labels [B, 1, *patch]."""
+    B = len(items)
+    arr = (nat.AugParam * B)(*[p for _, p in items])
+    prm = torch.frombuffer(bytearray(arr), dtype=torch.uint8).to(dev)
+    pz, py, px = patch
+    P = pz * py * px
+    noise = None
+    if any(d.noise is not None for (_, _, d), _ in items):
+        nz = np.zeros((B, P), np.float64)
+        for k, ((_, _, d), _) in enumerate(items):
+            if d.noise is not None:
+                nz[k] = d.noise.reshape(-1)
+        noise = torch.from_numpy(nz).to(dev)
+    tmp = torch.empty(2, B, P, dtype=torch.float32, device=dev)
+    out = torch.empty(2, B, 1, pz, py, px, dtype=torch.float32, device=dev)
+    nat.call("l3u_aug_patches", prm.data_ptr(), B, pz, py, px,
+             noise.data_ptr() if noise is not None else None, tmp[0].data_ptr(),
+             tmp[1].data_ptr(), out[0].data_ptr(), out[1].data_ptr(), nat.stream())
+    return out[0], out[1]
+
+
+class DeviceMixedPatchDataset:
+    """MixedPatchDataset (patch_dataset.py:223-268) over two DevicePatchDatasets: per item,
+    np.random.rand() < fl_ratio picks the FL stream (else DLBCL), the reference's (unused) index
+    draw np.random.randint(len(sub)) is made, then the sub-dataset's __getitem__ draws.  The
+    per-domain sample counts are kept on `counts` (the reference MixedPatchDataset object when
+    built by from_reference, so Trainer.train_epoch reads them there, trainer.py:210-256)."""
+
+    def __init__(self, fl, dlbcl, fl_ratio=0.5, counts=None):
+        self.fl, self.dlbcl, self.fl_ratio = fl, dlbcl, fl_ratio
+        self.patch_size, self.dev = fl.patch_size, fl.dev
+        self.counts = counts if counts is not None else self
+        if counts is None:
+            self.reset_sample_counts()
+        self.last_draws = []
+
+    @classmethod
+    def from_reference(cls, ds, read=None, device=None):
+        return cls(DevicePatchDataset.from_reference(ds.fl_dataset, read, device),
+                   DevicePatchDataset.from_reference(ds.dlbcl_dataset, read, device),
+                   ds.fl_ratio, counts=ds)
+
+    def reset_sample_counts(self):
+        self.fl_sample_count = 0
+        self.dlbcl_sample_count = 0
+
+    def get_sample_counts(self):
+        return {"fl_samples": self.fl_sample_count, "dlbcl_samples": self.dlbcl_sample_count,
+                "total_samples": self.fl_sample_count + self.dlbcl_sample_count}
+
+    def __len__(self):
+        return len(self.fl) + len(self.dlbcl)
+
+    def draw_item(self):
+        if np.random.rand() < self.fl_ratio and len(self.fl) > 0:
+            self.counts.fl_sample_count += 1
+            np.random.randint(len(self.fl))
+            return self.fl.draw_item()
+        if len(self.dlbcl) > 0:
+            self.counts.dlbcl_sample_count += 1
+            np.random.randint(len(self.dlbcl))
+            return self.dlbcl.draw_item()
+        np.random.randint(len(self.fl))
+        return self.fl.draw_item()
+
+    def sample_batch(self, B):
+        items = [self.draw_item() for _ in range(B)]
+        self.last_draws = [i[0] for i in items]
+        return cut_patches(items, self.patch_size, self.dev)
+
+
+class DevicePatchLoader:
+    """The training DataLoader of loader.py:9-10 (batch_size, shuffle=True, drop_last=False)
+    over a device dataset, with num_workers = 0 semantics: batch k holds the next batch_size
+    __getitem__ draws of the process's global numpy / python RNGs (the sampler's index order is
+    irrelevant: __getitem__ ignores its index, patch_dataset.py:114-124, :254-261), the last batch
+    is ragged, and each epoch takes the two int64 seeds a torch DataLoader iterator draws from
+    torch's global generator (the iterator's base seed and RandomSampler's seed), so the torch
+    RNG stream after an epoch is the host loader's.  Batches are device tensors
+    (images, labels) [b, 1, *patch_size]."""
+
+    def __init__(self, dataset, batch_size):
+        self.dataset, self.batch_size = dataset, int(batch_size)
+
+    def __len__(self):
+        return (len(self.dataset) + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        torch.empty((), dtype=torch.int64).random_()   # _BaseDataLoaderIter._base_seed
+        torch.empty((), dtype=torch.int64).random_()   # RandomSampler's generator seed
+        n = len(self.dataset)
+        for b0 in range(0, n, self.batch_size):
+            yield self.dataset.sample_batch(min(self.batch_size, n - b0))
+
+
+def device_loader(dataset, batch_size, read=None, device=None):
+    """A DevicePatchLoader for a reference PatchDataset / MixedPatchDataset (by duck type:
+    MixedPatchDataset carries fl_dataset / dlbcl_dataset)."""
+    if hasattr(dataset, "fl_dataset") and hasattr(dataset, "dlbcl_dataset"):
+        dd = DeviceMixedPatchDataset.from_reference(dataset, read, device)
+    else:
+        dd = DevicePatchDataset.from_reference(dataset, read, device)
+    return DevicePatchLoader(dd, batch_size)

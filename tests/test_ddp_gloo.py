@@ -123,3 +123,48 @@ def test_mode_validation():
     from light_unet.exchange import check_mode
     with pytest.raises(ValueError):
         check_mode("sum")
+
+
+def _share_validation_worker(rank, world, port, q):
+    import sys as _s
+    _s.path.insert(0, PKG)
+    import torch.distributed as dist
+    import l3u_train
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+
+    class T:
+        calls = 0
+        saved = []
+
+        def validate(self, epoch):
+            T.calls += 1
+            return 0.0, {"best_recall": 0.5 + epoch, "rank": rank}
+
+        def save_checkpoint(self, epoch, is_best=False):
+            T.saved.append(epoch)
+    t = T()
+    l3u_train.share_validation(t, rank, dist)
+    res = [t.validate(e) for e in range(2)]
+    t.save_checkpoint(0, True)
+    q.put((rank, T.calls, res, list(T.saved)))
+    dist.destroy_process_group()
+
+
+def test_validation_on_rank0_broadcast():
+    """l3u_train: Trainer.validate runs on rank 0 only and every rank receives its result (same
+    scheduler / early-stopping decisions); ranks > 0 write no checkpoints."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_share_validation_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=60) for _ in ps)
+    for p in ps:
+        p.join(30)
+    assert got[0][1] == 2 and got[1][1] == 0
+    assert got[0][2] == got[1][2] == [(0.0, {"best_recall": 0.5, "rank": 0}),
+                                      (0.0, {"best_recall": 1.5, "rank": 0})]
+    assert got[0][3] == [0] and got[1][3] == []

@@ -101,3 +101,30 @@ def test_bboxes_match_oracle_ragged(cuda):
     for g, r in zip(got, ref):
         for k in ("mask_id", "bbox_voxel", "volume_cc", "confidence"):
             assert g[k] == r[k], k
+
+
+def test_float64_maps_threshold_in_float64(cuda):
+    """A float64 probability map (Trainer.validate's prob_map * body_mask) is thresholded in
+    float64, as the reference's numpy `pred >= threshold` does (metrics.py:245,
+    inferencer.py:64): voxels equal to float32(0.7) = 0.69999998... lie below 0.7 there, so they
+    are background; the boxes' confidence is the float64 maximum (inferencer.py:98)."""
+    from light_unet import lesion
+    rng = np.random.default_rng(11)
+    p = rng.random((40, 36, 44)) * 0.6
+    blobs = rng.random((40, 36, 44)) < 0.02
+    p[blobs] = float(np.float32(0.7))            # just below 0.7 in float64
+    hot = rng.random((40, 36, 44)) < 0.01
+    p[hot] = 0.7 + rng.random(int(hot.sum())) * 0.3
+    assert p.dtype == np.float64
+    lab, n = lesion.get_connected_components(p >= 0.7)
+    ref, nr = L.get_connected_components(p >= 0.7)
+    assert n == nr and np.array_equal(lab, ref)
+    tgt = (p >= 0.7).astype(np.float32)
+    m = lesion.calculate_lesion_metrics(p, tgt, threshold=0.7)
+    assert (m["tp"], m["fp"], m["fn"]) == (nr, 0, 0), m
+    got = lesion.extract_bboxes(p, 0.7, 0.0, (4.0, 4.0, 4.0), expansion_voxels=0)
+    ref_b = L.bboxes(p, 0.7, 0.0, (4.0, 4.0, 4.0), expansion_voxels=0)
+    assert len(got) == len(ref_b) == nr
+    for g, r in zip(got, ref_b):
+        assert g["bbox_voxel"] == r["bbox_voxel"]
+        assert g["confidence"] == float(p[ref == g["mask_id"]].max())
