@@ -65,7 +65,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--convt-only", action="store_true")
+    ap.add_argument("--scale", action="store_true",
+                    help="the fused backward at N = 1, 2, 4, 8 for the big shapes (bandwidth vs "
+                         "latency scaling)")
     a = ap.parse_args()
+    if a.scale:
+        global SHAPES
+        SHAPES = [(n, J, K, L, pro, acc, role) for (J, K, L, pro, acc, role) in
+                  [(16, 32, 48, True, False, "up3 conv1"), (16, 32, 48, False, True, "up3 shortcut"),
+                   (16, 16, 48, False, False, "up3 conv2"), (32, 64, 24, True, False, "up2 conv1"),
+                   (32, 32, 24, False, False, "up2 conv2")] for n in (1, 2, 4, 8)]
     if a.convt_only:
         convt(a.iters)
         return
@@ -105,10 +114,11 @@ def main():
 
         nb = 4 * N * S * (J * (2 if pro else 1) + K + K * (2 if acc else 1))
         tf = graph_time(fused, a.iters)
-        tu = graph_time(unfused, a.iters)
-        print(f"{tag:12s} J{J:<3d} K{K:<3d} {L}^3 pro={int(pro)} acc={int(acc)} {role:24s} fused "
+        tu = graph_time(unfused, a.iters) if not a.scale else float("nan")
+        print(f"{tag:12s} N{N} J{J:<3d} K{K:<3d} {L}^3 pro={int(pro)} acc={int(acc)} {role:24s} fused "
               f"{tf:7.2f} us ({nb / tf / 1e3:5.0f} GB/s)  unfused {tu:7.2f} us", flush=True)
-    convt(a.iters)
+    if not a.scale:
+        convt(a.iters)
 
 
 def convt(iters):
