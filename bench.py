@@ -294,6 +294,29 @@ def family_rooflines(nat_call, calls):
     return out
 
 
+def instep_evidence(workload, launches):
+    """In-step family rooflines from the newest committed tools/instep.py record of this workload
+    (a rocprofv3 kernel trace of the graph-replayed step aligned with its C-ABI calls:
+    profiles/*_instep_<workload>.json), used only when it has this step's launch count (the same
+    schedule); per family: launches, bytes, in-step us, achieved GB/s, fraction of 8 TB/s."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_instep_{workload}.json")))
+    for fn in reversed(files):
+        with open(fn) as f:
+            rec = json.load(f)
+        ncalls = rec["dw"]["launches"] + rec["gemm"]["launches"]
+        out = {"source": os.path.relpath(fn, ROOT), "commit": rec.get("commit"),
+               "step_kernel_us": rec["step_kernel_us"], "launches": rec["launches"],
+               "under_10us": rec.get("under_10us")}
+        for fam in ("dw", "gemm"):
+            out[fam] = {k: rec[fam][k] for k in ("launches", "bytes", "us", "achieved", "frac")}
+        out["dominant"] = max(rec["dw"]["calls"] + rec["gemm"]["calls"], key=lambda r: r["us"])
+        out["family_calls"] = ncalls
+        out["matches_this_step"] = (rec.get("calls") == launches) if launches is not None else None
+        return out
+    return None
+
+
 def gemm_mfma_evidence(top=5):
     """MFMA-busy fractions of the step's GEMM launches from the committed rocprofv3 passes
     (tools/pmc_step.sh + tools/pmc_gemm.sh -> tools/pmc_launch_json.py -> profiles/*_pmc_step.json)."""
@@ -854,6 +877,8 @@ def main():
 
     sliding = sliding_bench(model, device) if (rank == 0 and not args.no_sliding) else None
     cfg5 = config5_bench(device, world, rank) if not args.no_config5 else None   # every rank
+    if cfg5 is not None:
+        cfg5["roofline_in_step"] = instep_evidence("c5", None)
     cfg5 = cfg5 if rank == 0 else None
     grouped = grouped_bench(device) if (rank == 0 and not args.no_grouped) else None
     bf16 = bf16_bench(device, args, enc, world, rank, pool) if (args.dtype == "fp32" and not args.no_bf16) else None
@@ -913,6 +938,8 @@ def main():
                 "algorithmic_bytes": dbytes,
                 "avg_launch_ms": round(dom_ms, 5) if dom_ms else None,
                 "cache_exceeding": dw_bwd_cache_exceeding(device),
+                "in_step": instep_evidence(
+                    "c5" if enc == (32, 64, 128, 256) and args.size == 64 else args.dtype, n_launch_calls),
                 "depthwise": fams["dw"],
                 "gemm": dict(fams["gemm"], calls=sorted(fams["gemm"]["calls"], key=lambda r: -r["us"])[:5],
                              mfma=gemm_mfma_evidence()),

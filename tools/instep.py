@@ -93,7 +93,8 @@ def main():
     rec = {"what": "in-step durations (rocprofv3 kernel trace of the graph-replayed step, mean over "
                    f"{nsteps} steps) against the calls' algorithmic bytes",
            "commit": commit, "workload": workload,
-           "step_kernel_us": round(sum(u for _, u in ks), 1), "launches": len(ks)}
+           "step_kernel_us": round(sum(u for _, u in ks), 1), "launches": len(ks),
+           "calls": len(calls)}
     for f, rows in fam.items():
         tb = sum(r["bytes"] for r in rows)
         tt = sum(r["us"] for r in rows) * 1e-6
