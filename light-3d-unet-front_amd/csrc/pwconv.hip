@@ -646,12 +646,21 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const int j = tid / PS, sub = tid % PS;
     double t0 = 0.0, t1 = 0.0;
     if (j < J) {
-      if (PRO == 2) {   // block-tail partials [J][N][npart][3]: {sum g, sum g*xhat2, sum g*xhat_r}
-        const double* pp = in_part + ((long long)j * N + n) * npart * 3;
-        for (int i = sub; i < npart; i += PS) { t0 += pp[i * 3]; t1 += pp[i * 3 + sel]; }
-      } else {
-        const double* pp = in_part + ((long long)j * N + n) * npart * 2;
-        for (int i = sub; i < npart; i += PS) { t0 += pp[i * 2]; t1 += pp[i * 2 + 1]; }
+      // the loads of 4 steps are issued together (one memory latency per 4 partials; the
+      // summation order is unchanged)
+      const int nv = PRO == 2 ? 3 : 2, o1 = PRO == 2 ? sel : 1;
+      const double* pp = in_part + ((long long)j * N + n) * npart * nv;
+      for (int i0 = sub; i0 < npart; i0 += 4 * PS) {
+        double a[4], b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = i0 + u * PS;
+          a[u] = i < npart ? pp[i * nv] : 0.0;
+          b[u] = i < npart ? pp[i * nv + o1] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (i0 + u * PS < npart) { t0 += a[u]; t1 += b[u]; }
       }
     }
     psum[tid * 2] = t0;
