@@ -217,8 +217,9 @@ def call_bytes(name, a):
         N, C, D, H, W = a[11:16]
         S = D * H * W
         acc = a[8]
-        return ("dw", f"bwd{'+IN' if a[5] else ''}{'+acc' if acc else ''} [{N},{C},{D}x{H}x{W}]",
-                4 * N * C * S * (2 + acc) + e * N * C * S + 108 * C)
+        ca = 1 if a[3] < 0 else C   # a rank-1 input (negative stride) reads one channel
+        return ("dw", f"bwd{'+IN' if a[5] else ''}{'+acc' if acc else ''}{' (rank-1 A)' if a[3] < 0 else ''} "
+                      f"[{N},{C},{D}x{H}x{W}]", 4 * N * C * S * (2 + acc) + e * N * ca * S + 108 * C)
     if base == "l3u_pw_fwd":      # (x, xns, w, trans, bias, y, yns, acc, part, N, K, J, S)
         N, K, J, S = a[9:13]
         if a[3]:                  # W^T dy of a backward (fp32 operands)
@@ -230,21 +231,25 @@ def call_bytes(name, a):
     if base == "l3u_pw_bwd":      # (dy, dyns, y, yns, rec, ip, np, x, xns, w, dx, dxns, acc, part, N, J, K, S)
         N, J, K, S = a[14:18]
         pro = a[2] is not None
+        jy = 1 if (pro and a[3] < 0) else J   # rank-1 y
         return ("gemm", f"pw_bwd {J}->{K}{'+IN' if pro else ''} [{N},{S}]",
-                N * S * (4 * J + (e * J if pro else 0) + e * K + 4 * K * (1 + a[12])))
+                N * S * (4 * J + (e * jy if pro else 0) + e * K + 4 * K * (1 + a[12])))
     if base == "l3u_pw_bwd_tail":  # (dout, dns, out, ons, yr, yns, rec, pn, ntp, sel, x, xns, w, dx, dxns, acc, part, N, J, K, S)
         N, J, K, S = a[17:21]
+        jr = 1 if a[5] < 0 else J   # rank-1 yr
         return ("gemm", f"pw_bwd_tail{a[9]} {J}->{K} [{N},{S}]",
-                N * S * (4 * J + 2 * e * J + e * K + 4 * K * (1 + a[15])))
+                N * S * (4 * J + e * (J + jr) + e * K + 4 * K * (1 + a[15])))
     if base == "l3u_pw_bwd_tail_r1":  # (dz, dzns, dscale, out, ons, yr, yns, rec, pn, ntp, sel, x, xns, w, dx, dxns, acc, part, N, J, K, S)
         N, J, K, S = a[18:22]           # rank-1 dout: one fp32 channel
+        jr = 1 if a[6] < 0 else J
         return ("gemm", f"pw_bwd_tail{a[10]} (rank-1 dout) {J}->{K} [{N},{S}]",
-                N * S * (4 + 2 * e * J + e * K + 4 * K * (1 + a[16])))
+                N * S * (4 + e * (J + jr) + e * K + 4 * K * (1 + a[16])))
     if base == "l3u_pw_bwd_tail_up":  # (dskip, dskns, dpool, dpns, idx, out, ons, yr, yns, rec, pn, ntp, sel, x, xns, w, dx, dxns, acc, part, N, J, K, D, H, W)
         N, J, K, D, H, W = a[20:26]     # dout = skip gradient + unpooled dpool (+ argmax bytes)
         S = D * H * W
-        return ("gemm", f"pw_bwd_tail{a[12]} (+maxpool bwd) {J}->{K} [{N},{S}]",
-                N * S * (4 * J + 4 * J / 8 + J / 8 + 2 * e * J + e * K + 4 * K * (1 + a[18])))
+        jr = 1 if a[8] < 0 else J
+        return ("gemm", f"pw_bwd_tail{a[12]} (+maxpool bwd) {J}->{K}{' (rank-1 r)' if a[8] < 0 else ''} [{N},{S}]",
+                N * S * (4 * J + 4 * J / 8 + J / 8 + e * (J + jr) + e * K + 4 * K * (1 + a[18])))
     if base == "l3u_pw_bwd_weight":  # (dy, dyns, x, xns, part, N, J, K, S)
         N, J, K, S = a[5:9]
         return "gemm", f"pw_bwd_weight {J}x{K} [{N},{S}]", N * S * (4 * J + e * K)
@@ -260,13 +265,16 @@ def call_bytes(name, a):
         N, K, J, D, H, W = a[15:21]
         S = D * H * W
         sc = a[9] is not None
-        return ("dw", f"dwsep fwd (dw + pw{' + shortcut' if sc else ''}) [{N},{K}->{J},{D}x{H}x{W}]",
-                e * N * S * (K + J * (1 + sc) + (K if a[13] is not None else 0)) + 4 * K * (27 + J * (1 + sc)))
+        kin = 1 if a[1] < 0 else K   # a rank-1 input reads one channel
+        return ("dw", f"dwsep fwd (dw + pw{' + shortcut' if sc else ''}){' (rank-1 input)' if a[1] < 0 else ''} "
+                      f"[{N},{K}->{J},{D}x{H}x{W}]",
+                e * N * S * (kin + J * (1 + sc) + (K if a[13] is not None else 0)) + 4 * K * (27 + J * (1 + sc)))
     if base == "l3u_front_fwd":   # (x, xns, wdw, wpw, wsc, z1, y1, r, s1, so, xc, N, cout, d, h, w)
         N, co, d, h, w = a[11:16]
         S = d * h * w
-        return ("dw", f"front (1ch dw + 2 rank-1 pw) [{N},1->{co},{d}x{h}x{w}]",
-                4 * N * S + e * N * S * (1 + 2 * co + (1 if a[10] else 0)))
+        nw = (co if a[6] else 0) + (co if a[7] else 0)   # y1 / r not written when rank-1
+        return ("dw", f"front (1ch dw{' + 2 rank-1 pw' if nw else ''}) [{N},1->{co},{d}x{h}x{w}]",
+                4 * N * S + e * N * S * (1 + nw + (1 if a[10] else 0)))
     return None
 
 

@@ -55,7 +55,20 @@ typedef struct l3u_norm_src {
   unsigned long long seed;
   const int* step;             /* device step counter or NULL */
   float* rec_out;              /* [N][C][8] or NULL */
+  const float* rank1;          /* [C] or NULL: the normalised tensor is rank-1, channel c =
+                                  rank1[c] * ONE stored channel (see "rank-1 operands" below);
+                                  the record's slot 7 carries rank1[c] (0 otherwise) */
 } l3u_norm_src;
+
+/* Rank-1 operands (the first block's y1 = w1[c] * z1 and r = wsc[c] * x, unet3d.py:163-167 with
+ * one input channel): a NEGATIVE batch stride (-ns) on the normalised operand of
+ *   l3u_dwpw_fwd (x, with src/rec), l3u_norm_act_fwd / l3u_norm_act_pool_fwd (r),
+ *   l3u_norm_act_bwd_reduce[_r1|_up] (r), l3u_pw_bwd (y), l3u_pw_bwd_tail[_r1|_up] (yr) and
+ *   l3u_dw3_bwd (x, with rec)
+ * means that operand holds ONE channel per sample (batch stride ns) and channel c is
+ * record[c][7] * it, the float product the materialised tensor would hold (bit for bit).  The
+ * record's slot 7 is set when it is finalized from an l3u_norm_src with rank1 != NULL.  fp32
+ * entry points only.                                                                          */
 
 /* ---- depthwise 3x3x3 conv, stride 1, padding 1, no bias ------------------------------------
  * replaces nn.Conv3d(C, C, 3, 1, 1, groups=C, bias=False)
@@ -63,6 +76,7 @@ typedef struct l3u_norm_src {
  * w: [C][27].  rec != NULL fuses a = lrelu(scale*(x-mean) + shift) into the input load (the
  * InstanceNorm1 + LeakyReLU + Dropout3d that precede conv2.depthwise, unet3d.py:84-89).      */
 int l3u_dw3_nchunk(int N, int C, int D, int H, int W);   /* z/y chunks per (n, c) */
+int l3u_dw3_bwd_rank1(int N, int C, int D, int H, int W); /* 1: l3u_dw3_bwd takes a rank-1 x */
 int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float* rec,
                 const l3u_norm_src* src, float* y, long long y_nstride, int N, int C, int D,
                 int H, int W, hipStream_t stream);   /* src != NULL: finalize rec in-kernel */
@@ -384,7 +398,8 @@ int l3u_ftl_bwd(const float* p, const float* t, long long numel, const double* s
  * ([N][C][l3u_front_nblocks(S)][3], the l3u_pw_fwd format) from the channel's own moments.
  * Replaces three launches of unet3d.py:70-73,16-18 for the init_conv block.  W % 4 == 0.
  * x is the caller's fp32 input; x_copy != NULL also receives x in the storage type (the bf16
- * network's backward reads its input in bf16).                                                  */
+ * network's backward reads its input in bf16).  y1 / r == NULL (fp32): not written; the
+ * consumers take them as rank-1 operands (w1[c] * z1, w_sc[c] * x: see "Rank-1 operands").      */
 int l3u_front_nblocks(int S);
 int l3u_front_fwd(const float* x, long long x_nstride, const float* w_dw, const float* w1,
                   const float* wr, float* z1, float* y1, float* r, float* stat1, float* statr,

@@ -19,7 +19,8 @@ constexpr float kEps = 1e-5f;     // InstanceNorm3d eps (torch default)  unet3d.
 
 // Per-(n,c) InstanceNorm record written by in_finalize and read by every consumer.
 //  [0] mean  [1] rstd  [2] scale = k*gamma*rstd  [3] shift = k*beta
-//  [4] k (Dropout3d keep scale: 0 or 1/(1-p); 1 when no dropout)  [5] gamma  [6] beta  [7] 0
+//  [4] k (Dropout3d keep scale: 0 or 1/(1-p); 1 when no dropout)  [5] gamma  [6] beta
+//  [7] rank-1 scale of the normalised operand (l3u_norm_src.rank1[c]; 0: a full tensor)
 // With the dropout scale folded in, the forward transform is  a = lrelu(scale*(y - mean) + shift),
 // valid because lrelu(k*v) = k*lrelu(v) for k >= 0.  (y - mean) is formed first: folding the mean
 // into the shift cancels catastrophically when |mean| >> std and costs ~1e-5 relative accuracy.
@@ -245,7 +246,7 @@ L3U_DEV void record_from(const l3u_norm_src& s, int n, int c, int C, float cn, f
   r[4] = k;
   r[5] = g;
   r[6] = b;
-  r[7] = 0.f;
+  r[7] = s.rank1 ? s.rank1[c] : 0.f;
 }
 
 // Workgroup-level: wave 0 finalizes, broadcasts through `sh8` (8 floats of LDS) and, if asked,
@@ -286,6 +287,7 @@ L3U_DEV void block_record2(const l3u_norm_src& a, const l3u_norm_src& b, bool ha
     s.seed = q ? a.seed : b.seed;
     s.step = q ? a.step : b.step;
     s.rec_out = q ? a.rec_out : b.rec_out;
+    s.rank1 = q ? a.rank1 : b.rank1;
     float r[kRec];
     finalize_record(s, n, c, C, r);
     if ((threadIdx.x & 63) == 0) {

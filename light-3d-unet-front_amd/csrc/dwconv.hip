@@ -892,8 +892,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
   const int WQ = W >> 2, LP = W + kLPad, PP = (RB + 2) * LP, HW = H * W;
   const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
   const long long cofs = (long long)b.c * D * HW;
+  // xns < 0 (GL + MODE 1): a rank-1 input, channel c = rec[c][7] * one stored channel (l3u.h)
+  const bool xk = GL && MODE == 1 && xns < 0;
   const float* dzp = dz + (long long)b.n * dzns + cofs;
-  const T* xp = x + (long long)b.n * xns + cofs;
+  const T* xp = x + (long long)b.n * (xk ? -xns : xns) + (xk ? 0ll : cofs);
   float* dxp = dx + (long long)b.n * dxns + cofs;
   constexpr int GNB = L3U_DWG_PD + 1;                  // DMA ring buffers per tensor
   const int GPSD = (RB + 2) * W;                       // dZ elements per ring buffer (nq quads)
@@ -909,10 +911,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
     wp[t] = f2{w[b.c * 27 + tf], w[b.c * 27 + 9 + tf]};
     w2[t] = w[b.c * 27 + 18 + tf];
   }
-  float sc = 1.f, sh = 0.f, kk = 1.f, mean = 0.f, rstd = 1.f;
+  float sc = 1.f, sh = 0.f, kk = 1.f, mean = 0.f, rstd = 1.f, rks = 1.f;
   if (MODE == 1) {
     const float* r = rec + (long long)b.nc * kRec;
-    mean = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];
+    mean = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4]; rks = r[7];
   }
   if (!GL)
     for (int i = threadIdx.x; i < 4 * PP; i += blockDim.x) lds[i] = 0.f;
@@ -1036,6 +1038,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
       // hold zero-page values and get scale = shift = 0
       float zm = in_rng(za) ? 1.f : 0.f;
       pin(zm);   // formed here: keeps the compiler from hoisting 3 x (TZC+3) masks
+      if (xk) {   // rank-1 input: the channel's value, the materialised product bit for bit
+#pragma unroll
+        for (int r = 0; r < 3; ++r) rowa[r] *= rks;
+      }
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const float mr = zm * rv[r];
@@ -1477,6 +1483,10 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
   L3U_REQUIRE(dx != nullptr && dw_part != nullptr);
   L3U_REQUIRE(rec == nullptr || in_part != nullptr);
   L3U_REQUIRE(rec == nullptr || accumulate == 0);
+  // a rank-1 input (x_nstride < 0) is taken by the fp32 LDS-DMA single pass with rec only
+  const bool xr1 = x_nstride < 0;
+  L3U_REQUIRE(!xr1 || (E == 4 && rec != nullptr && !use_volume(D, H, W) && use_quads(H, W) &&
+                       dw_gl(qgeom(N, C, D, H, W), W, E) && L3U_DW_FUSED && L3U_DWG_MODE1));
   if (use_volume(D, H, W)) {   // data + weight gradient in one launch
     size_t lds2 = 2 * (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
     if (lds2 < 160 * sizeof(float)) lds2 = 160 * sizeof(float);
@@ -1548,6 +1558,13 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
 }
 
 }  // namespace
+
+// 1 when l3u_dw3_bwd takes a rank-1 input (x_nstride < 0) with rec at this shape (the fp32
+// LDS-DMA single pass, include/l3u.h "Rank-1 operands")
+extern "C" int l3u_dw3_bwd_rank1(int N, int C, int D, int H, int W) {
+  return N > 0 && C > 0 && !use_volume(D, H, W) && use_quads(H, W) && L3U_DW_FUSED && L3U_DWG_MODE1 &&
+         dw_gl(qgeom(N, C, D, H, W), W, 4);
+}
 
 extern "C" int l3u_dw3_nchunk(int N, int C, int D, int H, int W) {
   if (use_volume(D, H, W)) return 1;

@@ -79,13 +79,14 @@ L3U_DEV void w_fetch(Stage<T>& p, const T* plane, const WMap& m) {
 
 template <bool XF, typename T>
 L3U_DEV void w_commit(const Stage<T>& p, float* lplane, const WMap& m, bool in, float sc, float mu,
-                      float sh) {
+                      float sh, bool rk = false, float rks = 1.f) {
   const float keep = in ? 1.f : 0.f;
   sc *= keep;
   sh *= keep;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     f4 v = widen(p.v[k]);
+    if (XF && rk) v *= rks;   // rank-1 operand: the channel's value rank1[c] * the stored one
     if (XF) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(sc, v[i] - mu, sh));
@@ -130,27 +131,30 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
   float* taps = reinterpret_cast<float*>(sred + NT * 16 * 2);   // [K][27] (LTAP)
 
   // ---- per-channel setup: taps, InstanceNorm record, first two planes in flight
-  const T* xn = x + (long long)n * xns;
+  // xns < 0: a rank-1 input (XF only): one stored channel, channel c = record[c][7] * it
+  const bool rk = XF && xns < 0;
+  const T* xn = x + (long long)n * (rk ? -xns : xns);
+  const long long cst = rk ? 0 : S;   // channel stride of the staged input
   const WMap wm = w_map(y0, rows, H, W, WQ, l);
   const int zlo = max(0, z0 - 1), zhi = min(D - 1, z1);
   auto zc = [&](int zz) { return (long long)min(max(zz, zlo), zhi) * HW; };
   Stage<T> st[CPW][PD];
 #pragma unroll
   for (int i = 0; i < CPW; ++i) {
-    const T* xc = xn + (long long)(wv * CPW + i) * S;
+    const T* xc = xn + (long long)(wv * CPW + i) * cst;
 #pragma unroll
     for (int k = 0; k < PD; ++k) w_fetch(st[i][k], xc + zc(z0 - 1 + k), wm);
   }
-  float sc[CPW], mu[CPW], sh[CPW];
+  float sc[CPW], mu[CPW], sh[CPW], rks[CPW];
 #pragma unroll
   for (int i = 0; i < CPW; ++i) {
-    sc[i] = 1.f; mu[i] = 0.f; sh[i] = 0.f;
+    sc[i] = 1.f; mu[i] = 0.f; sh[i] = 0.f; rks[i] = 1.f;
     if (XF) {
       const int c = wv * CPW + i;
       if (has_src) {
         float rr[kRec];
         finalize_record(src, n, c, K, rr);
-        mu[i] = rr[0]; sc[i] = rr[2]; sh[i] = rr[3];
+        mu[i] = rr[0]; sc[i] = rr[2]; sh[i] = rr[3]; rks[i] = rr[7];
         if (zb == 0 && yb == 0 && l == 0 && src.rec_out) {
           float* o = src.rec_out + ((long long)n * K + c) * kRec;
 #pragma unroll
@@ -158,7 +162,7 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
         }
       } else {
         const float* rp = rec + ((long long)n * K + c) * kRec;
-        mu[i] = rp[0]; sc[i] = rp[2]; sh[i] = rp[3];
+        mu[i] = rp[0]; sc[i] = rp[2]; sh[i] = rp[3]; rks[i] = rp[7];
       }
     }
   }
@@ -202,8 +206,9 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
     for (int i = 0; i < CPW; ++i) {
       const int c = wv * CPW + i;
       float* buf = planes + ((size_t)c * NB + bi) * PP;
-      w_commit<XF == 1>(st[i][slot], buf, wm, zi >= zlo && zi <= zhi, sc[i], mu[i], sh[i]);
-      w_fetch(st[i][slot], xn + (long long)c * S + zc(zi + PD), wm);
+      w_commit<XF == 1>(st[i][slot], buf, wm, zi >= zlo && zi <= zhi, sc[i], mu[i], sh[i], rk,
+                        rks[i]);
+      w_fetch(st[i][slot], xn + (long long)c * cst + zc(zi + PD), wm);
     }
     __syncthreads();   // B1: planes visible; the previous step's GEMM reads of zt are done
     const bool fin = zo >= z0 && zo < z1;
@@ -365,6 +370,7 @@ int dwpw_fwd_impl(const T* x, long long x_nstride, const float* w_dw, const floa
   const DPGeom g = dp_geom(K, Nout, D, H, W, sc);
   L3U_REQUIRE(N > 0 && g.ok && x && w_dw && w_pw && y);
   L3U_REQUIRE(!sc || (r != nullptr && rec == nullptr && src == nullptr));
+  L3U_REQUIRE(x_nstride >= 0 || (sizeof(T) == 4 && (rec != nullptr || src != nullptr)));
   L3U_REQUIRE(x_nstride % 4 == 0 && y_nstride % 4 == 0 && (!sc || r_nstride % 4 == 0) &&
               (z == nullptr || z_nstride % 4 == 0));
   const l3u_norm_src zs{};

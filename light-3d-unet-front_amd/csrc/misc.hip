@@ -556,6 +556,7 @@ int grid_for(long long n, int per_block, int cap) {
 // the workgroup's voxels is (count, w*mean, w^2*M2) of the input channel, exactly.
 // One workgroup per 1024 voxels (a float4 quad per thread) of one sample.
 // xc != NULL: also a copy of x in the storage type (the bf16 network's backward reads x as bf16).
+// y1 / r may be NULL (fp32): they are never materialised, their consumers form them on load.
 template <typename T>
 __global__ __launch_bounds__(256) void front_fwd_kernel(
     const float* __restrict__ x, long long xns, const float* __restrict__ wdw,
@@ -589,10 +590,11 @@ __global__ __launch_bounds__(256) void front_fwd_kernel(
     }
     stv4(z1 + (long long)n * S + i0, zv);
     if (xc) stv4(xc + (long long)n * S + i0, xv);
-    for (int c = 0; c < C; ++c) {
-      stv4(r + ((long long)n * C + c) * S + i0, wr[c] * xv);
-      stv4(y1 + ((long long)n * C + c) * S + i0, w1[c] * zv);
-    }
+    // r / y1 == NULL: the consumers take them rank-1 (wr[c] * x, w1[c] * z1; include/l3u.h)
+    if (r != nullptr)
+      for (int c = 0; c < C; ++c) stv4(r + ((long long)n * C + c) * S + i0, wr[c] * xv);
+    if (y1 != nullptr)
+      for (int c = 0; c < C; ++c) stv4(y1 + ((long long)n * C + c) * S + i0, w1[c] * zv);
   }
   // the workgroup's moments of x and z1 (fixed-order sums: deterministic)
   const int cnt = min(1024, S - b * 1024);

@@ -36,19 +36,20 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
     int shortcut, T* __restrict__ out, long long ons, int C, int S) {
   __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
+  const bool rk = rns < 0;   // rank-1 residual: record_r[7] * one stored channel (include/l3u.h)
   const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
-  const T* rp = r + (long long)n * rns + (long long)c * S;
+  const T* rp = r + (long long)n * (rk ? -rns : rns) + (rk ? 0ll : (long long)c * S);
   T* op = out + (long long)n * ons + (long long)c * S;
   // the first tile is requested before the records are finalized (their partial-sum loads
   // overlap it); every later tile one iteration ahead
   const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4, istep = gridDim.x * 1024;
   f4 yv = {0.f, 0.f, 0.f, 0.f}, rv = yv;
   if (VEC && i0 < S) { yv = ldv4(yp + i0); rv = ldv4(rp + i0); }
-  float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f;
+  float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f, rks = 1.f;
   if (HAS_SRC) {
     block_record2(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh);
     m2 = sh[0]; a2 = sh[2]; b2 = sh[3];
-    if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; }
+    if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; rks = sh[15]; }
   } else {
     m2 = rec2[(long long)nc * kRec + 0];
     a2 = rec2[(long long)nc * kRec + 2];
@@ -57,12 +58,14 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
       mr = recr[(long long)nc * kRec + 0];
       ar = recr[(long long)nc * kRec + 2];
       br = recr[(long long)nc * kRec + 3];
+      rks = recr[(long long)nc * kRec + 7];
     }
   }
   if (VEC) {
     for (int i = i0; i < S; i += istep) {
       f4 yn = {0.f, 0.f, 0.f, 0.f}, rn = yn;
       if (i + istep < S) { yn = ldv4(yp + i + istep); rn = ldv4(rp + i + istep); }
+      if (rk) rv *= rks;
       f4 o;
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = lrelu(fmaf(a2, yv[q] - m2, b2) + fmaf(ar, rv[q] - mr, br));
@@ -72,7 +75,8 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
     }
   } else {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256)
-      st1(op + i, lrelu(fmaf(a2, ld1(yp + i) - m2, b2) + fmaf(ar, ld1(rp + i) - mr, br)));
+      st1(op + i, lrelu(fmaf(a2, ld1(yp + i) - m2, b2) +
+                        fmaf(ar, (rk ? rks * ld1(rp + i) : ld1(rp + i)) - mr, br)));
   }
 }
 
@@ -92,8 +96,9 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
   const long long S = (long long)D * H * W;
   const int Ho = H / 2, W4 = W / 4;
   const long long So = (long long)(D / 2) * Ho * (W / 2), Sp = So / 2;
+  const bool rk = rns < 0;   // rank-1 residual: record_r[7] * one stored channel (include/l3u.h)
   const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
-  const T* rp = r + (long long)n * rns + (long long)c * S;
+  const T* rp = r + (long long)n * (rk ? -rns : rns) + (rk ? 0ll : (long long)c * S);
   T* op = out + (long long)n * ons + (long long)c * S;
   T* pp = pooled + (long long)n * pns + (long long)c * So;
   unsigned short* ip = reinterpret_cast<unsigned short*>(idx + (long long)nc * So);
@@ -115,11 +120,11 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
     }
   };
   if (o0 < Sp) fetch(o0);
-  float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f;
+  float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f, rks = 1.f;
   if (HAS_SRC) {
     block_record2(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh);
     m2 = sh[0]; a2 = sh[2]; b2 = sh[3];
-    if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; }
+    if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; rks = sh[15]; }
   } else {
     m2 = rec2[(long long)nc * kRec + 0];
     a2 = rec2[(long long)nc * kRec + 2];
@@ -128,11 +133,16 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
       mr = recr[(long long)nc * kRec + 0];
       ar = recr[(long long)nc * kRec + 2];
       br = recr[(long long)nc * kRec + 3];
+      rks = recr[(long long)nc * kRec + 7];
     }
   }
   for (long long o = o0; o < Sp; o += ostep) {
     const long long base = base_of(o);
     f4 v[4];
+    if (rk) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rv[j] *= rks;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -177,15 +187,19 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
   __shared__ double red[4];
   const int nc = blockIdx.y, c = nc % C, n = nc / C, nb = gridDim.x;
   const float m2 = rec2[(long long)nc * kRec + 0], rs2 = rec2[(long long)nc * kRec + 1];
-  float mr = 0.f, rsr = 1.f;
-  if (recr) { mr = recr[(long long)nc * kRec + 0]; rsr = recr[(long long)nc * kRec + 1]; }
+  float mr = 0.f, rsr = 1.f, rks = 1.f;
+  if (recr) {
+    mr = recr[(long long)nc * kRec + 0]; rsr = recr[(long long)nc * kRec + 1];
+    rks = recr[(long long)nc * kRec + 7];
+  }
+  const bool rk = rns < 0;   // rank-1 residual: record_r[7] * one stored channel (include/l3u.h)
   const long long co = (long long)c * S;
   // dscale: rank-1 dout = dscale[c] * dz (dz one channel, l3u_outconv_bwd_dz)
   const float* dp = dout + (long long)n * dns + (dscale ? 0 : co);
   const float dsc = dscale ? dscale[c] : 1.f;
   const T* op = out + (long long)n * ons + co;
   const T* yp = y2 + (long long)n * y2ns + co;
-  const T* rp = r + (long long)n * rns + co;
+  const T* rp = r + (long long)n * (rk ? -rns : rns) + (rk ? 0ll : co);
   double s0 = 0.0, s1 = 0.0, s2 = 0.0;
   if (VEC) {
     // U grid-stride tiles per round: all their loads in flight before the first use, the sums
@@ -207,7 +221,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
                                pidx + (long long)nc * (S / 8), z, y, rm - y * W, H, W);
           }
           yv[u] = ldv4(yp + i);
-          if (recr) rv[u] = ldv4(rp + i);
+          if (recr) rv[u] = rk ? rks * ldv4(rp + i) : ldv4(rp + i);
         }
       }
 #pragma unroll
@@ -228,7 +242,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
       const float g = (dscale ? dsc * ld1(dp + i) : ld1(dp + i)) * lrelu_d(ld1(op + i));
       s0 += g;
       s1 += (double)g * ((ld1(yp + i) - m2) * rs2);
-      if (recr) s2 += (double)g * ((ld1(rp + i) - mr) * rsr);
+      if (recr) s2 += (double)g * (((rk ? rks * ld1(rp + i) : ld1(rp + i)) - mr) * rsr);
     }
   }
   s0 = block_sum256d(s0, red);
@@ -496,6 +510,7 @@ int norm_act_fwd_impl(const T* y2, long long y2_nstride, const float* rec2,
                       long long out_nstride, int N, int C, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
   L3U_REQUIRE(src2 ? (!shortcut || src_r) : (rec2 && (!shortcut || rec_r)));
+  L3U_REQUIRE(r_nstride >= 0 || (sizeof(T) == 4 && shortcut));   // rank-1 r: fp32 Conv1x1 shortcut
   const bool vec = S % 4 == 0 && y2_nstride % 4 == 0 && r_nstride % 4 == 0 && out_nstride % 4 == 0;
   dim3 grid(elem_blocks(S), N * C);
   const l3u_norm_src z{};
@@ -518,6 +533,7 @@ int norm_act_pool_fwd_impl(const T* y2, long long y2_nstride, const float* rec2,
   constexpr int E = (int)sizeof(T);
   L3U_REQUIRE(N > 0 && C > 0 && D >= 2 && H >= 2 && W >= 4);
   L3U_REQUIRE(src2 ? (!shortcut || src_r) : (rec2 && (!shortcut || rec_r)));
+  L3U_REQUIRE(r_nstride >= 0 || (sizeof(T) == 4 && shortcut));   // rank-1 r: fp32 Conv1x1 shortcut
   L3U_REQUIRE(!(D & 1) && !(H & 1) && !(W & 3) && y2_nstride % 4 == 0 && r_nstride % 4 == 0 &&
               out_nstride % 4 == 0 && pooled_nstride % 2 == 0 && ((uintptr_t)y2 & (4 * E - 1)) == 0 &&
               ((uintptr_t)r & (4 * E - 1)) == 0 && ((uintptr_t)out & (4 * E - 1)) == 0 &&
@@ -544,6 +560,7 @@ int norm_act_bwd_reduce_impl(const float* dout, long long dout_nstride, const T*
                              const float* dpool = nullptr, long long dpns = 0,
                              const unsigned char* pidx = nullptr, int H = 0, int W = 0) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
+  L3U_REQUIRE(r_nstride >= 0 || (sizeof(T) == 4 && rec_r != nullptr));   // rank-1 r: fp32 only
   const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
                    y2_nstride % 4 == 0 && r_nstride % 4 == 0;
   L3U_REQUIRE(dpool == nullptr || (vec && pidx && H % 2 == 0 && W % 4 == 0 && (S / (H * W)) % 2 == 0 &&
@@ -562,6 +579,7 @@ int norm_act_bwd_apply_impl(const float* dout, long long dout_nstride, const T* 
                             long long dy2_nstride, float* dr, long long dr_nstride, int N, int C,
                             int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
+  L3U_REQUIRE(r_nstride >= 0);   // no rank-1 residual on the split tail
   const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
                    y2_nstride % 4 == 0 && r_nstride % 4 == 0 && dy2_nstride % 4 == 0 &&
                    dr_nstride % 4 == 0;
@@ -579,6 +597,7 @@ int norm_act_bwd_impl(const float* dout, long long dout_nstride, const T* out,
                       double* part, float* dy2, long long dy2_nstride, float* dr,
                       long long dr_nstride, int N, int C, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0 && elem_blocks(S) == 1);
+  L3U_REQUIRE(r_nstride >= 0);   // no rank-1 residual on the split tail
   const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
                    y2_nstride % 4 == 0 && r_nstride % 4 == 0 && dy2_nstride % 4 == 0 &&
                    dr_nstride % 4 == 0;

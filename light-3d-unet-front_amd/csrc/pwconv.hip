@@ -619,13 +619,15 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       if (j < J && sd < s_hi) ov[jr] = ldv4(on + (long long)j * S + sd);
     }
   }
+  // yns < 0: a rank-1 normalised operand, channel j = rec[j][7] * one stored channel (l3u.h)
+  const bool yk = PRO && yns < 0;
   if (PRO) {
-    const T* yn = yin + (long long)n * yns;
+    const T* yn = yin + (long long)n * (yk ? -yns : yns);
 #pragma unroll
     for (int jr = 0; jr < JR; ++jr) {
       const int j = 4 * jr + lk;
       yv[jr] = f4{0.f, 0.f, 0.f, 0.f};
-      if (j < J && sd < s_hi) yv[jr] = ldv4(yn + (long long)j * S + sd);
+      if (j < J && sd < s_hi) yv[jr] = ldv4(yn + (yk ? 0ll : (long long)j * S) + sd);
     }
   }
   f4 xv[4][NK];
@@ -678,8 +680,9 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       o[2] = q[0];                 // mu
       o[3] = q[1];                 // rstd
       o[4] = (float)(t1 / S);      // M2
+      o[5] = q[7];                 // rank-1 scale of the operand (yns < 0)
     } else {
-      o[0] = o[1] = o[2] = o[3] = o[4] = 0.f;
+      o[0] = o[1] = o[2] = o[3] = o[4] = o[5] = 0.f;
     }
   }
   if (PRO) __syncthreads();
@@ -692,6 +695,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       const float* c = coef + j * 8;
       const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
       const bool ok = j < J && sd < s_hi;
+      if (yk) yv[jr] *= c[5];   // the materialised operand's value, bit for bit
       if (PRO == 2) {   // g = dout * lrelu'(out), then the tail InstanceNorm backward
 #pragma unroll
         for (int q = 0; q < 4; ++q) g[jr][q] = g[jr][q] * lrelu_d(ov[jr][q]);
@@ -1351,7 +1355,7 @@ int pw_bwd_weight_launch(const TD* dy, long long dy_nstride, const TX* x, long l
 #define L3U_CONVT_ONEPASS_MAX_S 8192
 #endif
 #ifndef L3U_PWBF_MIN_BLOCKS
-#define L3U_PWBF_MIN_BLOCKS 512
+#define L3U_PWBF_MIN_BLOCKS 256   // A/B r3: 256 -4 us/step (3 of 3), 128 +17 us, vs 512
 #endif
 
 // wide form: J a multiple of 64 (<= 128), any K; narrow form: J <= 32, K <= 64
@@ -1376,6 +1380,7 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
                                    dpns % 2 == 0 && ((uintptr_t)dpool & 7) == 0));
   L3U_REQUIRE(dout && out && yr && rec && tail_part && npart > 0 && (sel == 1 || sel == 2));
   L3U_REQUIRE(x && w && dx && part);
+  L3U_REQUIRE(yr_nstride >= 0 || sizeof(T) == 4);   // rank-1 yr: fp32 only
   const bool al = al4<float>(dout) && al4<T>(out) && al4<T>(yr) && al4<T>(x) && al4<float>(dx) &&
                   dout_nstride % 4 == 0 && out_nstride % 4 == 0 && yr_nstride % 4 == 0 &&
                   x_nstride % 4 == 0 && dx_nstride % 4 == 0;
@@ -1408,6 +1413,7 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
                 float* part, int N, int J, int K, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && l3u_pw_bwd_supported(J, K, S) && dy && x && w && dx && part);
   L3U_REQUIRE(y == nullptr || (rec && in_part && npart > 0));
+  L3U_REQUIRE(y_nstride >= 0 || (sizeof(T) == 4 && y != nullptr && !pw_bwd_wide(J)));   // rank-1 y
   const bool al = al4<float>(dy) && al4<T>(x) && al4<float>(dx) && (dy_nstride % 4 == 0) &&
                   (x_nstride % 4 == 0) && (dx_nstride % 4 == 0) &&
                   (y == nullptr || (al4<T>(y) && y_nstride % 4 == 0));

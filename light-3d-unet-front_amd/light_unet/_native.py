@@ -85,6 +85,7 @@ _SIGS = {
     "l3u_pw_bwd_tail_up": [P, L, P, L, P, P, L, P, L, P, P, I, I, P, L, P, P, L, I, P, I, I, I, I, I, I,
                            P],
     "l3u_dwpw_supported": [I, I, I, I, I, I],
+    "l3u_dw3_bwd_rank1": [I, I, I, I, I],
     "l3u_dwpw_stat_nsb": [I, I, I, I, I],
     "l3u_dwpw_fwd": [P, L, P, P, P, P, P, L, P, P, P, L, P, P, L, I, I, I, I, I, I, P],
 }
@@ -106,7 +107,8 @@ _QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_
             "l3u_pw_bwd_supported", "l3u_pw_bwd_nparts", "l3u_convt_bwd_fused_nparts",
             "l3u_norm_act_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks",
             "l3u_gconv3_nblocks", "l3u_gconv3_wgrad_nparts", "l3u_front_nblocks",
-            "l3u_ccl_nchunks", "l3u_dwpw_supported", "l3u_dwpw_stat_nsb"}
+            "l3u_ccl_nchunks", "l3u_dwpw_supported", "l3u_dwpw_stat_nsb",
+            "l3u_dw3_bwd_rank1"}
 
 _lib = None
 
@@ -119,7 +121,7 @@ class NormSrc(ctypes.Structure):
     """struct l3u_norm_src (include/l3u.h): where a consumer kernel finalizes an InstanceNorm
     record from.  Pass `norm_src_ptr(s)`; keep the object alive across the call."""
     _fields_ = [("stat_part", P), ("nsb", I), ("layer", I), ("gamma", P), ("beta", P),
-                ("drop_p", F), ("seed", U64), ("step", P), ("rec_out", P)]
+                ("drop_p", F), ("seed", U64), ("step", P), ("rec_out", P), ("rank1", P)]
 
 
 class AugParam(ctypes.Structure):

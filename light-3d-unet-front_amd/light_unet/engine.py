@@ -43,11 +43,17 @@ _RANK1 = os.environ.get("L3U_RANK1", "1") != "0"
 # the encoder's MaxPool3d backward formed in the loads of the consuming block tail (no
 # l3u_maxpool2_bwd launch, no level-output gradient tensor); L3U_POOLFOLD=0 disables
 _POOLFOLD = os.environ.get("L3U_POOLFOLD", "1") != "0"
+# the first block's rank-1 activations (y1 = w1[c] * z1, r = wsc[c] * x: one input channel) are
+# never materialised; their consumers form them on load (include/l3u.h "Rank-1 operands", fp32
+# only); L3U_FRONT_R1=0 writes them as tensors
+_FRONT_R1 = os.environ.get("L3U_FRONT_R1", "1") != "0"
 
 
 class V:
     """A strided activation view: channel c of sample n at t[off + n*ns + c*S].  scale (a device
-    pointer to C floats): a rank-1 gradient, channel c = scale[c] * the one stored channel."""
+    pointer to C floats): a rank-1 tensor, channel c = scale[c] * the one stored channel (a
+    gradient: scale passed to the kernel; an activation: the kernel reads the scale from the
+    record, `sns` is the batch stride it is given, negative for a rank-1 operand)."""
     __slots__ = ("t", "off", "ns", "C", "scale", "pool")
 
     def __init__(self, t, off, ns, C, scale=None, pool=None):
@@ -58,6 +64,10 @@ class V:
     @property
     def p(self):
         return self.t.data_ptr() + self.t.element_size() * self.off
+
+    @property
+    def sns(self):
+        return -self.ns if self.scale is not None else self.ns
 
 
 def conv_kinds(cin, cout, use_depthwise_separable=True, use_grouped=True, groups=8):
@@ -401,11 +411,12 @@ class UNetEngine:
         sv["blk"] = blk
         return p, (sv if save else None)
 
-    def _src(self, flat, norm_prefix, stat_off, nsb, rec_out, drop, cptr, layer):
-        """l3u_norm_src for an InstanceNorm whose statistics partials sit at stat_off."""
+    def _src(self, flat, norm_prefix, stat_off, nsb, rec_out, drop, cptr, layer, rank1=None):
+        """l3u_norm_src for an InstanceNorm whose statistics partials sit at stat_off (rank1: the
+        per-channel scale of a rank-1 normalised operand, recorded in the record's slot 7)."""
         return nat.NormSrc(self.fwd_arena.ptr(stat_off), nsb, layer,
                            self._w(flat, norm_prefix + "weight"), self._w(flat, norm_prefix + "bias"),
-                           float(drop), self.seed, cptr or 0, rec_out)
+                           float(drop), self.seed, cptr or 0, rec_out, rank1 or 0)
 
     @staticmethod
     def _front_ok(x, dims):
@@ -441,21 +452,30 @@ class UNetEngine:
             # rank-1 channel maps) and their IN statistics in one launch (bf16: plus the bf16
             # copy of the input the backward reads)
             nbf = nat.query("l3u_front_nblocks", S)
-            r, z1, y1 = e(N, cout, S), e(N, cin, S), e(N, cout, S)
+            r1 = self._front_rank1(x, N, cout, dims)
+            z1 = e(N, cin, S)
+            r = None if r1 else e(N, cout, S)
+            y1 = None if r1 else e(N, cout, S)
             xc = e(N, cin, S) if self.bf16 else None
             so = self.fwd_arena.alloc(N * cout * nbf * 3)
             s1 = self.fwd_arena.alloc(N * cout * nbf * 3)
             self._call("l3u_front_fwd", x.p, x.ns, self._w(flat, pre + "conv1.depthwise.weight"),
                        self._w(flat, pre + "conv1.pointwise.weight"),
-                       self._w(flat, pre + "shortcut.0.weight"), z1.data_ptr(), y1.data_ptr(),
-                       r.data_ptr(), self.fwd_arena.ptr(s1), self.fwd_arena.ptr(so),
-                       xc.data_ptr() if xc is not None else None, N, cout, d, h, w, st)
+                       self._w(flat, pre + "shortcut.0.weight"), z1.data_ptr(),
+                       y1.data_ptr() if y1 is not None else None,
+                       r.data_ptr() if r is not None else None, self.fwd_arena.ptr(s1),
+                       self.fwd_arena.ptr(so), xc.data_ptr() if xc is not None else None, N, cout,
+                       d, h, w, st)
             if xc is not None:
                 sv["x"] = V(xc, 0, cin * S, cin)
-            src_r = self._src(flat, pre + "shortcut.1.", so, nbf, rec_r, 0.0, cptr, 0)
-            rv = V(r, 0, cout * S, cout)
+            src_r = self._src(flat, pre + "shortcut.1.", so, nbf, rec_r, 0.0, cptr, 0,
+                              rank1=self._w(flat, pre + "shortcut.0.weight") if r1 else None)
+            # rank-1: r = wsc[c] * x and y1 = w1[c] * z1 formed on load by every consumer
+            rv = V(x.t, x.off, x.ns, cout, scale=self._w(flat, pre + "shortcut.0.weight")) if r1 \
+                else V(r, 0, cout * S, cout)
             sv["r"] = rv
-            src1 = self._src(flat, pre + "norm1.", s1, nbf, rec1, drop, cptr, 1 + layer)
+            src1 = self._src(flat, pre + "norm1.", s1, nbf, rec1, drop, cptr, 1 + layer,
+                             rank1=self._w(flat, pre + "conv1.pointwise.weight") if r1 else None)
         elif _PAIR_PW and shortcut and S % 4 == 0 and x.ns % 4 == 0:
             # conv1.depthwise, then the shortcut and conv1.pointwise (same K -> Nout over the
             # same volume) as one paired GEMM launch
@@ -497,16 +517,19 @@ class UNetEngine:
             src1 = self._src(flat, pre + "norm1.", s1, nsb, rec1, drop, cptr, 1 + layer)
         z2 = e(N, cout, S)
         y2 = e(N, cout, S)
+        # y1 as conv2 reads it: a tensor, or rank-1 (z1 with a negative batch stride)
+        y1v = V(z1, 0, S, cout, scale=True) if y1 is None else V(y1, 0, cout * S, cout)
         if _DWPW and S >= _DWPW_MIN_S and nat.query("l3u_dwpw_supported", cout, cout, d, h, w, 0):
             # conv2 = depthwise (IN1 + LeakyReLU + Dropout3d on load) + pointwise in one launch
             nsb2 = nat.query("l3u_dwpw_stat_nsb", cout, cout, d, h, w)
             s2 = self.fwd_arena.alloc(N * cout * nsb2 * 3)
-            self._call("l3u_dwpw_fwd", y1.data_ptr(), cout * S,
+            self._call("l3u_dwpw_fwd", y1v.p, y1v.sns,
                        self._w(flat, pre + "conv2.depthwise.weight"), None, nat.norm_src_ptr(src1),
                        self._w(flat, pre + "conv2.pointwise.weight"), y2.data_ptr(), cout * S,
                        self.fwd_arena.ptr(s2), None, None, 0, None, z2.data_ptr(), cout * S, N, cout,
                        cout, d, h, w, st)
         else:
+            assert y1 is not None, "rank-1 y1 needs the fused conv2 (l3u_dwpw_fwd)"
             self._call("l3u_dw3_fwd", y1.data_ptr(), cout * S,
                        self._w(flat, pre + "conv2.depthwise.weight"), None, nat.norm_src_ptr(src1),
                        z2.data_ptr(), cout * S, N, cout, d, h, w, st)
@@ -517,16 +540,29 @@ class UNetEngine:
         src2 = self._src(flat, pre + "norm2.", s2, nsb2, rec2, 0.0, cptr, 0)
         if pool is None:
             self._call("l3u_norm_act_fwd", y2.data_ptr(), cout * S, None, nat.norm_src_ptr(src2),
-                       rv.p, rv.ns, None, nat.norm_src_ptr(src_r), 1 if shortcut else 0, out.p,
+                       rv.p, rv.sns, None, nat.norm_src_ptr(src_r), 1 if shortcut else 0, out.p,
                        out.ns, N, cout, S, st)
         else:
             pooled, idx = pool
             self._call("l3u_norm_act_pool_fwd", y2.data_ptr(), cout * S, None,
-                       nat.norm_src_ptr(src2), rv.p, rv.ns, None, nat.norm_src_ptr(src_r),
+                       nat.norm_src_ptr(src2), rv.p, rv.sns, None, nat.norm_src_ptr(src_r),
                        1 if shortcut else 0, out.p, out.ns, pooled.data_ptr(), cout * (S // 8),
                        idx.data_ptr(), N, cout, d, h, w, st)
-        sv.update(z1=z1, y1=y1, z2=z2, y2=y2, dims=dims, shortcut=shortcut)
+        sv.update(z1=z1, y1=y1, y1v=y1v, z2=z2, y2=y2, dims=dims, shortcut=shortcut)
         return sv
+
+    def _front_rank1(self, x, N, cout, dims):
+        """The first block's y1 / r stay rank-1 (never materialised) when every consumer takes a
+        rank-1 operand at this shape: the fused conv2 (l3u_dwpw_fwd), the LDS-DMA IN-fused
+        depthwise backward, the fused pointwise backwards and the fused block tail (fp32)."""
+        d, h, w = dims
+        S = d * h * w
+        return (_FRONT_R1 and not self.bf16 and self._front_ok(x, dims) and _DWPW and S >= _DWPW_MIN_S
+                and nat.query("l3u_dwpw_supported", cout, cout, d, h, w, 0)
+                and nat.query("l3u_dw3_bwd_rank1", N, cout, d, h, w)
+                and nat.query("l3u_pw_bwd_supported", cout, 1, S)
+                and _TAIL_FUSE and nat.query("l3u_norm_act_nblocks", S) > 1 and cout <= 32
+                and nat.query("l3u_pw_bwd_supported", cout, cout, S))
 
     def _conv_w(self, flat, pre, which):
         kind = self.kinds[pre][which - 1]
@@ -771,19 +807,20 @@ class UNetEngine:
             self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.bias", f64=1)
             if dout.scale is not None:   # rank-1 dout (l3u_outconv_bwd_dz)
                 self._call("l3u_norm_act_bwd_reduce_r1", dout.p, dout.ns, dout.scale, out.p, out.ns,
-                           y2.data_ptr(), cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S,
+                           y2.data_ptr(), cout * S, rec2, rv.p, rv.sns, rec_r, A.ptr(pn), N, cout, S,
                            st)
             elif dout.pool is not None:   # skip gradient + the folded MaxPool3d backward
                 dpool, idx, (d, h, w) = dout.pool
                 self._call("l3u_norm_act_bwd_reduce_up", dout.p, dout.ns, dpool.data_ptr(),
                            cout * (S // 8), idx.data_ptr(), out.p, out.ns, y2.data_ptr(), cout * S,
-                           rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, d, h, w, st)
+                           rec2, rv.p, rv.sns, rec_r, A.ptr(pn), N, cout, d, h, w, st)
             else:
                 self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(),
-                           cout * S, rec2, rv.p, rv.ns, rec_r, A.ptr(pn), N, cout, S, st)
+                           cout * S, rec2, rv.p, rv.sns, rec_r, A.ptr(pn), N, cout, S, st)
             return pn, nb
         assert dout.scale is None and dout.pool is None, "a formed-on-load output gradient " \
             "needs the fused block tail"
+        assert rv.scale is None, "a rank-1 residual needs the fused block tail"
         dy2 = self._empty(N, cout, S, device=dev)
         if shortcut:
             dr = self._empty(N, cout, S, device=dev)
@@ -871,7 +908,8 @@ class UNetEngine:
         rec_r, rec1, rec2 = recs[0].data_ptr(), recs[1].data_ptr(), recs[2].data_ptr()
         shortcut = sv["shortcut"]
         rv = sv["r"] if shortcut else x
-        y2, z2, y1, z1 = sv["y2"], sv["z2"], sv["y1"], sv["z1"]
+        y2, z2, z1 = sv["y2"], sv["z2"], sv["z1"]
+        y1v = sv.get("y1v") or V(sv["y1"], 0, cout * S, cout)   # rank-1: z1, negative stride
         # (1) block tail: out = lrelu(IN2(y2) + residual)
         fused = self._tail_fusable(sv, cin, cout, S)
         dz2 = e(N, cout, S)
@@ -893,7 +931,7 @@ class UNetEngine:
         pi1 = A.alloc(2 * cout * N * nch * 2)          # fp64 partials
         pid = pi1 // 2
         dpre = e(N, cout, S)
-        self._call("l3u_dw3_bwd", dz2.data_ptr(), cout * S, y1.data_ptr(), cout * S,
+        self._call("l3u_dw3_bwd", dz2.data_ptr(), cout * S, y1v.p, y1v.sns,
                    self._w(flat, pre + "conv2.depthwise.weight"), rec1, dpre.data_ptr(), cout * S, 0,
                    A.ptr(pd2), A.ptr(pi1), N, cout, d, h, w, st)
         self._seg_dw(pd2, N * nch, cout, pre + "conv2.depthwise.weight")
@@ -905,10 +943,11 @@ class UNetEngine:
         dpv = V(dpre, 0, cout * S, cout)
         name1 = pre + "conv1.pointwise.weight"
         if nat.query("l3u_pw_bwd_supported", cout, cin, S):
-            self._pw_bwd(flat, dpv, (y1.data_ptr(), cout * S, rec1, A.ptr(pi1), nch),
+            self._pw_bwd(flat, dpv, (y1v.p, y1v.sns, rec1, A.ptr(pi1), nch),
                          V(z1, 0, cin * S, cin), name1, V(dz1, 0, cin * S, cin), 0, N, S, st)
         else:
-            self._call("l3u_in_bwd_apply", dpre.data_ptr(), cout * S, y1.data_ptr(), cout * S, rec1,
+            assert y1v.scale is None
+            self._call("l3u_in_bwd_apply", dpre.data_ptr(), cout * S, y1v.p, y1v.ns, rec1,
                        A.ptr(pi1), nch, dpre.data_ptr(), cout * S, N, cout, S, st)
             self._pw_bwd(flat, dpv, None, V(z1, 0, cin * S, cin), name1, V(dz1, 0, cin * S, cin), 0,
                          N, S, st)
@@ -964,17 +1003,17 @@ class UNetEngine:
         npw = nat.query("l3u_pw_bwd_nparts", N, J, K, S)
         part = A.alloc(npw * J * K)
         if dout.scale is not None:   # rank-1 dout (l3u_outconv_bwd_dz)
-            self._call("l3u_pw_bwd_tail_r1", dout.p, dout.ns, dout.scale, out.p, out.ns, yr.p, yr.ns,
+            self._call("l3u_pw_bwd_tail_r1", dout.p, dout.ns, dout.scale, out.p, out.ns, yr.p, yr.sns,
                        rec, A.ptr(pn), ntp, sel, x.p, x.ns, self._w(flat, name), dx.p, dx.ns,
                        accumulate, A.ptr(part), N, J, K, S, st)
         elif dout.pool is not None:   # skip gradient + the folded MaxPool3d backward
             dpool, idx, (d, h, w) = dout.pool
             self._call("l3u_pw_bwd_tail_up", dout.p, dout.ns, dpool.data_ptr(), J * (S // 8),
-                       idx.data_ptr(), out.p, out.ns, yr.p, yr.ns, rec, A.ptr(pn), ntp, sel, x.p,
+                       idx.data_ptr(), out.p, out.ns, yr.p, yr.sns, rec, A.ptr(pn), ntp, sel, x.p,
                        x.ns, self._w(flat, name), dx.p, dx.ns, accumulate, A.ptr(part), N, J, K, d, h,
                        w, st)
         else:
-            self._call("l3u_pw_bwd_tail", dout.p, dout.ns, out.p, out.ns, yr.p, yr.ns, rec,
+            self._call("l3u_pw_bwd_tail", dout.p, dout.ns, out.p, out.ns, yr.p, yr.sns, rec,
                        A.ptr(pn), ntp, sel, x.p, x.ns, self._w(flat, name), dx.p, dx.ns, accumulate,
                        A.ptr(part), N, J, K, S, st)
         self._seg(part, npw, J * K, 1, J * K, name)

@@ -298,14 +298,19 @@ def test_trainstep_data_parallel_two_ranks(cuda, tmp_path):
 
 @pytest.mark.parametrize("switch,fixture", [("_RANK1", "model_b2_32.npz"),
                                             ("_POOLFOLD", "model_b2_32.npz"),
-                                            ("_POOLFOLD", "model_b1_48.npz")])
+                                            ("_POOLFOLD", "model_b1_48.npz"),
+                                            ("_FRONT_R1", "model_b1_48.npz")])
 def test_formed_on_load_gradients_bitwise(cuda, golden, switch, fixture):
     """Output gradients formed on load give bitwise the gradients of the materialised tensors,
     for the FocalTversky and the given-dL/dp forms of the backward:
     _RANK1: out_conv is rank-1 (unet3d.py:201), the last block gets d(pre-sigmoid) and the
     out_conv weight (l3u_outconv_bwd_dz + the _r1 tail kernels);
     _POOLFOLD: the encoder levels' MaxPool3d backward (unet3d.py:104) inside the consuming block
-    tail's loads (the _up tail kernels; at 48^3 the 48^3 and 24^3 levels)."""
+    tail's loads (the _up tail kernels; at 48^3 the 48^3 and 24^3 levels);
+    _FRONT_R1: the first block's rank-1 activations y1 = w1[c] * z1 and r = wsc[c] * x
+    (unet3d.py:163-167, one input channel) formed on load by the fused conv2, the block tail,
+    the IN-fused depthwise backward and the pointwise backwards instead of stored (48^3: the
+    shapes where all of them take the rank-1 form).  The output is compared too."""
     import light_unet.engine as E
     from light_unet.models.unet3d import Lightweight3DUNet
     from light_unet.train_step import TrainStep
@@ -328,8 +333,10 @@ def test_formed_on_load_gradients_bitwise(cuda, golden, switch, fixture):
             gg = torch.zeros_like(ts.gflat)
             m.engine.backward(ts.flat, gg, sv, dp)
             torch.cuda.synchronize()
-            res.append((g1, gg, ts.loss.clone()))
+            res.append((g1, gg, ts.loss.clone(), p.clone()))
+            if switch == "_FRONT_R1":
+                assert (sv["blk"]["init_conv."]["y1"] is None) == on
         finally:
             setattr(E, switch, True)
-    for name, a, b in zip(("ftl grad", "dp grad", "loss"), *res):
+    for name, a, b in zip(("ftl grad", "dp grad", "loss", "output"), *res):
         assert torch.equal(a, b), (name, (a - b).abs().max().item())
