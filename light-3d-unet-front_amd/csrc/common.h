@@ -57,6 +57,20 @@ L3U_DEV float ld1(const bf16* p) { return (float)*p; }
 L3U_DEV void st1(float* p, float v) { *p = v; }
 L3U_DEV void st1(bf16* p, float v) { *p = (bf16)v; }
 
+// a * b rounded on its own, never contracted into a following add (an FMA would round once and
+// differ from the product that was stored: the rank-1 operands must equal the materialised tensor)
+// (__fmul_rn is a plain contractible multiply on this toolchain: the empty asm fences the product)
+L3U_DEV float mul_rn(float a, float b) {
+  float p = a * b;
+  asm volatile("" : "+v"(p));
+  return p;
+}
+L3U_DEV f4_t mul_rn(f4_t v, float s) {
+  f4_t p = v * s;
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
 L3U_DEV float lrelu(float v) { return v > 0.f ? v : v * kSlope; }
 L3U_DEV float lrelu_d(float pre) { return pre > 0.f ? 1.f : kSlope; }   // torch: x > 0 ? 1 : slope
 

@@ -879,7 +879,7 @@ L3U_DEV void dw_wait_vm() {   // at most NOUT vector-memory operations still out
 // bf16 A on the LDS-DMA path: the DMA moves raw bf16, 8 elements (two quads) per lane, so one
 // slot per plane covers the 128-quad tile (needs an even quad count per row, W % 8 == 0, so a
 // lane's pair never straddles a row); that LDS image is bf16 and its rows widen at the read.
-template <typename T, int MODE, int TZC, bool GL = false>
+template <typename T, int MODE, int TZC, bool GL = false, bool XR1 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE == 1 ? L3U_DWG_WAVES1 : L3U_DWG_WAVES) : L3U_DWP_WAVES))) void dw3p_bwd_kernel(
     const float* __restrict__ dz, long long dzns, const T* __restrict__ x, long long xns,
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
@@ -892,8 +892,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
   const int WQ = W >> 2, LP = W + kLPad, PP = (RB + 2) * LP, HW = H * W;
   const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
   const long long cofs = (long long)b.c * D * HW;
-  // xns < 0 (GL + MODE 1): a rank-1 input, channel c = rec[c][7] * one stored channel (l3u.h)
-  const bool xk = GL && MODE == 1 && xns < 0;
+  // XR1 (xns < 0, GL + MODE 1): a rank-1 input, channel c = rec[c][7] * one stored channel
+  // (include/l3u.h); a template flag so that the other variants keep their schedule
+  constexpr bool xk = GL && MODE == 1 && XR1;
   const float* dzp = dz + (long long)b.n * dzns + cofs;
   const T* xp = x + (long long)b.n * (xk ? -xns : xns) + (xk ? 0ll : cofs);
   float* dxp = dx + (long long)b.n * dxns + cofs;
@@ -1040,7 +1041,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
       pin(zm);   // formed here: keeps the compiler from hoisting 3 x (TZC+3) masks
       if (xk) {   // rank-1 input: the channel's value, the materialised product bit for bit
 #pragma unroll
-        for (int r = 0; r < 3; ++r) rowa[r] *= rks;
+        for (int r = 0; r < 3; ++r) rowa[r] = mul_rn(rowa[r], rks);
       }
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
@@ -1515,7 +1516,15 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
       g.RPW, g.ny, g.TZ, g.nz); } while (0)
 #define DWPB_T(M_) do { TZ24(DWPB(M_, 24)) if (g.TZ == 16) DWPB(M_, 16); else if (g.TZ == 8) DWPB(M_, 8); else if (g.TZ == 4) DWPB(M_, 4); else DWPB(M_, 2); } while (0)
-      if (rec) DWPB_T(1);
+      if (xr1) {   // rank-1 input: the LDS-DMA IN-fused variant only (checked above)
+        if constexpr (E == 4) {
+#define DWPR(T_) hipLaunchKernelGGL((dw3p_bwd_kernel<T, 1, T_, true, true>), grid, block, lds, stream, dz, \
+      dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
+      g.RPW, g.ny, g.TZ, g.nz)
+          TZ24(DWPR(24)) if (g.TZ == 16) DWPR(16); else if (g.TZ == 8) DWPR(8); else if (g.TZ == 4) DWPR(4); else DWPR(2);
+#undef DWPR
+        }
+      } else if (rec) DWPB_T(1);
       else if (accumulate) DWPB_T(2);
       else DWPB_T(0);
 #undef DWPB_T

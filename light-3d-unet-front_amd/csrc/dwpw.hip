@@ -86,7 +86,7 @@ L3U_DEV void w_commit(const Stage<T>& p, float* lplane, const WMap& m, bool in, 
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     f4 v = widen(p.v[k]);
-    if (XF && rk) v *= rks;   // rank-1 operand: the channel's value rank1[c] * the stored one
+    if (XF && rk) v = mul_rn(v, rks);   // rank-1 operand: the channel's value rank1[c] * the stored one
     if (XF) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = lrelu(fmaf(sc, v[i] - mu, sh));
@@ -100,7 +100,7 @@ L3U_DEV void w_commit(const Stage<T>& p, float* lplane, const WMap& m, bool in, 
 // XF: IN-on-load input (conv2); CPW: channels per wave (K = 16 * CPW, 16 waves); NC: output
 // channel blocks of 16 (Nout = 16 * NC); SC: also the Conv1x1 shortcut R = Wsc . X (XF = 0);
 // TZC: output planes per slab.  Grid: N * nz * ny workgroups of 1024 threads.
-template <typename T, int XF, int CPW, int NC, int SC, int TZC>
+template <typename T, int XF, int CPW, int NC, int SC, int TZC, bool XR1 = false>
 __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
     const T* __restrict__ x, long long xns, const float* __restrict__ wdw,
     const float* __restrict__ rec, l3u_norm_src src, int has_src,
@@ -131,8 +131,8 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
   float* taps = reinterpret_cast<float*>(sred + NT * 16 * 2);   // [K][27] (LTAP)
 
   // ---- per-channel setup: taps, InstanceNorm record, first two planes in flight
-  // xns < 0: a rank-1 input (XF only): one stored channel, channel c = record[c][7] * it
-  const bool rk = XF && xns < 0;
+  // XR1 (xns < 0): a rank-1 input (XF only): one stored channel, channel c = record[c][7] * it
+  constexpr bool rk = XF && XR1;
   const T* xn = x + (long long)n * (rk ? -xns : xns);
   const long long cst = rk ? 0 : S;   // channel stride of the staged input
   const WMap wm = w_map(y0, rows, H, W, WQ, l);
@@ -370,7 +370,7 @@ int dwpw_fwd_impl(const T* x, long long x_nstride, const float* w_dw, const floa
   const DPGeom g = dp_geom(K, Nout, D, H, W, sc);
   L3U_REQUIRE(N > 0 && g.ok && x && w_dw && w_pw && y);
   L3U_REQUIRE(!sc || (r != nullptr && rec == nullptr && src == nullptr));
-  L3U_REQUIRE(x_nstride >= 0 || (sizeof(T) == 4 && (rec != nullptr || src != nullptr)));
+  L3U_REQUIRE(x_nstride >= 0 || (sizeof(T) == 4 && w_sc == nullptr && (rec != nullptr || src != nullptr)));
   L3U_REQUIRE(x_nstride % 4 == 0 && y_nstride % 4 == 0 && (!sc || r_nstride % 4 == 0) &&
               (z == nullptr || z_nstride % 4 == 0));
   const l3u_norm_src zs{};
@@ -379,15 +379,19 @@ int dwpw_fwd_impl(const T* x, long long x_nstride, const float* w_dw, const floa
   const int NB = 2 + sc;
   const size_t lds = dp_lds(K, NB, g.RB, W);
   dim3 grid(N * g.nz * g.ny), block(1024);
-#define DPF(XF_, CPW_, NC_, SC_) hipLaunchKernelGGL((dwpw_fwd_kernel<T, XF_, CPW_, NC_, SC_, L3U_DWPW_TZ>), grid, \
+#define DPF0(XF_, CPW_, NC_, SC_, R_) hipLaunchKernelGGL((dwpw_fwd_kernel<T, XF_, CPW_, NC_, SC_, L3U_DWPW_TZ, R_>), grid, \
       block, lds, stream, x, x_nstride, w_dw, rec, s, src ? 1 : 0, w_pw, y, y_nstride, y_stat, w_sc, r, \
       r_nstride, r_stat, z, z_nstride, D, H, W, g.RB, g.ny, g.nz)
+#define DPF(XF_, CPW_, NC_, SC_) DPF0(XF_, CPW_, NC_, SC_, false)
 #define DPF_C(CPW_, NC_) do { if (sc) DPF(0, CPW_, NC_, 1); else if (xf) DPF(1, CPW_, NC_, 0); \
                               else DPF(0, CPW_, NC_, 0); } while (0)
-  if (Nout == 16) DPF_C(1, 1);
+  if (x_nstride < 0) {   // rank-1 input (fp32, XF: checked above)
+    if constexpr (sizeof(T) == 4) { if (Nout == 16) DPF0(1, 1, 1, 0, true); else DPF0(1, 1, 2, 0, true); }
+  } else if (Nout == 16) DPF_C(1, 1);
   else DPF_C(1, 2);
 #undef DPF_C
 #undef DPF
+#undef DPF0
   L3U_CHECK_LAUNCH();
 }
 

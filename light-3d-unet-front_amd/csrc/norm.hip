@@ -29,14 +29,15 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(l3u_norm_src src, int 
 // out = lrelu(scale2*(y2-mean2) + shift2 + R),  R = r (identity) or scale_r*(r-mean_r) + shift_r.
 // With HAS_SRC the records are finalized here from the GEMM partials (no in_finalize launch);
 // workgroup x == 0 of each (n, c) stores them for the backward.
-template <typename T, bool VEC, bool HAS_SRC>
+template <typename T, bool VEC, bool HAS_SRC, bool RK = false>
 __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
     const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2, l3u_norm_src src2,
     const T* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
     int shortcut, T* __restrict__ out, long long ons, int C, int S) {
   __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
-  const bool rk = rns < 0;   // rank-1 residual: record_r[7] * one stored channel (include/l3u.h)
+  // RK (rns < 0): rank-1 residual, record_r[7] * one stored channel (include/l3u.h)
+  constexpr bool rk = RK;
   const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
   const T* rp = r + (long long)n * (rk ? -rns : rns) + (rk ? 0ll : (long long)c * S);
   T* op = out + (long long)n * ons + (long long)c * S;
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
     for (int i = i0; i < S; i += istep) {
       f4 yn = {0.f, 0.f, 0.f, 0.f}, rn = yn;
       if (i + istep < S) { yn = ldv4(yp + i + istep); rn = ldv4(rp + i + istep); }
-      if (rk) rv *= rks;
+      if (rk) rv = mul_rn(rv, rks);
       f4 o;
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = lrelu(fmaf(a2, yv[q] - m2, b2) + fmaf(ar, rv[q] - mr, br));
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
   } else {
     for (int i = blockIdx.x * 256 + threadIdx.x; i < S; i += gridDim.x * 256)
       st1(op + i, lrelu(fmaf(a2, ld1(yp + i) - m2, b2) +
-                        fmaf(ar, (rk ? rks * ld1(rp + i) : ld1(rp + i)) - mr, br)));
+                        fmaf(ar, (rk ? mul_rn(rks, ld1(rp + i)) : ld1(rp + i)) - mr, br)));
   }
 }
 
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
 // (four float4 rows), stores them and the two window maxima (float2) with their argmax bytes.
 // Same scan order and comparison as maxpool2_fwd_v_kernel (misc.hip).  Needs even D, H and
 // W % 4 == 0.
-template <typename T, bool HAS_SRC>
+template <typename T, bool HAS_SRC, bool RK = false>
 __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
     const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2, l3u_norm_src src2,
     const T* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
   const long long S = (long long)D * H * W;
   const int Ho = H / 2, W4 = W / 4;
   const long long So = (long long)(D / 2) * Ho * (W / 2), Sp = So / 2;
-  const bool rk = rns < 0;   // rank-1 residual: record_r[7] * one stored channel (include/l3u.h)
+  constexpr bool rk = RK;   // rank-1 residual (rns < 0): record_r[7] * one stored channel
   const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
   const T* rp = r + (long long)n * (rk ? -rns : rns) + (rk ? 0ll : (long long)c * S);
   T* op = out + (long long)n * ons + (long long)c * S;
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
     f4 v[4];
     if (rk) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) rv[j] *= rks;
+      for (int j = 0; j < 4; ++j) rv[j] = mul_rn(rv[j], rks);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
 #ifndef L3U_NABR_U
 #define L3U_NABR_U 2
 #endif
-template <typename T, bool VEC>
+template <typename T, bool VEC, bool RK = false>
 __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     const float* __restrict__ dout, long long dns, const T* __restrict__ out, long long ons,
     const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     mr = recr[(long long)nc * kRec + 0]; rsr = recr[(long long)nc * kRec + 1];
     rks = recr[(long long)nc * kRec + 7];
   }
-  const bool rk = rns < 0;   // rank-1 residual: record_r[7] * one stored channel (include/l3u.h)
+  constexpr bool rk = RK;   // rank-1 residual (rns < 0): record_r[7] * one stored channel
   const long long co = (long long)c * S;
   // dscale: rank-1 dout = dscale[c] * dz (dz one channel, l3u_outconv_bwd_dz)
   const float* dp = dout + (long long)n * dns + (dscale ? 0 : co);
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
                                pidx + (long long)nc * (S / 8), z, y, rm - y * W, H, W);
           }
           yv[u] = ldv4(yp + i);
-          if (recr) rv[u] = rk ? rks * ldv4(rp + i) : ldv4(rp + i);
+          if (recr) rv[u] = rk ? mul_rn(ldv4(rp + i), rks) : ldv4(rp + i);
         }
       }
 #pragma unroll
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
       const float g = (dscale ? dsc * ld1(dp + i) : ld1(dp + i)) * lrelu_d(ld1(op + i));
       s0 += g;
       s1 += (double)g * ((ld1(yp + i) - m2) * rs2);
-      if (recr) s2 += (double)g * (((rk ? rks * ld1(rp + i) : ld1(rp + i)) - mr) * rsr);
+      if (recr) s2 += (double)g * (((rk ? mul_rn(rks, ld1(rp + i)) : ld1(rp + i)) - mr) * rsr);
     }
   }
   s0 = block_sum256d(s0, red);
@@ -510,16 +511,19 @@ int norm_act_fwd_impl(const T* y2, long long y2_nstride, const float* rec2,
                       long long out_nstride, int N, int C, int S, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0);
   L3U_REQUIRE(src2 ? (!shortcut || src_r) : (rec2 && (!shortcut || rec_r)));
-  L3U_REQUIRE(r_nstride >= 0 || (sizeof(T) == 4 && shortcut));   // rank-1 r: fp32 Conv1x1 shortcut
   const bool vec = S % 4 == 0 && y2_nstride % 4 == 0 && r_nstride % 4 == 0 && out_nstride % 4 == 0;
+  L3U_REQUIRE(r_nstride >= 0 || (sizeof(T) == 4 && shortcut && vec));   // rank-1 r: fp32 Conv1x1 shortcut
   dim3 grid(elem_blocks(S), N * C);
   const l3u_norm_src z{};
   const l3u_norm_src s2 = src2 ? *src2 : z, sr = src_r ? *src_r : z;
-#define NAF(V_, S_) hipLaunchKernelGGL((norm_act_fwd_kernel<T, V_, S_>), grid, dim3(256), 0, stream, y2, \
+#define NAF0(V_, S_, R_) hipLaunchKernelGGL((norm_act_fwd_kernel<T, V_, S_, R_>), grid, dim3(256), 0, stream, y2, \
       y2_nstride, rec2, s2, r, r_nstride, rec_r, sr, shortcut, out, out_nstride, C, S)
-  if (src2) { if (vec) NAF(true, true); else NAF(false, true); }
+#define NAF(V_, S_) NAF0(V_, S_, false)
+  if (r_nstride < 0) { if constexpr (sizeof(T) == 4) { if (src2) NAF0(true, true, true); else NAF0(true, false, true); } }
+  else if (src2) { if (vec) NAF(true, true); else NAF(false, true); }
   else { if (vec) NAF(true, false); else NAF(false, false); }
 #undef NAF
+#undef NAF0
   L3U_CHECK_LAUNCH();
 }
 
@@ -542,11 +546,12 @@ int norm_act_pool_fwd_impl(const T* y2, long long y2_nstride, const float* rec2,
   dim3 grid(elem_blocks((int)S), N * C);
   const l3u_norm_src z{};
   const l3u_norm_src s2 = src2 ? *src2 : z, sr = src_r ? *src_r : z;
-#define NAP(S_) hipLaunchKernelGGL((norm_act_pool_fwd_kernel<T, S_>), grid, dim3(256), 0, stream, y2, \
+#define NAP(S_, R_) hipLaunchKernelGGL((norm_act_pool_fwd_kernel<T, S_, R_>), grid, dim3(256), 0, stream, y2, \
       y2_nstride, rec2, s2, r, r_nstride, rec_r, sr, shortcut, out, out_nstride, pooled, \
       pooled_nstride, idx, C, D, H, W)
-  if (src2) NAP(true);
-  else NAP(false);
+  if (r_nstride < 0) { if constexpr (sizeof(T) == 4) { if (src2) NAP(true, true); else NAP(false, true); } }
+  else if (src2) NAP(true, false);
+  else NAP(false, false);
 #undef NAP
   L3U_CHECK_LAUNCH();
 }
@@ -566,7 +571,11 @@ int norm_act_bwd_reduce_impl(const float* dout, long long dout_nstride, const T*
   L3U_REQUIRE(dpool == nullptr || (vec && pidx && H % 2 == 0 && W % 4 == 0 && (S / (H * W)) % 2 == 0 &&
                                    dpns % 2 == 0 && ((uintptr_t)dpool & 7) == 0));
   dim3 grid(elem_blocks(S), N * C);
-  if (vec) hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale, dpool, dpns, pidx, H, W);
+  L3U_REQUIRE(r_nstride >= 0 || vec);
+  if (r_nstride < 0) {
+    if constexpr (sizeof(T) == 4)
+      hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale, dpool, dpns, pidx, H, W);
+  } else if (vec) hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale, dpool, dpns, pidx, H, W);
   else hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, false>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale);
   L3U_CHECK_LAUNCH();
 }

@@ -562,7 +562,7 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 // (row lr, voxels 16g + 4lk..+3) is read back transposed, conflict-free.  X is only needed by
 // the weight gradient and is loaded in its B layout.  The weights sit in LDS as W[j][k] with a
 // row stride = 16 mod 64 floats (conflict-free A-operand reads for the data gradient).
-template <typename T, int NJ, int NK, int PRO>
+template <typename T, int NJ, int NK, int PRO, bool R1 = false>
 __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
@@ -619,8 +619,9 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       if (j < J && sd < s_hi) ov[jr] = ldv4(on + (long long)j * S + sd);
     }
   }
-  // yns < 0: a rank-1 normalised operand, channel j = rec[j][7] * one stored channel (l3u.h)
-  const bool yk = PRO && yns < 0;
+  // R1 (yns < 0): a rank-1 normalised operand, channel j = rec[j][7] * one stored channel
+  // (include/l3u.h); a template flag so that the other variants keep their registers
+  constexpr bool yk = PRO && R1;
   if (PRO) {
     const T* yn = yin + (long long)n * (yk ? -yns : yns);
 #pragma unroll
@@ -648,21 +649,12 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const int j = tid / PS, sub = tid % PS;
     double t0 = 0.0, t1 = 0.0;
     if (j < J) {
-      // the loads of 4 steps are issued together (one memory latency per 4 partials; the
-      // summation order is unchanged)
-      const int nv = PRO == 2 ? 3 : 2, o1 = PRO == 2 ? sel : 1;
-      const double* pp = in_part + ((long long)j * N + n) * npart * nv;
-      for (int i0 = sub; i0 < npart; i0 += 4 * PS) {
-        double a[4], b[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int i = i0 + u * PS;
-          a[u] = i < npart ? pp[i * nv] : 0.0;
-          b[u] = i < npart ? pp[i * nv + o1] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (i0 + u * PS < npart) { t0 += a[u]; t1 += b[u]; }
+      if (PRO == 2) {   // block-tail partials [J][N][npart][3]: {sum g, sum g*xhat2, sum g*xhat_r}
+        const double* pp = in_part + ((long long)j * N + n) * npart * 3;
+        for (int i = sub; i < npart; i += PS) { t0 += pp[i * 3]; t1 += pp[i * 3 + sel]; }
+      } else {
+        const double* pp = in_part + ((long long)j * N + n) * npart * 2;
+        for (int i = sub; i < npart; i += PS) { t0 += pp[i * 2]; t1 += pp[i * 2 + 1]; }
       }
     }
     psum[tid * 2] = t0;
@@ -695,7 +687,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       const float* c = coef + j * 8;
       const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
       const bool ok = j < J && sd < s_hi;
-      if (yk) yv[jr] *= c[5];   // the materialised operand's value, bit for bit
+      if (yk) yv[jr] = mul_rn(yv[jr], c[5]);   // the materialised operand's value, bit for bit
       if (PRO == 2) {   // g = dout * lrelu'(out), then the tail InstanceNorm backward
 #pragma unroll
         for (int q = 0; q < 4; ++q) g[jr][q] = g[jr][q] * lrelu_d(ov[jr][q]);
@@ -1393,16 +1385,21 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
   const size_t dlds = (size_t)nwv * 16 * NJ * 68 * sizeof(float);   // dY tiles (DS = 68)
-#define PWBT(A_, B_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2>), grid, block, dlds, stream, \
+#define PWBT0(A_, B_, R_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2, R_>), grid, block, dlds, stream, \
       dout, dout_nstride, yr, yr_nstride, rec, tail_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel, dscale, dpool, dpns, pidx, Hf, Wf)
-  if (NJ == 1 && NK == 1) PWBT(1, 1);
+#define PWBT(A_, B_) PWBT0(A_, B_, false)
+  // a rank-1 yr (the first block's shortcut, K = 1): its own variant
+  L3U_REQUIRE(yr_nstride >= 0 || (NJ == 1 && NK == 1));
+  if (yr_nstride < 0) { if constexpr (sizeof(T) == 4) PWBT0(1, 1, true); }
+  else if (NJ == 1 && NK == 1) PWBT(1, 1);
   else if (NJ == 1 && NK == 2) PWBT(1, 2);
   else if (NJ == 1 && NK == 4) PWBT(1, 4);
   else if (NJ == 2 && NK == 1) PWBT(2, 1);
   else if (NJ == 2 && NK == 2) PWBT(2, 2);
   else PWBT(2, 4);
 #undef PWBT
+#undef PWBT0
   L3U_CHECK_LAUNCH();
 }
 
@@ -1437,6 +1434,15 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);   // one sweep of the chunk per workgroup
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
   const size_t dlds = (size_t)nwv * 16 * NJ * 68 * sizeof(float);   // dY tiles (DS = 68)
+  // a rank-1 y (the first block's conv1.pointwise, K = 1): its own variant
+  L3U_REQUIRE(y_nstride >= 0 || (NJ == 1 && NK == 1));
+  if (y && y_nstride < 0) {
+    if constexpr (sizeof(T) == 4)
+      hipLaunchKernelGGL((pw_bwd_fused_kernel<T, 1, 1, 1, true>), grid, block, dlds, stream, dy,
+                         dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx,
+                         dx_nstride, accumulate, part, N, J, K, S, SCH, nsc);
+    L3U_CHECK_LAUNCH();
+  }
 #define PWBF(A_, B_) do { if (y) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 1>), grid, block, dlds, \
       stream, dy, dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, N, J, K, S, SCH, nsc); \
