@@ -325,6 +325,25 @@ def instep_evidence(workload, launches):
     return None
 
 
+def step_traffic_evidence(workload, ms_per_step):
+    """Whole-step HBM traffic of the eager step from the newest committed PMC record of this
+    workload (tools/pmc_step.sh -> profiles/*_pmc_step_<workload>.json: FETCH_SIZE x 2 +
+    WRITE_SIZE per launch, separate passes) and the average rate it implies at this step time."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_step_{workload}.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        rec = json.load(f)
+    b = rec["step_traffic_bytes"]
+    out = {"source": os.path.relpath(files[-1], ROOT), "commit": rec.get("commit"),
+           "bytes": b, "launches": rec.get("launches")}
+    if ms_per_step:
+        out["avg_tb_s"] = round(b / (ms_per_step * 1e-3) / 1e12, 3)
+        out["frac_of_8tb_s"] = round(out["avg_tb_s"] / 8.0, 4)
+    return out
+
+
 def gemm_mfma_evidence(top=5):
     """MFMA-busy fractions of the step's GEMM launches from the committed rocprofv3 passes
     (tools/pmc_step.sh + tools/pmc_gemm.sh -> tools/pmc_launch_json.py -> profiles/*_pmc_step.json)."""
@@ -887,6 +906,7 @@ def main():
     cfg5 = config5_bench(device, world, rank) if not args.no_config5 else None   # every rank
     if cfg5 is not None:
         cfg5["roofline_in_step"] = instep_evidence("c5", None)
+        cfg5["step_traffic"] = step_traffic_evidence("c5", cfg5.get("ms_per_step"))
     cfg5 = cfg5 if rank == 0 else None
     grouped = grouped_bench(device) if (rank == 0 and not args.no_grouped) else None
     bf16 = bf16_bench(device, args, enc, world, rank, pool) if (args.dtype == "fp32" and not args.no_bf16) else None
