@@ -198,8 +198,19 @@ L3U_DEV unsigned long long splitmix64(unsigned long long z) {
   return z ^ (z >> 31);
 }
 
-L3U_DEV void record_from(const l3u_norm_src& s, int n, int c, int C, float cn, float mu, float m2,
-                         float r[kRec]);
+// the record's per-channel inputs (affine parameters, Dropout3d step, rank-1 scale), loaded
+// BEFORE the partials so that both arrive in one memory round trip
+struct RecIn { float g, b, rk1; int st; };
+L3U_DEV RecIn record_inputs(const l3u_norm_src& s, int c) {
+  RecIn q;
+  q.g = s.gamma ? s.gamma[c] : 1.f;
+  q.b = s.beta ? s.beta[c] : 0.f;
+  q.st = (s.drop_p > 0.f && s.step) ? *s.step : 0;
+  q.rk1 = s.rank1 ? s.rank1[c] : 0.f;
+  return q;
+}
+L3U_DEV void record_from(const l3u_norm_src& s, const RecIn& q, int n, int c, int C, float cn,
+                         float mu, float m2, float r[kRec]);
 
 // Merge the (count, mean, M2) partials of one (n, c) with the 64 lanes of the calling wave
 // (lane-strided Chan merges, then a fixed xor tree) and build the 8-float record.  Every caller
@@ -207,6 +218,7 @@ L3U_DEV void record_from(const l3u_norm_src& s, int n, int c, int C, float cn, f
 // record in `r` on every lane.
 L3U_DEV void finalize_record(const l3u_norm_src& s, int n, int c, int C, float r[kRec]) {
   const int l = threadIdx.x & 63;
+  const RecIn q = record_inputs(s, c);
   const float* p = s.stat_part + ((long long)n * C + c) * s.nsb * 3;
   float cn = 0.f, mu = 0.f, m2 = 0.f;
   // lane-strided sequential merges; the loads of 8 steps are issued together (one memory
@@ -234,19 +246,19 @@ L3U_DEV void finalize_record(const l3u_norm_src& s, int n, int c, int C, float r
       chan_merge(cn, mu, m2, cb, mb, vb);
     }
   }
-  record_from(s, n, c, C, cn, mu, m2, r);
+  record_from(s, q, n, c, C, cn, mu, m2, r);
 }
 
 // The record of (n, c) from its merged (count, mean, M2): rstd, the affine parameters and the
 // Dropout3d keep scale of (step, layer, n*C + c).
-L3U_DEV void record_from(const l3u_norm_src& s, int n, int c, int C, float cn, float mu, float m2,
-                         float r[kRec]) {
+L3U_DEV void record_from(const l3u_norm_src& s, const RecIn& q, int n, int c, int C, float cn,
+                         float mu, float m2, float r[kRec]) {
   const float var = cn > 0.f ? m2 / cn : 0.f;
   const float rstd = 1.0f / sqrtf(var + kEps);
-  const float g = s.gamma ? s.gamma[c] : 1.f, b = s.beta ? s.beta[c] : 0.f;
+  const float g = q.g, b = q.b;
   float k = 1.f;
   if (s.drop_p > 0.f) {
-    const int st = s.step ? *s.step : 0;
+    const int st = q.st;
     const unsigned long long h = splitmix64(s.seed ^ splitmix64(((unsigned long long)st << 32) ^
                                                                 ((unsigned long long)s.layer << 24) ^
                                                                 (unsigned long long)(n * C + c)));
@@ -260,7 +272,7 @@ L3U_DEV void record_from(const l3u_norm_src& s, int n, int c, int C, float cn, f
   r[4] = k;
   r[5] = g;
   r[6] = b;
-  r[7] = s.rank1 ? s.rank1[c] : 0.f;
+  r[7] = q.rk1;
 }
 
 // Workgroup-level: wave 0 finalizes, broadcasts through `sh8` (8 floats of LDS) and, if asked,
@@ -352,6 +364,57 @@ L3U_DEV int xcd_remap(int bid, int nblocks) {
   const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + (bid >> 3);
 }
+
+// Wave stamps (profiling variant builds only, -DL3U_STAMP; tools/stamp.py): lane 0 of every wave
+// of a launch with at most kStampMaxWaves waves records {begin, end} in wall-clock ticks (100 MHz),
+// the kernel id (L3U_STAMP_SCOPE in each kernel) and the flat block index into a device buffer
+// that l3u_stamp_setup installs (256 shards of cap / 256 records, one counter each).  Product builds compile the scope to nothing.
+#ifdef L3U_STAMP
+struct StampRec { unsigned long long t0, t1, m0, m1; unsigned id, blk, nwg, pad, r0, r1; };
+constexpr unsigned kStampMaxWaves = 65536;
+static __device__ StampRec* l3u_stamp_dptr;
+static __device__ unsigned* l3u_stamp_dctr;
+static __device__ unsigned l3u_stamp_cap;
+void stamp_register(void (*set)(void*, void*, unsigned));
+static void l3u_stamp_set_tu(void* b, void* c, unsigned cap) {
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(l3u_stamp_dptr), &b, sizeof b);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(l3u_stamp_dctr), &c, sizeof c);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(l3u_stamp_cap), &cap, sizeof cap);
+}
+static const int l3u_stamp_reg = (stamp_register(l3u_stamp_set_tu), 0);
+struct StampScope {   // the slot is taken at wave begin (the atomic's return overlaps the body)
+  unsigned long long t0, m[2];
+  unsigned id, slot, shard;
+  bool on;
+  __device__ void mark(int k) { m[k] = wall_clock64(); }   // intermediate stage stamps
+  __device__ explicit StampScope(unsigned i) : m{0, 0}, id(i), slot(0), shard(0) {
+    t0 = wall_clock64();
+    const unsigned long long nwv = (blockDim.x * blockDim.y * blockDim.z + 63) / 64;
+    on = l3u_stamp_dptr != nullptr && (threadIdx.x & 63) == 0 &&
+         (unsigned long long)gridDim.x * gridDim.y * gridDim.z * nwv <= kStampMaxWaves;
+    if (on) {   // 256 counters (by block): no fan-in on one word
+      shard = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) & 255;
+      slot = atomicAdd(l3u_stamp_dctr + shard, 1u);
+    }
+  }
+  __device__ ~StampScope() {
+    if (on) {
+      const unsigned long long t1 = wall_clock64();
+      if (slot < l3u_stamp_cap / 256) {
+        const unsigned blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        l3u_stamp_dptr[shard * (l3u_stamp_cap / 256) + slot] =
+            StampRec{t0, t1, m[0], m[1], id, blk * 16 + threadIdx.x / 64,
+                     gridDim.x * gridDim.y * gridDim.z, 1, 0, 0};
+      }
+    }
+  }
+};
+#define L3U_STAMP_SCOPE(ID) l3u::StampScope l3u_stamp_scope_(ID)
+#define L3U_STAMP_MARK(K) l3u_stamp_scope_.mark(K)
+#else
+#define L3U_STAMP_SCOPE(ID) ((void)0)
+#define L3U_STAMP_MARK(K) ((void)0)
+#endif
 
 }  // namespace l3u
 

@@ -26,6 +26,7 @@ __global__ __launch_bounds__(256) void dw3_fwd_kernel(
     const T* __restrict__ x, long long xns, const float* __restrict__ w,
     const float* __restrict__ rec, l3u_norm_src src, int has_src, T* __restrict__ y,
     long long yns, int C, int D, int H, int W, int TZ, int nchunk) {
+  L3U_STAMP_SCOPE(201);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int HW = H * W, PW = W + 2, PP = (H + 2) * PW;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -139,6 +140,7 @@ __global__ __launch_bounds__(256) void dw3_bwd_kernel(
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
     long long dxns, int accumulate, float* __restrict__ dw_part, double* __restrict__ in_part,
     int N, int C, int D, int H, int W, int TZ, int nchunk) {
+  L3U_STAMP_SCOPE(202);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int HW = H * W, PW = W + 2, PP = (H + 2) * PW;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -516,6 +518,7 @@ __global__ __launch_bounds__(256) void dw3q_fwd_kernel(
     const float* __restrict__ rec, l3u_norm_src src, int has_src, T* __restrict__ y,
     long long yns, const TE* __restrict__ ep, long long epns, double* __restrict__ in_part,
     int N, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
+  L3U_STAMP_SCOPE(203);
   constexpr bool FLIP = EPI != 0;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int WQ = W >> 2, PP = (RB + 2) * W, HW = H * W;
@@ -629,6 +632,7 @@ __global__ __launch_bounds__(256) void dw3q_dw_kernel(
     const float* __restrict__ dz, long long dzns, const T* __restrict__ x, long long xns,
     const float* __restrict__ rec, float* __restrict__ dw_part, int N, int C, int D, int H, int W,
     int RB, int RPW, int ny, int TZ, int nz) {
+  L3U_STAMP_SCOPE(204);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int WQ = W >> 2, PP = (RB + 2) * W, HW = H * W;
   const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
@@ -885,6 +889,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
     long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part,
     int N, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
+  L3U_STAMP_SCOPE(205);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   using LTA = std::conditional_t<GL, T, float>;        // LDS element type of the A image
   constexpr bool BH = GL && sizeof(T) == 2;
@@ -1250,6 +1255,7 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
     const float* __restrict__ rec, l3u_norm_src src, int has_src, T* __restrict__ y,
     long long yns, const T* __restrict__ ep, long long epns, double* __restrict__ in_part,
     int N, int C, int D, int H, int W) {
+  L3U_STAMP_SCOPE(206);
   constexpr bool FLIP = EPI != 0;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int nc = blockIdx.x, c = nc % C, n = nc / C;
@@ -1271,8 +1277,10 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
       mu = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];
     }
   }
+  L3U_STAMP_MARK(0);
   v_put<XF == 1>(lds, raw, D, H, W, sc, mu, sh);
   __syncthreads();
+  L3U_STAMP_MARK(1);
   const int PW = W + 2, PHW = (H + 2) * PW;
   T* yp = y + (long long)n * yns + cofs;
   const T* epp = (EPI == 1 || EPI == 2) ? ep + (long long)n * epns + cofs : nullptr;
@@ -1324,6 +1332,7 @@ __global__ __launch_bounds__(256) void dwv_bwd_kernel(
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
     long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part, int N, int C, int D,
     int H, int W) {
+  L3U_STAMP_SCOPE(207);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int nc = blockIdx.x, c = nc % C, n = nc / C;
   const long long HW = (long long)H * W, S = D * HW, cofs = (long long)c * S;

@@ -107,6 +107,7 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
     const float* __restrict__ wpw, T* __restrict__ y, long long yns, float* __restrict__ ystat,
     const float* __restrict__ wsc, T* __restrict__ r, long long rns, float* __restrict__ rstat,
     T* __restrict__ z, long long zns, int D, int H, int W, int RB, int ny, int nz) {
+  L3U_STAMP_SCOPE(501);
   constexpr int K = 16 * CPW, NB = 2 + SC, NT = 4 * NC * (1 + SC);
   // register budget (1024 threads: <= 128 VGPRs): two channels per wave stage one plane ahead
   // and read their taps from LDS; one channel per wave stages two planes ahead, taps in SGPRs

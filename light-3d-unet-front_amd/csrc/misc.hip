@@ -5,6 +5,9 @@
 //   adamw                torch.optim.AdamW step on the flat parameter buffer     trainer.py:75-79
 //   reduce_segments      deterministic second stage of every split-K / partial reduction
 #include "common.h"
+#ifdef L3U_STAMP
+#include <vector>
+#endif
 using namespace l3u;
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -16,6 +19,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void maxpool2_fwd_kernel(
     const T* __restrict__ x, long long xns, T* __restrict__ y, long long yns,
     unsigned char* __restrict__ idx, int C, int D, int H, int W) {
+  L3U_STAMP_SCOPE(401);
   const int Do = D / 2, Ho = H / 2, Wo = W / 2;
   const long long So = (long long)Do * Ho * Wo, Si = (long long)D * H * W;
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
@@ -45,6 +49,7 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(
     const T* __restrict__ dy, long long dyns, const unsigned char* __restrict__ idx,
     const T* __restrict__ add, long long addns, T* __restrict__ dx, long long dxns,
     int C, int D, int H, int W) {
+  L3U_STAMP_SCOPE(402);
   const int Do = D / 2, Ho = H / 2, Wo = W / 2;
   const long long So = (long long)Do * Ho * Wo, Si = (long long)D * H * W;
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
@@ -75,6 +80,7 @@ __global__ __launch_bounds__(256) void outconv_fwd_kernel(
     const T* __restrict__ h, long long hns, const float* __restrict__ w,
     const float* __restrict__ b, float* __restrict__ p, const float* __restrict__ t,
     float* __restrict__ ftl_part, int C, int S) {
+  L3U_STAMP_SCOPE(403);
   __shared__ float red[4];
   const int n = blockIdx.y;
   const T* hp = h + (long long)n * hns;
@@ -183,6 +189,7 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     const float* __restrict__ w, float* __restrict__ dh, long long dhns,
     double* __restrict__ part, float* __restrict__ loss, int C, int S,
     const float* __restrict__ fpart = nullptr, int fnp = 0) {
+  L3U_STAMP_SCOPE(404);
   extern __shared__ double redd[];   // [4][C+1]
   const int n = blockIdx.y, nb = gridDim.x;
   const T* hp = h + (long long)n * hns;
@@ -285,6 +292,7 @@ __global__ __launch_bounds__(256) void ftl_partials_kernel(const float* __restri
                                                            const float* __restrict__ t,
                                                            long long numel,
                                                            float* __restrict__ part) {
+  L3U_STAMP_SCOPE(405);
   __shared__ float red[4];
   float spt = 0.f, sp = 0.f, st = 0.f;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < numel; i += (long long)gridDim.x * 256) {
@@ -305,6 +313,7 @@ __global__ __launch_bounds__(256) void ftl_partials_kernel(const float* __restri
 
 // sums[0..2] (double) = fixed-order sum of the partials
 __global__ void ftl_sums_kernel(const float* __restrict__ part, int nb, double* __restrict__ sums) {
+  L3U_STAMP_SCOPE(406);
   double a, b, c;
   ftl_lane_sums(part, nb, a, b, c);
   if (threadIdx.x == 0) { sums[0] = a; sums[1] = b; sums[2] = c; }
@@ -312,6 +321,7 @@ __global__ void ftl_sums_kernel(const float* __restrict__ part, int nb, double* 
 
 __global__ void ftl_loss_kernel(const double* __restrict__ sums, double alpha, double beta,
                                 double gamma, double smooth, float* __restrict__ loss) {
+  L3U_STAMP_SCOPE(407);
   const FtlCoef r = ftl_coef(sums, alpha, beta, gamma, smooth);
   loss[0] = (float)r.loss;
 }
@@ -321,6 +331,7 @@ __global__ __launch_bounds__(256) void ftl_bwd_kernel(
     const float* __restrict__ p, const float* __restrict__ t, long long numel,
     const double* __restrict__ sums, double alpha, double beta, double gamma, double smooth,
     const float* __restrict__ gscale, int through_sigmoid, float* __restrict__ g) {
+  L3U_STAMP_SCOPE(408);
   __shared__ float coef[2];
   if (threadIdx.x == 0) {
     const FtlCoef r = ftl_coef(sums, alpha, beta, gamma, smooth);
@@ -349,6 +360,7 @@ __global__ __launch_bounds__(256) void adamw_tick_kernel(float* __restrict__ p, 
                                                          float beta1, float beta2, float eps, float wd,
                                                          int* step, float gscale, int* ticket,
                                                          int* counter2) {
+  L3U_STAMP_SCOPE(409);
   const float lrv = lr[0];
   const int t = step[0] + 1;
   const float bc1 = 1.f - powf(beta1, (float)t);
@@ -413,6 +425,7 @@ __global__ void counter_add_kernel(int* c, int v) { c[0] += v; }
 __global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __restrict__ src,
                                                               const long long* __restrict__ items,
                                                               float* __restrict__ dst) {
+  L3U_STAMP_SCOPE(410);
   __shared__ double red[256];
   const long long* it = items + (long long)blockIdx.x * 8;
   const int t = threadIdx.x;
@@ -469,6 +482,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void maxpool2_fwd_v_kernel(
     const T* __restrict__ x, long long xns, T* __restrict__ y, long long yns,
     unsigned char* __restrict__ idx, int C, int D, int H, int W) {
+  L3U_STAMP_SCOPE(411);
   const int Ho = H / 2, W4 = W / 4;
   const long long So = (long long)(D / 2) * Ho * (W / 2), Si = (long long)D * H * W;
   const long long Sp = So / 2;
@@ -504,6 +518,7 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_v_kernel(
     const T* __restrict__ dy, long long dyns, const unsigned char* __restrict__ idx,
     const T* __restrict__ add, long long addns, T* __restrict__ dx, long long dxns,
     int C, int D, int H, int W) {
+  L3U_STAMP_SCOPE(412);
   const int Ho = H / 2, W4 = W / 4;
   const long long So = (long long)(D / 2) * Ho * (W / 2), Si = (long long)D * H * W;
   const long long Sp = So / 2;
@@ -563,6 +578,7 @@ __global__ __launch_bounds__(256) void front_fwd_kernel(
     const float* __restrict__ w1, const float* __restrict__ wr, T* __restrict__ z1,
     T* __restrict__ y1, T* __restrict__ r, float* __restrict__ stat1,
     float* __restrict__ statr, T* __restrict__ xc, int C, int D, int H, int W) {
+  L3U_STAMP_SCOPE(413);
   __shared__ float red[4];
   const int S = D * H * W, nb = gridDim.x, b = blockIdx.x, n = blockIdx.y;
   const int i0 = (b * 256 + threadIdx.x) * 4;
@@ -627,6 +643,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void box_copy_kernel(
     const T* __restrict__ src, long long sns, int sd, int sh, int sw, T* __restrict__ dst,
     long long dns, int dd, int dh, int dw, int oz, int oy, int ox, int C, long long total) {
+  L3U_STAMP_SCOPE(414);
   const long long dS = (long long)dd * dh * dw, sS = (long long)sd * sh * sw;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const int x = (int)(i % dw);
@@ -648,6 +665,7 @@ __global__ __launch_bounds__(256) void box_copy_kernel(
 template <typename S_, typename D_>
 __global__ __launch_bounds__(256) void cast_kernel(const S_* __restrict__ x, D_* __restrict__ y,
                                                    long long n4, long long n) {
+  L3U_STAMP_SCOPE(415);
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256)
     stv4(y + 4 * i, ldv4(x + 4 * i));
   const long long t = 4 * n4 + blockIdx.x * 256ll + threadIdx.x;
@@ -874,3 +892,20 @@ int l3u_counter_add(int* counter, int value, hipStream_t stream) {
 int l3u_abi_version(void) { return 2; }
 
 }  // extern "C"
+
+#ifdef L3U_STAMP
+// Wave-stamp registry of the profiling variant build (common.h StampScope): every translation
+// unit registers the setter of its own device pointers; l3u_stamp_setup installs one buffer in
+// all of them (buf: cap StampRec records, ctr: 256 zeroed unsigned; NULL buf turns stamping off).
+namespace l3u {
+static std::vector<void (*)(void*, void*, unsigned)>& stamp_setters() {
+  static std::vector<void (*)(void*, void*, unsigned)> v;
+  return v;
+}
+void stamp_register(void (*set)(void*, void*, unsigned)) { stamp_setters().push_back(set); }
+}  // namespace l3u
+extern "C" int l3u_stamp_setup(void* buf, void* ctr, unsigned cap) {
+  for (auto f : l3u::stamp_setters()) f(buf, ctr, cap);
+  return (int)hipDeviceSynchronize();
+}
+#endif

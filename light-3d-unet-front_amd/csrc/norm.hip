@@ -15,6 +15,7 @@ namespace {
 
 // one wave per (n, c)
 __global__ __launch_bounds__(256) void in_finalize_kernel(l3u_norm_src src, int NC, int C) {
+  L3U_STAMP_SCOPE(301);
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
   if (wid >= NC) return;
   float r[kRec];
@@ -34,6 +35,7 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
     const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2, l3u_norm_src src2,
     const T* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
     int shortcut, T* __restrict__ out, long long ons, int C, int S) {
+  L3U_STAMP_SCOPE(302);
   __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   // RK (rns < 0): rank-1 residual, record_r[7] * one stored channel (include/l3u.h)
@@ -92,6 +94,7 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
     const T* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
     int shortcut, T* __restrict__ out, long long ons, T* __restrict__ pooled,
     long long pns, unsigned char* __restrict__ idx, int C, int D, int H, int W) {
+  L3U_STAMP_SCOPE(303);
   __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   const long long S = (long long)D * H * W;
@@ -185,6 +188,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     double* __restrict__ part, int N, int C, int S, const float* __restrict__ dscale = nullptr,
     const float* __restrict__ dpool = nullptr, long long dpns = 0,
     const unsigned char* __restrict__ pidx = nullptr, int H = 0, int W = 0) {
+  L3U_STAMP_SCOPE(304);
   __shared__ double red[4];
   const int nc = blockIdx.y, c = nc % C, n = nc / C, nb = gridDim.x;
   const float m2 = rec2[(long long)nc * kRec + 0], rs2 = rec2[(long long)nc * kRec + 1];
@@ -263,6 +267,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_apply_kernel(
     const T* __restrict__ r, long long rns, const float* __restrict__ recr,
     const double* __restrict__ part, int npart, float* __restrict__ dy2, long long dy2ns,
     float* __restrict__ dr, long long drns, int N, int C, int S) {
+  L3U_STAMP_SCOPE(305);
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   const double* pp = part + ((long long)c * N + n) * npart * 3;
   double t[3];
@@ -316,6 +321,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
     const T* __restrict__ r, long long rns, const float* __restrict__ recr,
     double* __restrict__ part, float* __restrict__ dy2, long long dy2ns, float* __restrict__ dr,
     long long drns, int N, int C, int S) {
+  L3U_STAMP_SCOPE(306);
   __shared__ double red[4];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   const float* q2 = rec2 + (long long)nc * kRec;
@@ -445,6 +451,7 @@ __global__ __launch_bounds__(256) void in_bwd_apply_kernel(
     const float* dpre, long long dns, const T* __restrict__ y, long long yns,
     const float* __restrict__ rec, const double* __restrict__ part, int npart, float* dy,
     long long dyns, int N, int C, int S) {
+  L3U_STAMP_SCOPE(307);
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   const double* pp = part + ((long long)c * N + n) * npart * 2;
   double t[2];

@@ -110,6 +110,7 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
     const T* __restrict__ x2 = nullptr, long long xns2 = 0, const float* __restrict__ w2 = nullptr,
     T* __restrict__ y2 = nullptr, long long yns2 = 0, float* __restrict__ stat2 = nullptr,
     int N1 = 0) {
+  L3U_STAMP_SCOPE(101);
   constexpr int CO_BLK = 16 * NC;
   constexpr int TSB = 256 * NSW;
   constexpr int WS = (CO_BLK % 32 == 16) ? CO_BLK : CO_BLK + 16;
@@ -305,14 +306,11 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
   }
 }
 
-#ifndef L3U_PWKS_UNROLL
-#define L3U_PWKS_UNROLL 4
-#endif
 // Small-volume variant (per-sample S < 8192: the 12^3 / 6^3 levels): the 4 waves of a workgroup
 // share ONE 64-voxel tile and split the reduction dimension K (k-steps interleaved by wave), then
 // combine through LDS in a fixed order; weights are read straight from L2 (they are tiny and
 // every workgroup re-reads them).  This turns an 8-workgroup grid into hundreds.
-template <typename T, int NC, bool VEC, int XM>
+template <typename T, int NC, bool VEC, int XM, int KSM>
 __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
     const T* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
     const float* __restrict__ bias, T* __restrict__ y, long long yns, int accumulate,
@@ -320,6 +318,7 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
     const T* __restrict__ x2 = nullptr, long long xns2 = 0, const float* __restrict__ w2 = nullptr,
     T* __restrict__ y2 = nullptr, long long yns2 = 0, float* __restrict__ stat2 = nullptr,
     int N1 = 0) {
+  L3U_STAMP_SCOPE(102);
   constexpr int CO_BLK = 16 * NC;
   constexpr int NT = NC * 16;   // accumulator floats per lane
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [4 waves][NT][64 lanes]
@@ -337,18 +336,30 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
   for (int m = 0; m < NC; ++m)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[m][q] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll L3U_PWKS_UNROLL
-  for (int ks = wave; ks < ksteps; ks += 4) {
-    const int kk = 4 * ks + lk;
-    const f4 a = load_x4<VEC, XM == 2>(xn, kk, K, s, S, S, Hq, Wq);
+  // KSM k-steps per wave in flight: every load of a round is issued before its first MFMA (one
+  // memory round trip per round); 8 for latency-bound grids, 4 keeps the registers of big ones
+  for (int k0s = wave; k0s < ksteps; k0s += 4 * KSM) {
+    f4 av[KSM];
+    float bv[KSM][NC];
 #pragma unroll
-    for (int m = 0; m < NC; ++m) {
-      const int co = co0 + 16 * m + lr;
-      float b = 0.f;
-      if (kk < K && co < Nout) b = wl == 0 ? w[(long long)co * K + kk] : w[(long long)kk * Nout + co];
+    for (int u = 0; u < KSM; ++u) {
+      const int kk = 4 * (k0s + 4 * u) + lk;
+      av[u] = load_x4<VEC, XM == 2>(xn, kk, K, s, S, S, Hq, Wq);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[m][q] = mfma4(b, a[q], acc[m][q]);
+      for (int m = 0; m < NC; ++m) {
+        const int co = co0 + 16 * m + lr;
+        bv[u][m] = 0.f;
+        if (kk < K && co < Nout) bv[u][m] = wl == 0 ? w[(long long)co * K + kk] : w[(long long)kk * Nout + co];
+      }
     }
+#pragma unroll
+    for (int u = 0; u < KSM; ++u)
+      if (k0s + 4 * u < ksteps) {
+#pragma unroll
+        for (int m = 0; m < NC; ++m)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[m][q] = mfma4(bv[u][m], av[u][q], acc[m][q]);
+      }
   }
   // cross-wave combine through LDS, value-major ([wave][value][lane]: consecutive lanes hit
   // consecutive banks, conflict-free).  Every wave parks its partials; wave w then owns output
@@ -364,6 +375,7 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
         for (int r = 0; r < 4; ++r) dst[((m * 4 + q) * 4 + r) * 64] = acc[m][q][r];
   }
   __syncthreads();
+  L3U_STAMP_MARK(0);
   const int m = wave;
   if (m >= NC) return;
   f4 t4[4];
@@ -375,6 +387,7 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
       t4[q][r] = ((src[0] + src[NT * 64]) + src[2 * NT * 64]) + src[3 * NT * 64];
     }
   }
+  L3U_STAMP_MARK(1);
   // epilogue: lane (lr, lk) holds Y[co0 + 16m + 4lk + r][sb*64 + 4lr + q]
   T* yn = y + (long long)n * yns;
   const int sv = sb * 64 + 4 * lr;
@@ -442,6 +455,7 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
     const TD* __restrict__ dy, long long dyns, const TX* __restrict__ x, long long xns,
     float* __restrict__ part, float* __restrict__ bsum, int J, int K, int S, int SCH, int nsc,
     int Hq, int Wq) {
+  L3U_STAMP_SCOPE(103);
   constexpr int TJ = 16 * NJ, TK = 16 * NK;
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [64][T]
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
@@ -571,6 +585,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     int K, int S, int SCH, int nsc, const T* __restrict__ oin = nullptr, long long oins = 0,
     int sel = 1, const float* __restrict__ dscale = nullptr, const float* __restrict__ dpool = nullptr,
     long long dpns = 0, const unsigned char* __restrict__ pidx = nullptr, int Hf = 0, int Wf = 0) {
+  L3U_STAMP_SCOPE(104);
   constexpr int TJ = 16 * NJ, TK = 16 * NK, JR = TJ / 4;
   constexpr int WS = TK + ((16 - TK) % 64 + 64) % 64;   // >= TK, = 16 mod 64
   constexpr int DS = 68;                                // dY tile row stride (floats)
@@ -794,6 +809,7 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
     const T* __restrict__ x, long long xns, const float* __restrict__ w,
     float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part,
     float* __restrict__ bpart, int N, int J, int K, int S, int Hq, int Wq) {
+  L3U_STAMP_SCOPE(105);
   constexpr int JW = 16 * JT;                 // dY rows per wave
   constexpr bool GV = GATHER != 2;            // vector loads
   constexpr bool G = GATHER != 0;
@@ -851,6 +867,7 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
       o[4] = (float)(t[1] / S);
     }
     __syncthreads();
+    L3U_STAMP_MARK(0);
 #pragma unroll
     for (int jr = 0; jr < JT * 4; ++jr) {
       const float* c = coef + (jb + 4 * jr + lk) * 8;
@@ -921,6 +938,7 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][(q * 4 + r) * 64 + l] = acc[q][r];
   __syncthreads();
+  L3U_STAMP_MARK(1);
   if (wave < 4) {
     const int r = wave;
     const int k = k0 + 4 * lk + r;
@@ -1044,6 +1062,7 @@ template <int NC, int KW>
 __global__ __launch_bounds__(64 * KW) void convt_dx_pair_kernel(
     const float* __restrict__ dy, long long dyns, const float* __restrict__ w, float* __restrict__ dx,
     long long dxns, int Ci, int Co, int D, int H, int W) {
+  L3U_STAMP_SCOPE(106);
   convt_dx_pair_body<NC, KW>(blockIdx.x, blockIdx.y, blockIdx.z, dy, dyns, w, dx, dxns, Ci, Co, D, H, W);
 }
 
@@ -1163,6 +1182,7 @@ __global__ __launch_bounds__(256) void convt_dw_pair_kernel(
     const T* __restrict__ x, long long xns, const float* __restrict__ dy, long long dyns,
     float* __restrict__ part, float* __restrict__ bsum, int Ci, int Co, int D, int H, int W,
     int SCH, int nsc) {
+  L3U_STAMP_SCOPE(107);
   convt_dw_pair_body<T, NJ, NG>(blockIdx.x, blockIdx.y, x, xns, dy, dyns, part, bsum, Ci, Co, D, H, W,
                                 SCH, nsc);
 }
@@ -1178,6 +1198,7 @@ __global__ __launch_bounds__(256) void convt_pair_bwd_kernel(
     long long dxns, const T* __restrict__ x, long long xns, float* __restrict__ part,
     float* __restrict__ bsum, int Ci, int Co, int D, int H, int W, int SCH, int nsc, int gx, int gy,
     int nA, int gwx) {
+  L3U_STAMP_SCOPE(108);
   const int b = blockIdx.x;
   if (b < nA) {
     convt_dx_pair_body<NC, 4>(b % gx, (b / gx) % gy, b / (gx * gy), dy, dyns, w, dx, dxns, Ci, Co, D, H, W);
@@ -1213,6 +1234,9 @@ int pw_nsw(int NC) { const int n = 4 / NC; return n < L3U_PW_NSW_MAX ? n : L3U_P
 #ifndef L3U_CONVT_KS_MIN_K
 #define L3U_CONVT_KS_MIN_K 64  // ConvTranspose3d forward: shallower K takes the unsplit kernel (up3: 19.3 -> 14.5 us)
 #endif
+#ifndef L3U_PWKS8_MAX_WG
+#define L3U_PWKS8_MAX_WG 1024  // grids up to this many workgroups take all k-steps in flight
+#endif
 // K split across the 4 waves (pw_fwd_ks_kernel) for small volumes with a deep enough reduction
 bool pw_use_ks(int S, int K) { return S < 32768 && K >= L3U_PW_KS_MIN_K; }
 
@@ -1245,9 +1269,14 @@ int pw_launch(const T* x, long long x_nstride, const float* w, int w_layout, con
     while (NC > 1 && (long long)nsb * ((Nout + 16 * NC - 1) / (16 * NC)) * N < 256) NC >>= 1;
     const size_t lds = 4 * 64 * (size_t)NC * 16 * sizeof(float);
     dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), NZ), block(256);
-#define PWK(NC_, V_, X_) hipLaunchKernelGGL((pw_fwd_ks_kernel<T, NC_, V_, X_>), grid, block, lds, stream, \
+    // the whole grid in one round of waves: the latency-bound form (all k-steps of a wave in flight)
+    const bool ks8 = NC <= 2 && xm != 2 && (long long)grid.x * grid.y * grid.z <= L3U_PWKS8_MAX_WG;
+#define PWK(NC_, V_, X_) do { if (ks8) hipLaunchKernelGGL((pw_fwd_ks_kernel<T, NC_, V_, X_, 8>), grid, block, lds, \
+      stream, x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq, \
+      p2.x, p2.xns, p2.w, p2.y, p2.yns, p2.stat, N); \
+      else hipLaunchKernelGGL((pw_fwd_ks_kernel<T, NC_, V_, X_, 4>), grid, block, lds, stream, \
       x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq, \
-      p2.x, p2.xns, p2.w, p2.y, p2.yns, p2.stat, N)
+      p2.x, p2.xns, p2.w, p2.y, p2.yns, p2.stat, N); } while (0)
 #define PWK_X(NC_, V_) do { if (xm == 1) PWK(NC_, V_, 1); else if (xm == 2) PWK(NC_, V_, 2); else PWK(NC_, V_, 0); } while (0)
 #define PWK_V(NC_) do { if (vec) PWK_X(NC_, true); else PWK_X(NC_, false); } while (0)
     if (NC == 1) PWK_V(1);
