@@ -802,13 +802,13 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
 // (the ConvTranspose3d weight [Ci][Co*8]) and so are the partials; bpart != NULL receives the
 // bias partials sum_{tile, abc} dY[co] per (tile, co) from the K-tile-0 workgroups.
 // Partials are per 64-voxel tile: part[N * ceil(S/64)][J][K] ([K][J] for GATHER).
-template <typename T, int JT, int NWV, int PRO, int GATHER>
+template <typename T, int JT, int NWV, int PRO, int GATHER, bool MT = false>
 __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
     const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
     const T* __restrict__ x, long long xns, const float* __restrict__ w,
     float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part,
-    float* __restrict__ bpart, int N, int J, int K, int S, int Hq, int Wq) {
+    float* __restrict__ bpart, int N, int J, int K, int S, int Hq, int Wq, int tpb) {
   L3U_STAMP_SCOPE(105);
   constexpr int JW = 16 * JT;                 // dY rows per wave
   constexpr bool GV = GATHER != 2;            // vector loads
@@ -816,43 +816,16 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
   __shared__ __attribute__((aligned(16))) float coef[PRO ? 128 * 8 : 1];
   __shared__ __attribute__((aligned(16))) float red[NWV][16 * 64];
   const int tid = threadIdx.x, wave = tid >> 6, l = tid & 63, lr = l & 15, lk = l >> 4;
-  const int ntile = (S + 63) / 64;
-  const int tile = blockIdx.x % ntile, n = blockIdx.x / ntile, k0 = blockIdx.y * 16;
-  const int v0 = tile * 64, jb = wave * JW;
+  // workgroup = tpb consecutive 64-voxel tiles of one sample (weight-gradient partials summed
+  // over them in registers: one partial per workgroup)
+  // MT = false: one tile per workgroup (tpb == 1, compile-time: the latency-bound levels keep
+  // the single-tile schedule and registers)
+  if (!MT) tpb = 1;
+  const int ntile = (S + 63) / 64, nblk = (ntile + tpb - 1) / tpb;
+  const int tb = blockIdx.x % nblk, n = blockIdx.x / nblk, k0 = blockIdx.y * 16;
+  const int t0 = tb * tpb, t1 = min(ntile, t0 + tpb), jb = wave * JW;
   const float* dyn = dy + (long long)n * dyns;
   const T* xn = x + (long long)n * xns;
-
-  // streamed loads first: dY in the data-gradient B layout (rows jb + 4jr + lk, voxels
-  // v0 + 4lr..), dY in the weight-gradient A layout (rows jb + 16t + lr, voxels v0 + 16g + 4lk..),
-  // X in the B layout (rows k0 + lr), the weights W[jb + 4jr + lk][k0 + lr]
-  f4 gd[JT * 4], ga[JT][4], yd[PRO ? JT * 4 : 1], ya[PRO ? JT : 1][4], xb[4];
-  float wa[JT * 4];
-  const int vd = v0 + 4 * lr;
-#pragma unroll
-  for (int jr = 0; jr < JT * 4; ++jr) {
-    const int j = jb + 4 * jr + lk;
-    gd[jr] = load_x4<GV, G>(dyn, j, J, vd, S, S, Hq, Wq);
-    const int k = k0 + lr;
-    wa[jr] = k < K ? (G ? w[(long long)k * J + j] : w[(long long)j * K + k]) : 0.f;
-  }
-#pragma unroll
-  for (int t = 0; t < JT; ++t)
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-      ga[t][g] = load_x4<GV, G>(dyn, jb + 16 * t + lr, J, v0 + 16 * g + 4 * lk, S, S, Hq, Wq);
-  if (PRO) {
-    const T* yn = yin + (long long)n * yns;
-#pragma unroll
-    for (int jr = 0; jr < JT * 4; ++jr) yd[jr] = load_x4<true, false>(yn, jb + 4 * jr + lk, J, vd, S, S, 0, 0);
-#pragma unroll
-    for (int t = 0; t < JT; ++t)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        ya[t][g] = load_x4<true, false>(yn, jb + 16 * t + lr, J, v0 + 16 * g + 4 * lk, S, S, 0, 0);
-  }
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-    xb[g] = load_x4<GV, false>(xn, k0 + lr, K, v0 + 16 * g + 4 * lk, S, S, 0, 0);
 
   if (PRO) {   // per-row InstanceNorm-backward coefficients (rows < J <= 128)
     if (tid < J) {
@@ -867,46 +840,134 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
       o[4] = (float)(t[1] / S);
     }
     __syncthreads();
-    L3U_STAMP_MARK(0);
+  }
+  f4 gw[JT];
+  float bsum[JT];
 #pragma unroll
-    for (int jr = 0; jr < JT * 4; ++jr) {
-      const float* c = coef + (jb + 4 * jr + lk) * 8;
-      const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
+  for (int t = 0; t < JT; ++t) { gw[t] = f4{0.f, 0.f, 0.f, 0.f}; bsum[t] = 0.f; }
+  float wa[JT * 4];   // the weights W[jb + 4jr + lk][k0 + lr]
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        gd[jr][q] = vd + q < S ? f * (gd[jr][q] - M1 - (yd[jr][q] - mu) * rs * M2) : 0.f;
-    }
-#pragma unroll
-    for (int t = 0; t < JT; ++t) {
-      const float* c = coef + (jb + 16 * t + lr) * 8;
-      const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int v = v0 + 16 * g + 4 * lk;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          ga[t][g][q] = v + q < S ? f * (ga[t][g][q] - M1 - (ya[t][g][q] - mu) * rs * M2) : 0.f;
-      }
-    }
+  for (int jr = 0; jr < JT * 4; ++jr) {
+    const int j = jb + 4 * jr + lk, k = k0 + lr;
+    wa[jr] = k < K ? (G ? w[(long long)k * J + j] : w[(long long)j * K + k]) : 0.f;
   }
 
-  // data gradient: this wave's split-J partial of dX[k0 + 4lk + r][vd + q]
-  f4 acc[4];
+  for (int tile = t0; tile < t1; ++tile) {
+    const int v0 = tile * 64;
+    // streamed loads first: dY in the data-gradient B layout (rows jb + 4jr + lk, voxels
+    // v0 + 4lr..), dY in the weight-gradient A layout (rows jb + 16t + lr, voxels v0 + 16g + 4lk..),
+    // X in the B layout (rows k0 + lr)
+    f4 gd[JT * 4], ga[JT][4], yd[PRO ? JT * 4 : 1], ya[PRO ? JT : 1][4], xb[4];
+    const int vd = v0 + 4 * lr;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int jr = 0; jr < JT * 4; ++jr) gd[jr] = load_x4<GV, G>(dyn, jb + 4 * jr + lk, J, vd, S, S, Hq, Wq);
 #pragma unroll
-  for (int jr = 0; jr < JT * 4; ++jr)
+    for (int t = 0; t < JT; ++t)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = mfma4(wa[jr], gd[jr][q], acc[q]);
-  // weight gradient of the wave's rows over the tile
-  f4 gw[JT];
+      for (int g = 0; g < 4; ++g)
+        ga[t][g] = load_x4<GV, G>(dyn, jb + 16 * t + lr, J, v0 + 16 * g + 4 * lk, S, S, Hq, Wq);
+    if (PRO) {
+      const T* yn = yin + (long long)n * yns;
 #pragma unroll
-  for (int t = 0; t < JT; ++t) {
-    gw[t] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int jr = 0; jr < JT * 4; ++jr) yd[jr] = load_x4<true, false>(yn, jb + 4 * jr + lk, J, vd, S, S, 0, 0);
+#pragma unroll
+      for (int t = 0; t < JT; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          ya[t][g] = load_x4<true, false>(yn, jb + 16 * t + lr, J, v0 + 16 * g + 4 * lk, S, S, 0, 0);
+    }
 #pragma unroll
     for (int g = 0; g < 4; ++g)
+      xb[g] = load_x4<GV, false>(xn, k0 + lr, K, v0 + 16 * g + 4 * lk, S, S, 0, 0);
+
+    if (PRO) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) gw[t] = mfma4(ga[t][g][q], xb[g][q], gw[t]);
+      for (int jr = 0; jr < JT * 4; ++jr) {
+        const float* c = coef + (jb + 4 * jr + lk) * 8;
+        const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          gd[jr][q] = vd + q < S ? f * (gd[jr][q] - M1 - (yd[jr][q] - mu) * rs * M2) : 0.f;
+      }
+#pragma unroll
+      for (int t = 0; t < JT; ++t) {
+        const float* c = coef + (jb + 16 * t + lr) * 8;
+        const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int v = v0 + 16 * g + 4 * lk;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            ga[t][g][q] = v + q < S ? f * (ga[t][g][q] - M1 - (ya[t][g][q] - mu) * rs * M2) : 0.f;
+        }
+      }
+    }
+
+    // data gradient: this wave's split-J partial of dX[k0 + 4lk + r][vd + q]
+    f4 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int jr = 0; jr < JT * 4; ++jr)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = mfma4(wa[jr], gd[jr][q], acc[q]);
+    // weight gradient of the wave's rows over the tile, accumulated over the workgroup's tiles
+#pragma unroll
+    for (int t = 0; t < JT; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gw[t] = mfma4(ga[t][g][q], xb[g][q], gw[t]);
+    if (G && bpart != nullptr && blockIdx.y == 0) {
+      // bias partial of co = j / 8: row sums over the tile (lanes lk), then the 8 rows abc of
+      // each co (lanes lr & 7), both in a fixed xor-tree order; tiles added in order
+#pragma unroll
+      for (int t = 0; t < JT; ++t) {
+        float sum = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) sum += (ga[t][g][0] + ga[t][g][1]) + (ga[t][g][2] + ga[t][g][3]);
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        sum += __shfl_xor(sum, 1, 64);
+        sum += __shfl_xor(sum, 2, 64);
+        sum += __shfl_xor(sum, 4, 64);
+        bsum[t] += sum;
+      }
+    }
+    // combine the NWV split-J partials in wave order; waves 0..3 then store rows r == wave
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][(q * 4 + r) * 64 + l] = acc[q][r];
+    __syncthreads();
+    L3U_STAMP_MARK(1);
+    if (wave < 4) {
+      const int r = wave;
+      const int k = k0 + 4 * lk + r;
+      f4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = (q * 4 + r) * 64 + l;
+        float sum = red[0][i];
+#pragma unroll
+        for (int wv = 1; wv < NWV; ++wv) sum += red[wv][i];
+        v[q] = sum;
+      }
+      if (k < K) {
+        float* dst = dx + (long long)n * dxns + (long long)k * S + vd;
+        if (GV) {
+          if (vd < S) {
+            if (accumulate) v += ldv4(dst);
+            stv4(dst, v);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (vd + q < S) st1(dst + q, accumulate ? ld1(dst + q) + v[q] : v[q]);
+        }
+      }
+    }
+    if (tile + 1 < t1) __syncthreads();   // red is rewritten by the next tile
   }
   float* o = part + (long long)blockIdx.x * J * K;
 #pragma unroll
@@ -917,53 +978,9 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
       if (k < K) o[G ? (long long)k * J + j : (long long)j * K + k] = gw[t][r];
     }
   if (G && bpart != nullptr && blockIdx.y == 0) {
-    // bias partial of co = j / 8: row sums over the tile (lanes lk), then the 8 rows abc of
-    // each co (lanes lr & 7), both in a fixed xor-tree order
 #pragma unroll
-    for (int t = 0; t < JT; ++t) {
-      float sum = 0.f;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) sum += (ga[t][g][0] + ga[t][g][1]) + (ga[t][g][2] + ga[t][g][3]);
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      sum += __shfl_xor(sum, 1, 64);
-      sum += __shfl_xor(sum, 2, 64);
-      sum += __shfl_xor(sum, 4, 64);
-      if (lk == 0 && (lr & 7) == 0) bpart[(long long)blockIdx.x * (J / 8) + (jb + 16 * t + lr) / 8] = sum;
-    }
-  }
-  // combine the NWV split-J partials in wave order; waves 0..3 then store rows r == wave
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[wave][(q * 4 + r) * 64 + l] = acc[q][r];
-  __syncthreads();
-  L3U_STAMP_MARK(1);
-  if (wave < 4) {
-    const int r = wave;
-    const int k = k0 + 4 * lk + r;
-    f4 v;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = (q * 4 + r) * 64 + l;
-      float sum = red[0][i];
-#pragma unroll
-      for (int wv = 1; wv < NWV; ++wv) sum += red[wv][i];
-      v[q] = sum;
-    }
-    if (k < K) {
-      float* dst = dx + (long long)n * dxns + (long long)k * S + vd;
-      if (GV) {
-        if (vd < S) {
-          if (accumulate) v += ldv4(dst);
-          stv4(dst, v);
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (vd + q < S) st1(dst + q, accumulate ? ld1(dst + q) + v[q] : v[q]);
-      }
-    }
+    for (int t = 0; t < JT; ++t)
+      if (lk == 0 && (lr & 7) == 0) bpart[(long long)blockIdx.x * (J / 8) + (jb + 16 * t + lr) / 8] = bsum[t];
   }
 }
 
@@ -1384,6 +1401,19 @@ int pw_bwd_weight_launch(const TD* dy, long long dy_nstride, const TX* x, long l
 #define L3U_PW_BWD_WIDE 1
 #endif
 bool pw_bwd_wide(int J) { return L3U_PW_BWD_WIDE && (J == 64 || J == 128); }
+#ifndef L3U_PWW_TPB_MAX
+#define L3U_PWW_TPB_MAX 8
+#endif
+// 64-voxel tiles per workgroup of pw_bwd_wide_kernel: one at the latency-bound small levels, up
+// to L3U_PWW_TPB_MAX on big volumes (fewer weight-gradient partials to write and reduce) while
+// each sample keeps >= 32 workgroups per column block
+int pww_tpb(int S) {
+  const int ntile = (S + 63) / 64;
+  int t = 1;
+  while (2 * t <= L3U_PWW_TPB_MAX && ntile / (2 * t) >= 32) t *= 2;
+  return t;
+}
+int pww_nblk(int S) { const int t = pww_tpb(S); return ((S + 63) / 64 + t - 1) / t; }
 
 // every pointer aligned to 4 elements of T (one vector load / store)
 template <typename T>
@@ -1445,10 +1475,13 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
                   (y == nullptr || (al4<T>(y) && y_nstride % 4 == 0));
   L3U_REQUIRE(al);
   if (pw_bwd_wide(J)) {
-    dim3 grid(N * ((S + 63) / 64), (K + 15) / 16), block(256);
-#define PWBW(T_, P_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T, T_, 4, P_, 0>), grid, block, 0, stream, \
+    dim3 grid(N * pww_nblk(S), (K + 15) / 16), block(256);
+#define PWBW(T_, P_) do { if (pww_tpb(S) > 1) hipLaunchKernelGGL((pw_bwd_wide_kernel<T, T_, 4, P_, 0, true>), grid, \
+      block, 0, stream, dy, dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, \
+      accumulate, part, nullptr, N, J, K, S, 0, 0, pww_tpb(S)); \
+      else hipLaunchKernelGGL((pw_bwd_wide_kernel<T, T_, 4, P_, 0>), grid, block, 0, stream, \
       dy, dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, \
-      accumulate, part, nullptr, N, J, K, S, 0, 0)
+      accumulate, part, nullptr, N, J, K, S, 0, 0, 1); } while (0)
     if (J == 64) { if (y) PWBW(1, 1); else PWBW(1, 0); }
     else { if (y) PWBW(2, 1); else PWBW(2, 0); }
 #undef PWBW
@@ -1496,10 +1529,13 @@ int convt_bwd_fused_impl(const float* dy, long long dy_nstride, const T* x, long
   const int S = D * H * W, J = Co * 8;
   const bool vec = W % 4 == 0 && S % 4 == 0 && dy_nstride % 4 == 0 && x_nstride % 4 == 0 &&
                    dx_nstride % 4 == 0 && al4<float>(dy) && al4<T>(x) && al4<float>(dx);
-  dim3 grid(N * ((S + 63) / 64), (Ci + 15) / 16);
-#define CTB(T_, NW_, G_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T, T_, NW_, 0, G_>), grid, dim3(64 * NW_), \
+  dim3 grid(N * pww_nblk(S), (Ci + 15) / 16);
+#define CTB(T_, NW_, G_) do { if (pww_tpb(S) > 1) hipLaunchKernelGGL((pw_bwd_wide_kernel<T, T_, NW_, 0, G_, true>), \
+      grid, dim3(64 * NW_), 0, stream, dy, dy_nstride, nullptr, 0, nullptr, nullptr, 0, x, x_nstride, w, dx, \
+      dx_nstride, 0, wpart, bpart, N, J, Ci, S, H, W, pww_tpb(S)); \
+      else hipLaunchKernelGGL((pw_bwd_wide_kernel<T, T_, NW_, 0, G_>), grid, dim3(64 * NW_), \
       0, stream, dy, dy_nstride, nullptr, 0, nullptr, nullptr, 0, x, x_nstride, w, dx, dx_nstride, 0, \
-      wpart, bpart, N, J, Ci, S, H, W)
+      wpart, bpart, N, J, Ci, S, H, W, 1); } while (0)
 #define CTB_G(T_, NW_) do { if (vec) CTB(T_, NW_, 1); else CTB(T_, NW_, 2); } while (0)
   if (J == 64) CTB_G(1, 4);
   else if (J == 128) CTB_G(2, 4);
@@ -1629,7 +1665,7 @@ int l3u_pw_bwd_supported(int J, int K, int S) {
 
 int l3u_pw_bwd_nparts(int N, int J, int K, int S) {
   if (!l3u_pw_bwd_supported(J, K, S)) return 0;
-  return pw_bwd_wide(J) ? N * ((S + 63) / 64) : l3u_pw_bwd_weight_nparts(N, S);
+  return pw_bwd_wide(J) ? N * pww_nblk(S) : l3u_pw_bwd_weight_nparts(N, S);
 }
 
 // fused ConvTranspose3d backward: Co*8 = 16 * 2 * NWV rows (Co in {8, 16, 32, 64}).  Offered for
@@ -1640,7 +1676,7 @@ int l3u_convt_bwd_fused_nparts(int N, int Ci, int Co, int D, int H, int W) {
   if (!(N > 0 && Ci > 0 && (Co == 8 || Co == 16 || Co == 32 || Co == 64) && D > 0 && H > 0 && W > 0))
     return 0;
   if ((!L3U_CONVT_ONEPASS_ANYW && W % 4 != 0) || D * H * W > L3U_CONVT_ONEPASS_MAX_S) return 0;
-  return N * ((D * H * W + 63) / 64);
+  return N * pww_nblk(D * H * W);
 }
 
 }  // extern "C"
