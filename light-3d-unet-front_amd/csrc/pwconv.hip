@@ -1401,6 +1401,9 @@ int pw_bwd_weight_launch(const TD* dy, long long dy_nstride, const TX* x, long l
 #define L3U_PW_BWD_WIDE 1
 #endif
 bool pw_bwd_wide(int J) { return L3U_PW_BWD_WIDE && (J == 64 || J == 128); }
+#ifndef L3U_PWBF_NK_MAX
+#define L3U_PWBF_NK_MAX 4   // K columns per fused-backward workgroup, in 16s
+#endif
 #ifndef L3U_PWW_TPB_MAX
 #define L3U_PWW_TPB_MAX 8
 #endif
@@ -1439,6 +1442,7 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
   const int NJ = J <= 16 ? 1 : 2;
   int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
+  if (NK > L3U_PWBF_NK_MAX) NK = L3U_PWBF_NK_MAX;
   while (NK > 1 && (long long)N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < L3U_PWBF_MIN_BLOCKS) NK >>= 1;
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
@@ -1491,6 +1495,7 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
   const int NJ = J <= 16 ? 1 : 2;
   // K columns per workgroup: all of them unless the grid would be too small to fill the chip
   int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
+  if (NK > L3U_PWBF_NK_MAX) NK = L3U_PWBF_NK_MAX;
   while (NK > 1 && (long long)N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < L3U_PWBF_MIN_BLOCKS) NK >>= 1;
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);   // one sweep of the chunk per workgroup
