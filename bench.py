@@ -348,7 +348,7 @@ def gemm_mfma_evidence(top=5):
     """MFMA-busy fractions of the step's GEMM launches from the committed rocprofv3 passes
     (tools/pmc_step.sh + tools/pmc_gemm.sh -> tools/pmc_launch_json.py -> profiles/*_pmc_step.json)."""
     import glob
-    files = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r2*_pmc_step.json")))]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_step.json")))
     items, src = [], None
     for fn in reversed(files):   # the newest pass that carries the MFMA counters
         with open(fn) as f:

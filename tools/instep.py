@@ -16,6 +16,17 @@ import sys
 PEAK = 8000.0
 
 
+def kernel_name(raw):
+    """Readable kernel name; rocprofv3 leaves the bf16 (DF16b) instantiations mangled: keep their
+    identifier and mark them <bf16 ...>."""
+    n = re.sub(r"\(.*", "", raw.replace("void ", "").replace("(anonymous namespace)::", ""))
+    m = re.match(r"_ZN12_GLOBAL__N_1(\d+)", n)
+    if m:
+        ln = int(m.group(1))
+        n = n[m.end():m.end() + ln] + "<bf16 ...>"
+    return n
+
+
 def step_kernels(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     ends = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
@@ -24,8 +35,7 @@ def step_kernels(path):
     steps = [s for s in steps if len(s) == n][1:]
     out = []
     for i in range(n):
-        name = re.sub(r"\(.*", "", steps[-1][i]["Kernel_Name"].replace("void ", "")
-                      .replace("(anonymous namespace)::", ""))
+        name = kernel_name(steps[-1][i]["Kernel_Name"])
         us = sum(int(s[i]["End_Timestamp"]) - int(s[i]["Start_Timestamp"]) for s in steps) / len(steps) / 1e3
         out.append((name, us))
     return out, len(steps)

@@ -14,8 +14,10 @@ for i in range(n):
     r = steps[-1][i]
     d = sum(int(s[i]["End_Timestamp"]) - int(s[i]["Start_Timestamp"]) for s in steps) / len(steps) / 1e3
     tot += d
-    name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
-    name = re.sub(r"\(.*", "", name)
+    name = re.sub(r"\(.*", "", r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", ""))
+    m = re.match(r"_ZN12_GLOBAL__N_1(\d+)", name)   # bf16 instantiations stay mangled
+    if m:
+        name = name[m.end():m.end() + int(m.group(1))] + "<bf16 ...>"
     print(f"{d:7.1f} {name[:44]:44s} {r['Grid_Size_X']}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']}/"
           f"{r['Workgroup_Size_X']} v{r['VGPR_Count']}")
 print(f"sum {tot:.1f} us, {n} launches, mean of {len(steps)} steps")
