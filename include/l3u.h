@@ -174,6 +174,17 @@ int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long 
                const float* rec, const double* in_part, int npart, const float* x,
                long long x_nstride, const float* w, float* dx, long long dx_nstride, int accumulate,
                float* part, int N, int J, int K, int S, hipStream_t stream);
+/* two plain l3u_pw_bwd calls (y == NULL) of the same J, N and S in ONE launch (a ResidualBlock's
+ * conv2.pointwise and Conv1x1 shortcut backwards, unet3d.py:18,70-73: both read the block tail's
+ * dy2 / dr), for the shapes l3u_pw_bwd2_supported(J, S) accepts (J in {64, 128}, the 12^3 / 6^3
+ * levels); each problem gets l3u_pw_bwd_nparts(N, J, K, S) partials and the results are the two
+ * calls' bit for bit.                                                                            */
+int l3u_pw_bwd2_supported(int J, int S);
+int l3u_pw_bwd2(const float* dya, long long dya_nstride, const float* xa, long long xa_nstride,
+                const float* wa, float* dxa, long long dxa_nstride, int acc_a, float* part_a, int Ka,
+                const float* dyb, long long dyb_nstride, const float* xb, long long xb_nstride,
+                const float* wb, float* dxb, long long dxb_nstride, int acc_b, float* part_b, int Kb,
+                int N, int J, int S, hipStream_t stream);
 
 /* ---- InstanceNorm3d(affine=True, eps=1e-5) + LeakyReLU(0.01) + Dropout3d + residual --------
  * replaces nn.InstanceNorm3d / nn.LeakyReLU / nn.Dropout3d / "out + residual"
@@ -480,6 +491,11 @@ int l3u_dw3_bwd_bf16(const float* dz, long long dz_nstride, const l3u_bf16* x, l
                      const float* w, const float* rec, float* dx, long long dx_nstride,
                      int accumulate, float* dw_part, double* in_part, int N, int C, int D, int H,
                      int W, hipStream_t stream);
+int l3u_dwpw_fwd_bf16(const l3u_bf16* x, long long x_nstride, const float* w_dw, const float* rec,
+                      const l3u_norm_src* src, const float* w_pw, l3u_bf16* y, long long y_nstride,
+                      float* y_stat, const float* w_sc, l3u_bf16* r, long long r_nstride,
+                      float* r_stat, l3u_bf16* z, long long z_nstride, int N, int K, int Nout,
+                      int D, int H, int W, hipStream_t stream);
 int l3u_maxpool2_fwd_bf16(const l3u_bf16* x, long long x_nstride, l3u_bf16* y, long long y_nstride,
                           unsigned char* idx, int N, int C, int D, int H, int W,
                           hipStream_t stream);
@@ -496,6 +512,17 @@ int l3u_outconv_bwd_ftl_bf16(const float* p, const float* t, const float* ftl_pa
                              const float* gscale, const l3u_bf16* h, long long h_nstride,
                              const float* w, float* dh, long long dh_nstride, double* part,
                              float* loss, int N, int C, int S, hipStream_t stream);
+int l3u_outconv_bwd_dz_bf16(const float* dp, const float* p, const float* t, const double* sums,
+                            double alpha, double beta, double gamma, double smooth,
+                            const float* gscale, const l3u_bf16* h, long long h_nstride,
+                            const float* w, float* dh, long long dh_nstride, double* part,
+                            float* loss, int N, int C, int S, hipStream_t stream);
+int l3u_outconv_bwd_ftl_dz_bf16(const float* p, const float* t, const float* ftl_part,
+                                int ftl_nparts, double alpha, double beta, double gamma,
+                                double smooth, const float* gscale, const l3u_bf16* h,
+                                long long h_nstride, const float* w, float* dh,
+                                long long dh_nstride, double* part, float* loss, int N, int C,
+                                int S, hipStream_t stream);
 int l3u_box_copy_bf16(const l3u_bf16* src, long long src_nstride, int sd, int sh, int sw,
                       l3u_bf16* dst, long long dst_nstride, int dd, int dh, int dw, int oz, int oy,
                       int ox, int N, int C, hipStream_t stream);
@@ -519,6 +546,17 @@ int l3u_norm_act_bwd_reduce_bf16(const float* dout, long long dout_nstride, cons
                                  const float* rec2, const l3u_bf16* r, long long r_nstride,
                                  const float* rec_r, double* part, int N, int C, int S,
                                  hipStream_t stream);
+int l3u_norm_act_bwd_reduce_up_bf16(const float* dskip, long long dskip_nstride, const float* dpool,
+                                    long long dpool_nstride, const unsigned char* idx,
+                                    const l3u_bf16* out, long long out_nstride, const l3u_bf16* y2,
+                                    long long y2_nstride, const float* rec2, const l3u_bf16* r,
+                                    long long r_nstride, const float* rec_r, double* part, int N,
+                                    int C, int D, int H, int W, hipStream_t stream);
+int l3u_norm_act_bwd_reduce_r1_bf16(const float* dz, long long dz_nstride, const float* dscale,
+                                    const l3u_bf16* out, long long out_nstride, const l3u_bf16* y2,
+                                    long long y2_nstride, const float* rec2, const l3u_bf16* r,
+                                    long long r_nstride, const float* rec_r, double* part, int N,
+                                    int C, int S, hipStream_t stream);
 int l3u_norm_act_bwd_apply_bf16(const float* dout, long long dout_nstride, const l3u_bf16* out,
                                 long long out_nstride, const l3u_bf16* y2, long long y2_nstride,
                                 const float* rec2, const l3u_bf16* r, long long r_nstride,
@@ -536,47 +574,6 @@ int l3u_in_bwd_apply_bf16(const float* dpre, long long dpre_nstride, const l3u_b
 int l3u_pw_fwd_bf16(const l3u_bf16* x, long long x_nstride, const float* w, int w_layout,
                     const float* bias, l3u_bf16* y, long long y_nstride, int accumulate,
                     float* stat_part, int N, int K, int Nout, int S, hipStream_t stream);
-int l3u_dwpw_fwd_bf16(const l3u_bf16* x, long long x_nstride, const float* w_dw, const float* rec,
-                      const l3u_norm_src* src, const float* w_pw, l3u_bf16* y, long long y_nstride,
-                      float* y_stat, const float* w_sc, l3u_bf16* r, long long r_nstride,
-                      float* r_stat, l3u_bf16* z, long long z_nstride, int N, int K, int Nout,
-                      int D, int H, int W, hipStream_t stream);
-int l3u_outconv_bwd_dz_bf16(const float* dp, const float* p, const float* t, const double* sums,
-                            double alpha, double beta, double gamma, double smooth,
-                            const float* gscale, const l3u_bf16* h, long long h_nstride,
-                            const float* w, float* dh, long long dh_nstride, double* part,
-                            float* loss, int N, int C, int S, hipStream_t stream);
-int l3u_outconv_bwd_ftl_dz_bf16(const float* p, const float* t, const float* ftl_part,
-                                int ftl_nparts, double alpha, double beta, double gamma,
-                                double smooth, const float* gscale, const l3u_bf16* h,
-                                long long h_nstride, const float* w, float* dh,
-                                long long dh_nstride, double* part, float* loss, int N, int C,
-                                int S, hipStream_t stream);
-int l3u_norm_act_bwd_reduce_r1_bf16(const float* dz, long long dz_nstride, const float* dscale,
-                                    const l3u_bf16* out, long long out_nstride, const l3u_bf16* y2,
-                                    long long y2_nstride, const float* rec2, const l3u_bf16* r,
-                                    long long r_nstride, const float* rec_r, double* part, int N,
-                                    int C, int S, hipStream_t stream);
-int l3u_pw_bwd_tail_r1_bf16(const float* dz, long long dz_nstride, const float* dscale,
-                            const l3u_bf16* out, long long out_nstride, const l3u_bf16* yr,
-                            long long yr_nstride, const float* rec, const double* tail_part,
-                            int npart, int sel, const l3u_bf16* x, long long x_nstride,
-                            const float* w, float* dx, long long dx_nstride, int accumulate,
-                            float* part, int N, int J, int K, int S, hipStream_t stream);
-int l3u_norm_act_bwd_reduce_up_bf16(const float* dskip, long long dskip_nstride,
-                                    const float* dpool, long long dpool_nstride,
-                                    const unsigned char* idx, const l3u_bf16* out,
-                                    long long out_nstride, const l3u_bf16* y2, long long y2_nstride,
-                                    const float* rec2, const l3u_bf16* r, long long r_nstride,
-                                    const float* rec_r, double* part, int N, int C, int D, int H,
-                                    int W, hipStream_t stream);
-int l3u_pw_bwd_tail_up_bf16(const float* dskip, long long dskip_nstride, const float* dpool,
-                            long long dpool_nstride, const unsigned char* idx, const l3u_bf16* out,
-                            long long out_nstride, const l3u_bf16* yr, long long yr_nstride,
-                            const float* rec, const double* tail_part, int npart, int sel,
-                            const l3u_bf16* x, long long x_nstride, const float* w, float* dx,
-                            long long dx_nstride, int accumulate, float* part, int N, int J, int K,
-                            int D, int H, int W, hipStream_t stream);
 int l3u_pw_fwd2_bf16(const l3u_bf16* xa, long long xa_nstride, const float* wa, l3u_bf16* ya,
                      long long ya_nstride, float* stat_a, const l3u_bf16* xb, long long xb_nstride,
                      const float* wb, l3u_bf16* yb, long long yb_nstride, float* stat_b, int N,
@@ -593,10 +590,29 @@ int l3u_pw_bwd_tail_bf16(const float* dout, long long dout_nstride, const l3u_bf
                          const l3u_bf16* x, long long x_nstride, const float* w, float* dx,
                          long long dx_nstride, int accumulate, float* part, int N, int J, int K,
                          int S, hipStream_t stream);
+int l3u_pw_bwd_tail_up_bf16(const float* dskip, long long dskip_nstride, const float* dpool,
+                            long long dpool_nstride, const unsigned char* idx, const l3u_bf16* out,
+                            long long out_nstride, const l3u_bf16* yr, long long yr_nstride,
+                            const float* rec, const double* tail_part, int npart, int sel,
+                            const l3u_bf16* x, long long x_nstride, const float* w, float* dx,
+                            long long dx_nstride, int accumulate, float* part, int N, int J, int K,
+                            int D, int H, int W, hipStream_t stream);
+int l3u_pw_bwd_tail_r1_bf16(const float* dz, long long dz_nstride, const float* dscale,
+                            const l3u_bf16* out, long long out_nstride, const l3u_bf16* yr,
+                            long long yr_nstride, const float* rec, const double* tail_part,
+                            int npart, int sel, const l3u_bf16* x, long long x_nstride,
+                            const float* w, float* dx, long long dx_nstride, int accumulate,
+                            float* part, int N, int J, int K, int S, hipStream_t stream);
 int l3u_pw_bwd_bf16(const float* dy, long long dy_nstride, const l3u_bf16* y, long long y_nstride,
                     const float* rec, const double* in_part, int npart, const l3u_bf16* x,
                     long long x_nstride, const float* w, float* dx, long long dx_nstride,
                     int accumulate, float* part, int N, int J, int K, int S, hipStream_t stream);
+int l3u_pw_bwd2_bf16(const float* dya, long long dya_nstride, const l3u_bf16* xa,
+                     long long xa_nstride, const float* wa, float* dxa, long long dxa_nstride,
+                     int acc_a, float* part_a, int Ka, const float* dyb, long long dyb_nstride,
+                     const l3u_bf16* xb, long long xb_nstride, const float* wb, float* dxb,
+                     long long dxb_nstride, int acc_b, float* part_b, int Kb, int N, int J, int S,
+                     hipStream_t stream);
 int l3u_convt_bwd_fused_bf16(const float* dy, long long dy_nstride, const l3u_bf16* x,
                              long long x_nstride, const float* w, float* dx, long long dx_nstride,
                              float* wpart, float* bpart, int N, int Ci, int Co, int D, int H, int W,

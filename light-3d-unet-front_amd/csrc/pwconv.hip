@@ -802,14 +802,28 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
 // (the ConvTranspose3d weight [Ci][Co*8]) and so are the partials; bpart != NULL receives the
 // bias partials sum_{tile, abc} dY[co] per (tile, co) from the K-tile-0 workgroups.
 // Partials are per 64-voxel tile: part[N * ceil(S/64)][J][K] ([K][J] for GATHER).
+// the second problem of a paired wide launch (l3u_pw_bwd2): same J, N, S; its own dY, X, W, dX,
+// K, accumulate flag and partials (blockIdx.z == 1)
+template <typename T>
+struct WideSecond {
+  const float* dy; long long dyns; const T* x; long long xns; const float* w; float* dx;
+  long long dxns; int accumulate; float* part; int K;
+};
+
 template <typename T, int JT, int NWV, int PRO, int GATHER, bool MT = false>
 __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
     const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
     const T* __restrict__ x, long long xns, const float* __restrict__ w,
     float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part,
-    float* __restrict__ bpart, int N, int J, int K, int S, int Hq, int Wq, int tpb) {
+    float* __restrict__ bpart, int N, int J, int K, int S, int Hq, int Wq, int tpb,
+    WideSecond<T> p2 = WideSecond<T>{}) {
   L3U_STAMP_SCOPE(105);
+  if (blockIdx.z == 1) {   // paired launch, second problem (PRO 0, no gather)
+    dy = p2.dy; dyns = p2.dyns; x = p2.x; xns = p2.xns; w = p2.w; dx = p2.dx; dxns = p2.dxns;
+    accumulate = p2.accumulate; part = p2.part; K = p2.K;
+  }
+  if ((int)blockIdx.y * 16 >= K) return;   // the narrower problem's unused column blocks
   constexpr int JW = 16 * JT;                 // dY rows per wave
   constexpr bool GV = GATHER != 2;            // vector loads
   constexpr bool G = GATHER != 0;
@@ -1526,6 +1540,34 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
   L3U_CHECK_LAUNCH();
 }
 
+// two independent plain (PRO 0) wide backwards of the same J, N and S in one launch: a block's
+// conv2.pointwise and its Conv1x1 shortcut at the 12^3 / 6^3 levels (both read the block tail's
+// dy2 / dr), grid.z selects the problem
+template <typename T>
+int pw_bwd2_impl(const float* dya, long long dya_nstride, const T* xa, long long xa_nstride,
+                 const float* wa, float* dxa, long long dxa_nstride, int acc_a, float* part_a,
+                 int Ka, const float* dyb, long long dyb_nstride, const T* xb, long long xb_nstride,
+                 const float* wb, float* dxb, long long dxb_nstride, int acc_b, float* part_b,
+                 int Kb, int N, int J, int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && pw_bwd_wide(J) && Ka > 0 && Kb > 0 && S > 0 && pww_tpb(S) == 1);
+  L3U_REQUIRE(dya && xa && wa && dxa && part_a && dyb && xb && wb && dxb && part_b);
+  const bool al = al4<float>(dya) && al4<T>(xa) && al4<float>(dxa) && al4<float>(dyb) && al4<T>(xb) &&
+                  al4<float>(dxb) && dya_nstride % 4 == 0 && xa_nstride % 4 == 0 &&
+                  dxa_nstride % 4 == 0 && dyb_nstride % 4 == 0 && xb_nstride % 4 == 0 &&
+                  dxb_nstride % 4 == 0;
+  L3U_REQUIRE(al);
+  const WideSecond<T> p2{dyb, dyb_nstride, xb, xb_nstride, wb, dxb, dxb_nstride, acc_b, part_b, Kb};
+  const int K = Ka > Kb ? Ka : Kb;
+  dim3 grid(N * pww_nblk(S), (K + 15) / 16, 2), block(256);
+#define PWB2(T_) hipLaunchKernelGGL((pw_bwd_wide_kernel<T, T_, 4, 0, 0>), grid, block, 0, stream, dya, \
+      dya_nstride, nullptr, 0, nullptr, nullptr, 0, xa, xa_nstride, wa, dxa, dxa_nstride, acc_a, part_a, \
+      nullptr, N, J, Ka, S, 0, 0, 1, p2)
+  if (J == 64) PWB2(1);
+  else PWB2(2);
+#undef PWB2
+  L3U_CHECK_LAUNCH();
+}
+
 template <typename T>
 int convt_bwd_fused_impl(const float* dy, long long dy_nstride, const T* x, long long x_nstride,
                          const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
@@ -1668,6 +1710,8 @@ int l3u_pw_bwd_supported(int J, int K, int S) {
   return (pw_bwd_wide(J) || (J <= 32 && K <= 64)) ? 1 : 0;
 }
 
+int l3u_pw_bwd2_supported(int J, int S) { return pw_bwd_wide(J) && pww_tpb(S) == 1 ? 1 : 0; }
+
 int l3u_pw_bwd_nparts(int N, int J, int K, int S) {
   if (!l3u_pw_bwd_supported(J, K, S)) return 0;
   return pw_bwd_wide(J) ? N * pww_nblk(S) : l3u_pw_bwd_weight_nparts(N, S);
@@ -1739,6 +1783,14 @@ L3U_TWIN(l3u_pw_bwd_tail_r1, P_PBT1, dscale == nullptr ? (int)hipErrorInvalidVal
     int K, int S, hipStream_t stream)
 L3U_TWIN(l3u_pw_bwd, P_PBD, pw_bwd_impl(dy, dy_nstride, bp(y), y_nstride, rec, in_part, npart,
          bp(x), x_nstride, w, dx, dx_nstride, accumulate, part, N, J, K, S, stream))
+#define P_PB2(TT) (const float* dya, long long dya_nstride, const TT* xa, long long xa_nstride,     \
+    const float* wa, float* dxa, long long dxa_nstride, int acc_a, float* part_a, int Ka,           \
+    const float* dyb, long long dyb_nstride, const TT* xb, long long xb_nstride, const float* wb,  \
+    float* dxb, long long dxb_nstride, int acc_b, float* part_b, int Kb, int N, int J, int S,      \
+    hipStream_t stream)
+L3U_TWIN(l3u_pw_bwd2, P_PB2, pw_bwd2_impl(dya, dya_nstride, bp(xa), xa_nstride, wa, dxa, dxa_nstride,
+         acc_a, part_a, Ka, dyb, dyb_nstride, bp(xb), xb_nstride, wb, dxb, dxb_nstride, acc_b, part_b,
+         Kb, N, J, S, stream))
 #define P_CBF(TT) (const float* dy, long long dy_nstride, const TT* x, long long x_nstride,         \
     const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart, int N, int Ci,     \
     int Co, int D, int H, int W, hipStream_t stream)

@@ -32,6 +32,8 @@ _SIGS = {
     "l3u_pw_bwd_supported": [I, I, I],
     "l3u_pw_bwd_nparts": [I, I, I, I],
     "l3u_pw_bwd": [P, L, P, L, P, P, I, P, L, P, P, L, I, P, I, I, I, I, P],
+    "l3u_pw_bwd2_supported": [I, I],
+    "l3u_pw_bwd2": [P, L, P, L, P, P, L, I, P, I, P, L, P, L, P, P, L, I, P, I, I, I, I, P],
     "l3u_in_finalize": [P, I, P, P, F, U64, P, I, P, I, I, P],
     "l3u_norm_act_nblocks": [I],
     "l3u_norm_act_fwd": [P, L, P, P, P, L, P, P, I, P, L, I, I, I, P],
@@ -92,7 +94,7 @@ _SIGS = {
 # entry points with a _bf16 twin (same arguments; saved activations stored as bf16, gradients
 # fp32, include/l3u.h)
 BF16_TWINS = ("l3u_dw3_fwd", "l3u_dw3_bwd", "l3u_pw_fwd", "l3u_pw_fwd2", "l3u_pw_bwd_weight",
-              "l3u_pw_bwd", "l3u_pw_bwd_tail", "l3u_convt_fwd", "l3u_convt_bwd",
+              "l3u_pw_bwd", "l3u_pw_bwd2", "l3u_pw_bwd_tail", "l3u_convt_fwd", "l3u_convt_bwd",
               "l3u_convt_bwd_fused", "l3u_norm_act_fwd", "l3u_norm_act_pool_fwd",
               "l3u_norm_act_bwd_reduce", "l3u_norm_act_bwd_apply", "l3u_norm_act_bwd",
               "l3u_in_bwd_apply", "l3u_maxpool2_fwd", "l3u_outconv_fwd", "l3u_outconv_bwd",
@@ -108,7 +110,7 @@ _QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_
             "l3u_norm_act_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks",
             "l3u_gconv3_nblocks", "l3u_gconv3_wgrad_nparts", "l3u_front_nblocks",
             "l3u_ccl_nchunks", "l3u_dwpw_supported", "l3u_dwpw_stat_nsb",
-            "l3u_dw3_bwd_rank1"}
+            "l3u_dw3_bwd_rank1", "l3u_pw_bwd2_supported"}
 
 _lib = None
 

@@ -35,6 +35,9 @@ _SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32").sp
 # at least this many voxels (the 48^3 level; at 24^3 its 1024-thread slabs are too few to fill
 # the chip, tools/dwpw_bench.py); L3U_DWPW=0 disables
 _DWPW = os.environ.get("L3U_DWPW", "1") != "0"
+# a block's conv2.pointwise and shortcut backwards as one launch at the 12^3 / 6^3 levels
+# (l3u_pw_bwd2); L3U_PAIR_BWD=0 keeps them separate
+_PAIR_BWD = os.environ.get("L3U_PAIR_BWD", "1") != "0"
 _DWPW_MIN_S = int(os.environ.get("L3U_DWPW_MIN_S", "65536"))
 # the out_conv backward hands the last block d(pre-sigmoid) and w (out_conv is rank-1) instead
 # of the [N, C, S] output gradient (l3u_outconv_bwd_dz + the _r1 tail kernels); L3U_RANK1=0
@@ -912,6 +915,7 @@ class UNetEngine:
         y1v = sv.get("y1v") or V(sv["y1"], 0, cout * S, cout)   # rank-1: z1, negative stride
         # (1) block tail: out = lrelu(IN2(y2) + residual)
         fused = self._tail_fusable(sv, cin, cout, S)
+        sc_done = False   # the shortcut's d(input) already written (paired with conv2's backward)
         dz2 = e(N, cout, S)
         if fused:
             # (1+2) the tail reduce, then conv2.pointwise backward with the tail's apply in its
@@ -922,9 +926,17 @@ class UNetEngine:
                               V(dz2, 0, cout * S, cout), 0, N, S, st)
         else:
             dy2, drv = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev)
-            # (2) conv2.pointwise backward
-            self._pw_bwd(flat, V(dy2, 0, cout * S, cout), None, V(z2, 0, cout * S, cout),
-                         pre + "conv2.pointwise.weight", V(dz2, 0, cout * S, cout), 0, N, S, st)
+            # (2) conv2.pointwise backward; at the 12^3 / 6^3 levels paired in one launch with the
+            # shortcut backward (both read the tail's outputs), which then writes d(input) first
+            if (_PAIR_BWD and shortcut and nat.query("l3u_pw_bwd2_supported", cout, S)
+                    and nat.query("l3u_pw_bwd_supported", cout, cin, S)):
+                self._pw_bwd2(flat, (V(dy2, 0, cout * S, cout), V(z2, 0, cout * S, cout),
+                                     pre + "conv2.pointwise.weight", V(dz2, 0, cout * S, cout)),
+                              (drv, x, pre + "shortcut.0.weight", dxv), N, S, st)
+                sc_done = True
+            else:
+                self._pw_bwd(flat, V(dy2, 0, cout * S, cout), None, V(z2, 0, cout * S, cout),
+                             pre + "conv2.pointwise.weight", V(dz2, 0, cout * S, cout), 0, N, S, st)
         # (3) conv2.depthwise backward fused with LeakyReLU/Dropout/IN1 backward partials
         nch = nat.query("l3u_dw3_nchunk", N, cout, d, h, w)
         pd2 = A.alloc(cout * N * nch * 27)
@@ -953,15 +965,18 @@ class UNetEngine:
                          N, S, st)
         dy1 = dpre
         # (5) conv1.depthwise backward: writes d(input) (Conv1x1 shortcut) or accumulates into the
-        # identity-shortcut gradient already there
+        # identity-shortcut gradient (or the paired shortcut's) already there; a + b == b + a, so
+        # the order of the two terms does not change a bit
         nch1 = nat.query("l3u_dw3_nchunk", N, cin, d, h, w)
         pd1 = A.alloc(cin * N * nch1 * 27)
         self._call("l3u_dw3_bwd", dz1.data_ptr(), cin * S, x.p, x.ns,
                    self._w(flat, pre + "conv1.depthwise.weight"), None, dxv.p, dxv.ns,
-                   0 if shortcut else 1, A.ptr(pd1), None, N, cin, d, h, w, st)
+                   0 if shortcut and not sc_done else 1, A.ptr(pd1), None, N, cin, d, h, w, st)
         self._seg_dw(pd1, N * nch1, cin, pre + "conv1.depthwise.weight")
         # (6) shortcut conv backward accumulates into d(input)
-        if fused:
+        if sc_done:
+            pass
+        elif fused:
             self._pw_bwd_tail(flat, dout, sv["out"], sv["r"], rec_r, pn, ntp, 2, x,
                               pre + "shortcut.0.weight", dxv, 1, N, S, st)
         elif shortcut:
@@ -993,6 +1008,22 @@ class UNetEngine:
                          K, S, st)
             self._call("l3u_pw_bwd_weight", dy.p, dy.ns, x.p, x.ns, A.ptr(part), N, J, K, S, st)
         self._seg(part, npw, J * K, 1, J * K, name)
+
+    def _pw_bwd2(self, flat, a, b, N, S, st):
+        """Two plain _pw_bwd calls (dy, x, weight name, dx) of the same J in one launch
+        (l3u_pw_bwd2); both dx are overwritten."""
+        A = self.bwd_arena
+        J = a[0].C
+        parts = []
+        for dy, x, name, dx in (a, b):
+            npw = nat.query("l3u_pw_bwd_nparts", N, J, x.C, S)
+            parts.append((A.alloc(npw * J * x.C), npw, x.C, name))
+        (dya, xa, _, dxa), (dyb, xb, _, dxb) = a, b
+        self._call("l3u_pw_bwd2", dya.p, dya.ns, xa.p, xa.ns, self._w(flat, a[2]), dxa.p, dxa.ns, 0,
+                   A.ptr(parts[0][0]), xa.C, dyb.p, dyb.ns, xb.p, xb.ns, self._w(flat, b[2]), dxb.p,
+                   dxb.ns, 0, A.ptr(parts[1][0]), xb.C, N, J, S, st)
+        for off, npw, K, name in parts:
+            self._seg(off, npw, J * K, 1, J * K, name)
 
     def _pw_bwd_tail(self, flat, dout, out, yr, rec, pn, ntp, sel, x, name, dx, accumulate, N, S,
                      st):

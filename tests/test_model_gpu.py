@@ -299,7 +299,9 @@ def test_trainstep_data_parallel_two_ranks(cuda, tmp_path):
 @pytest.mark.parametrize("switch,fixture", [("_RANK1", "model_b2_32.npz"),
                                             ("_POOLFOLD", "model_b2_32.npz"),
                                             ("_POOLFOLD", "model_b1_48.npz"),
-                                            ("_FRONT_R1", "model_b1_48.npz")])
+                                            ("_FRONT_R1", "model_b1_48.npz"),
+                                            ("_PAIR_BWD", "model_b1_48.npz"),
+                                            ("_PAIR_BWD", "model_b2_32.npz")])
 def test_formed_on_load_gradients_bitwise(cuda, golden, switch, fixture):
     """Output gradients formed on load give bitwise the gradients of the materialised tensors,
     for the FocalTversky and the given-dL/dp forms of the backward:
@@ -310,7 +312,10 @@ def test_formed_on_load_gradients_bitwise(cuda, golden, switch, fixture):
     _FRONT_R1: the first block's rank-1 activations y1 = w1[c] * z1 and r = wsc[c] * x
     (unet3d.py:163-167, one input channel) formed on load by the fused conv2, the block tail,
     the IN-fused depthwise backward and the pointwise backwards instead of stored (48^3: the
-    shapes where all of them take the rank-1 form).  The output is compared too."""
+    shapes where all of them take the rank-1 form);
+    _PAIR_BWD: a block's conv2.pointwise and shortcut backwards in one launch at the 12^3 / 6^3
+    levels (l3u_pw_bwd2), the shortcut writing d(input) before the depthwise backward adds to it.
+    The output is compared too."""
     import light_unet.engine as E
     from light_unet.models.unet3d import Lightweight3DUNet
     from light_unet.train_step import TrainStep

@@ -299,6 +299,36 @@ def test_pw_bwd_fused(cuda, case):
     close(part.view(P, J, K).double().sum(0), ref_dw, 2e-5, f"pw_bwd dw {case}")
 
 
+@pytest.mark.parametrize("case", [(4, 64, 64, 32, 12 ** 3), (4, 128, 128, 64, 6 ** 3), (2, 64, 128, 64, 12 ** 3),
+                                  (2, 128, 40, 24, 5 * 6 * 8)])
+def test_pw_bwd2_equals_two_calls(cuda, case):
+    """l3u_pw_bwd2 (a block's conv2.pointwise and shortcut backwards in one launch) gives the two
+    plain l3u_pw_bwd calls' dX and weight-gradient partials bit for bit."""
+    N, J, Ka, Kb, S = case
+    assert nat().query("l3u_pw_bwd2_supported", J, S) == 1
+    gen = torch.Generator().manual_seed(15)
+    r = lambda *s: torch.randn(*s, generator=gen).to(cuda)  # noqa: E731
+    dya, xa, wa, dyb, xb, wb = r(N, J, S), r(N, Ka, S), r(J, Ka), r(N, J, S), r(N, Kb, S), r(J, Kb)
+    P = nat().query("l3u_pw_bwd_nparts", N, J, Ka, S)
+    assert P == nat().query("l3u_pw_bwd_nparts", N, J, Kb, S)
+    out = []
+    for paired in (True, False):
+        dxa, dxb = torch.full((N, Ka, S), float("nan"), device=cuda), torch.full((N, Kb, S), float("nan"), device=cuda)
+        pa, pb = torch.full((P * J * Ka,), float("nan"), device=cuda), torch.full((P * J * Kb,), float("nan"), device=cuda)
+        if paired:
+            nat().call("l3u_pw_bwd2", dya.data_ptr(), J * S, xa.data_ptr(), Ka * S, wa.data_ptr(), dxa.data_ptr(),
+                       Ka * S, 0, pa.data_ptr(), Ka, dyb.data_ptr(), J * S, xb.data_ptr(), Kb * S, wb.data_ptr(),
+                       dxb.data_ptr(), Kb * S, 0, pb.data_ptr(), Kb, N, J, S, st())
+        else:
+            for dy, x, w, dx, p, K in ((dya, xa, wa, dxa, pa, Ka), (dyb, xb, wb, dxb, pb, Kb)):
+                nat().call("l3u_pw_bwd", dy.data_ptr(), J * S, None, 0, None, None, 0, x.data_ptr(), K * S,
+                           w.data_ptr(), dx.data_ptr(), K * S, 0, p.data_ptr(), N, J, K, S, st())
+        torch.cuda.synchronize()
+        out.append((dxa, dxb, pa, pb))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 def test_pw_bwd_matches_unfused(cuda):
     """The fused call reproduces in_bwd_apply + pw_fwd(data) + pw_bwd_weight to fp32 rounding."""
     N, J, K, S = 2, 16, 32, 12 ** 3
