@@ -81,13 +81,14 @@ def synthetic_pool(n_pool, bs, size, rank, device):
     return pool
 
 
-def dw_bytes(N, C, S, e=4):
+def dw_bytes(N, C, S, e=4, acc=0):
     """Algorithmic HBM bytes of one depthwise backward (data + weight gradient):
-    read dZ + write dX (fp32 gradients) + read X (e = 4 fp32 / 2 bf16 activations) + 27 weights."""
-    return 4 * (2 * N * C * S) + e * N * C * S + 4 * 27 * C
+    read dZ + write dX (fp32 gradients) + read X (e = 4 fp32 / 2 bf16 activations) + 27 weights,
+    + read dX when the call accumulates into it (acc)."""
+    return 4 * ((2 + acc) * N * C * S) + e * N * C * S + 4 * 27 * C
 
 
-def pmc_traffic(N, C, size):
+def pmc_traffic(N, C, size, acc=0):
     """Memory-side bytes per call of the dominant kernel from the committed rocprofv3 PMC passes
     (tools/pmc.sh -> profiles/*_pmc_dw3_bwd.json), when they were taken at this exact shape."""
     import glob
@@ -97,6 +98,8 @@ def pmc_traffic(N, C, size):
     with open(files[-1]) as f:
         rec = json.load(f)
     if f"[{N},{C},{size}^3]" not in rec.get("call", ""):
+        return None, None
+    if f"accumulate={acc}" not in rec.get("call", ""):   # taken in the step's mode
         return None, None
     return rec["traffic_bytes"], os.path.relpath(files[-1], ROOT) + " (FETCH_SIZE x2 + WRITE_SIZE)"
 
@@ -777,7 +780,7 @@ def bf16_bench(device, args, enc, world, rank, pool):
     lv = float(loss.item())
     if not np.isfinite(lv):
         raise SystemExit(f"bf16 step: non-finite loss {lv}")
-    b = dw_bytes(N, cdom, S, e=2)
+    b = dw_bytes(N, cdom, S, e=2, acc=int(bool(dom[0][1][8])) if dom else 0)
     ach = b / (dom_ms * 1e-3) / 1e9 if dom_ms else None
     return {"workload": "same step, bf16 activation storage (fp32 weights / AdamW / gradients / "
                         "accumulation), graph-replayed", "n_gpus": world,
@@ -919,9 +922,10 @@ def main():
     if rank == 0:
         patches = world * args.batch * args.steps
         value = patches / elapsed
-        dbytes = dw_bytes(N, cdom, S, e=2 if args.dtype == "bf16" else 4)
+        dacc = int(bool(dom_calls[0][1][8])) if dom_calls else 0   # accumulates into d(input)
+        dbytes = dw_bytes(N, cdom, S, e=2 if args.dtype == "bf16" else 4, acc=dacc)
         achieved = dbytes / (dom_ms * 1e-3) / 1e9 if dom_ms else None
-        traffic, traffic_src = pmc_traffic(N, cdom, args.size)
+        traffic, traffic_src = pmc_traffic(N, cdom, args.size, dacc)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -955,7 +959,8 @@ def main():
             "roofline": {
                 "kernel": f"l3u_dw3_bwd [{N},{cdom},{args.size}^3] (up3.res_block.conv1.depthwise "
                           "backward: one single-pass launch, data and weight gradients from one "
-                          "LDS-DMA-staged read of dZ and A)",
+                          "LDS-DMA-staged read of dZ and A"
+                          + (", adding to the shortcut's d(input))" if dacc else ")"),
                 "bound": "hbm",
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS,

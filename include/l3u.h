@@ -179,6 +179,21 @@ int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long 
  * dy2 / dr), for the shapes l3u_pw_bwd2_supported(J, S) accepts (J in {64, 128}, the 12^3 / 6^3
  * levels); each problem gets l3u_pw_bwd_nparts(N, J, K, S) partials and the results are the two
  * calls' bit for bit.                                                                            */
+/* the block tail's two pointwise backwards (conv2.pointwise: sel 1, yr = y2; the Conv1x1
+ * shortcut: sel 2, yr = r) of l3u_pw_bwd_tail in ONE launch, dout as l3u_pw_bwd_tail (dscale and
+ * dpool NULL), l3u_pw_bwd_tail_r1 (dscale) or l3u_pw_bwd_tail_up (dpool, idx and the plane Hf x Wf);
+ * no rank-1 yr; each problem's partials as l3u_pw_bwd_nparts(N, J, K, S), results bit-identical to
+ * the two calls.                                                                                */
+int l3u_pw_bwd_tail_pair(const float* dout, long long dout_nstride, const float* dscale,
+                         const float* dpool, long long dpool_nstride, const unsigned char* idx,
+                         int Hf, int Wf, const float* out, long long out_nstride,
+                         const double* tail_part, int npart, const float* yra, long long yra_nstride,
+                         const float* reca, const float* xa, long long xa_nstride, const float* wa,
+                         float* dxa, long long dxa_nstride, int acc_a, float* part_a, int Ka,
+                         int sel_a, const float* yrb, long long yrb_nstride, const float* recb,
+                         const float* xb, long long xb_nstride, const float* wb, float* dxb,
+                         long long dxb_nstride, int acc_b, float* part_b, int Kb, int sel_b, int N,
+                         int J, int S, hipStream_t stream);
 int l3u_pw_bwd2_supported(int J, int S);
 int l3u_pw_bwd2(const float* dya, long long dya_nstride, const float* xa, long long xa_nstride,
                 const float* wa, float* dxa, long long dxa_nstride, int acc_a, float* part_a, int Ka,
@@ -603,6 +618,17 @@ int l3u_pw_bwd_tail_r1_bf16(const float* dz, long long dz_nstride, const float* 
                             int npart, int sel, const l3u_bf16* x, long long x_nstride,
                             const float* w, float* dx, long long dx_nstride, int accumulate,
                             float* part, int N, int J, int K, int S, hipStream_t stream);
+int l3u_pw_bwd_tail_pair_bf16(const float* dout, long long dout_nstride, const float* dscale,
+                              const float* dpool, long long dpool_nstride, const unsigned char* idx,
+                              int Hf, int Wf, const l3u_bf16* out, long long out_nstride,
+                              const double* tail_part, int npart, const l3u_bf16* yra,
+                              long long yra_nstride, const float* reca, const l3u_bf16* xa,
+                              long long xa_nstride, const float* wa, float* dxa,
+                              long long dxa_nstride, int acc_a, float* part_a, int Ka, int sel_a,
+                              const l3u_bf16* yrb, long long yrb_nstride, const float* recb,
+                              const l3u_bf16* xb, long long xb_nstride, const float* wb, float* dxb,
+                              long long dxb_nstride, int acc_b, float* part_b, int Kb, int sel_b,
+                              int N, int J, int S, hipStream_t stream);
 int l3u_pw_bwd_bf16(const float* dy, long long dy_nstride, const l3u_bf16* y, long long y_nstride,
                     const float* rec, const double* in_part, int npart, const l3u_bf16* x,
                     long long x_nstride, const float* w, float* dx, long long dx_nstride,

@@ -576,6 +576,15 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 // (row lr, voxels 16g + 4lk..+3) is read back transposed, conflict-free.  X is only needed by
 // the weight gradient and is loaded in its B layout.  The weights sit in LDS as W[j][k] with a
 // row stride = 16 mod 64 floats (conflict-free A-operand reads for the data gradient).
+// the second problem of a paired block-tail launch (l3u_pw_bwd_tail_pair, PRO 2): the same
+// block tail (dout, out, tail partials) for the other pointwise backward of the block
+// (conv2.pointwise, sel 1, or the shortcut, sel 2); blockIdx.z == 1
+template <typename T>
+struct TailSecond {
+  const T* yr; long long yrns; const float* rec; const T* x; long long xns; const float* w;
+  float* dx; long long dxns; int accumulate; float* part; int K; int sel;
+};
+
 template <typename T, int NJ, int NK, int PRO, bool R1 = false>
 __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
@@ -584,9 +593,15 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     float* __restrict__ dx, long long dxns, int accumulate, float* __restrict__ part, int N, int J,
     int K, int S, int SCH, int nsc, const T* __restrict__ oin = nullptr, long long oins = 0,
     int sel = 1, const float* __restrict__ dscale = nullptr, const float* __restrict__ dpool = nullptr,
-    long long dpns = 0, const unsigned char* __restrict__ pidx = nullptr, int Hf = 0, int Wf = 0) {
+    long long dpns = 0, const unsigned char* __restrict__ pidx = nullptr, int Hf = 0, int Wf = 0,
+    TailSecond<T> p2 = TailSecond<T>{}) {
   L3U_STAMP_SCOPE(104);
   constexpr int TJ = 16 * NJ, TK = 16 * NK, JR = TJ / 4;
+  if (PRO == 2 && blockIdx.z == 1) {   // paired tail launch, second problem
+    yin = p2.yr; yns = p2.yrns; rec = p2.rec; x = p2.x; xns = p2.xns; w = p2.w; dx = p2.dx;
+    dxns = p2.dxns; accumulate = p2.accumulate; part = p2.part; K = p2.K; sel = p2.sel;
+  }
+  if ((int)blockIdx.y * TK >= K) return;   // the narrower problem's unused column blocks
   constexpr int WS = TK + ((16 - TK) % 64 + 64) % 64;   // >= TK, = 16 mod 64
   constexpr int DS = 68;                                // dY tile row stride (floats)
   constexpr int PS = 8;                                 // lanes per channel for the IN sums
@@ -1480,6 +1495,48 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   L3U_CHECK_LAUNCH();
 }
 
+// the block tail's two pointwise backwards (conv2.pointwise, sel 1, and the shortcut, sel 2) in one
+// launch, grid.z selecting the problem; same dout forms as l3u_pw_bwd_tail[_r1 / _up]
+template <typename T>
+int pw_bwd_tail_pair_impl(const float* dout, long long dout_nstride, const float* dscale,
+                          const float* dpool, long long dpns, const unsigned char* pidx, int Hf,
+                          int Wf, const T* out, long long out_nstride, const double* tail_part,
+                          int npart, const TailSecond<T>& a, const TailSecond<T>& b, int N, int J,
+                          int S, hipStream_t stream) {
+  L3U_REQUIRE(N > 0 && a.K > 0 && b.K > 0 && l3u_pw_bwd_supported(J, a.K, S) &&
+              l3u_pw_bwd_supported(J, b.K, S) && !pw_bwd_wide(J));
+  L3U_REQUIRE(dpool == nullptr || (pidx && Hf % 2 == 0 && Wf % 4 == 0 && (S / (Hf * Wf)) % 2 == 0 &&
+                                   dpns % 2 == 0 && ((uintptr_t)dpool & 7) == 0));
+  L3U_REQUIRE(dout && out && tail_part && npart > 0);
+  for (const TailSecond<T>* p : {&a, &b}) {
+    L3U_REQUIRE(p->yr && p->rec && p->x && p->w && p->dx && p->part && (p->sel == 1 || p->sel == 2));
+    L3U_REQUIRE(p->yrns >= 0 && al4<T>(p->yr) && al4<T>(p->x) && al4<float>(p->dx) && p->yrns % 4 == 0 &&
+                p->xns % 4 == 0 && p->dxns % 4 == 0);
+  }
+  L3U_REQUIRE(al4<float>(dout) && al4<T>(out) && dout_nstride % 4 == 0 && out_nstride % 4 == 0);
+  const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
+  const int NJ = J <= 16 ? 1 : 2, K = a.K > b.K ? a.K : b.K;
+  int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
+  if (NK > L3U_PWBF_NK_MAX) NK = L3U_PWBF_NK_MAX;
+  while (NK > 1 && 2ll * N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < L3U_PWBF_MIN_BLOCKS) NK >>= 1;
+  const int nwv = SCH / 64;
+  L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
+  dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK), 2), block(64 * nwv);
+  const size_t dlds = (size_t)nwv * 16 * NJ * 68 * sizeof(float);   // dY tiles (DS = 68)
+#define PWTP(A_, B_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2>), grid, block, dlds, stream, \
+      dout, dout_nstride, a.yr, a.yrns, a.rec, tail_part, npart, a.x, a.xns, a.w, a.dx, a.dxns, \
+      a.accumulate, a.part, N, J, a.K, S, SCH, nsc, out, out_nstride, a.sel, dscale, dpool, dpns, pidx, \
+      Hf, Wf, b)
+  if (NJ == 1 && NK == 1) PWTP(1, 1);
+  else if (NJ == 1 && NK == 2) PWTP(1, 2);
+  else if (NJ == 1 && NK == 4) PWTP(1, 4);
+  else if (NJ == 2 && NK == 1) PWTP(2, 1);
+  else if (NJ == 2 && NK == 2) PWTP(2, 2);
+  else PWTP(2, 4);
+#undef PWTP
+  L3U_CHECK_LAUNCH();
+}
+
 template <typename T>
 int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_nstride,
                 const float* rec, const double* in_part, int npart, const T* x,
@@ -1777,6 +1834,23 @@ L3U_TWIN(l3u_pw_bwd_tail_up, P_PBTU, dpool == nullptr ? (int)hipErrorInvalidValu
 L3U_TWIN(l3u_pw_bwd_tail_r1, P_PBT1, dscale == nullptr ? (int)hipErrorInvalidValue :
          pw_bwd_tail_impl(dz, dz_nstride, bp(out), out_nstride, bp(yr), yr_nstride, rec, tail_part,
          npart, sel, bp(x), x_nstride, w, dx, dx_nstride, accumulate, part, N, J, K, S, stream, dscale))
+// the block tail's conv2.pointwise (sel 1) and shortcut (sel 2) backwards in one launch; dscale /
+// dpool (+ idx, Hf, Wf) as l3u_pw_bwd_tail_r1 / _up, or NULL
+#define P_PBTP(TT) (const float* dout, long long dout_nstride, const float* dscale,                   \
+    const float* dpool, long long dpool_nstride, const unsigned char* idx, int Hf, int Wf,          \
+    const TT* out, long long out_nstride, const double* tail_part, int npart, const TT* yra,         \
+    long long yra_nstride, const float* reca, const TT* xa, long long xa_nstride, const float* wa,   \
+    float* dxa, long long dxa_nstride, int acc_a, float* part_a, int Ka, int sel_a, const TT* yrb,   \
+    long long yrb_nstride, const float* recb, const TT* xb, long long xb_nstride, const float* wb,   \
+    float* dxb, long long dxb_nstride, int acc_b, float* part_b, int Kb, int sel_b, int N, int J,    \
+    int S, hipStream_t stream)
+L3U_TWIN(l3u_pw_bwd_tail_pair, P_PBTP, pw_bwd_tail_pair_impl(dout, dout_nstride, dscale, dpool,
+         dpool_nstride, idx, Hf, Wf, bp(out), out_nstride, tail_part, npart,
+         TailSecond<std::remove_const_t<std::remove_pointer_t<decltype(bp(out))>>>{bp(yra), yra_nstride,
+             reca, bp(xa), xa_nstride, wa, dxa, dxa_nstride, acc_a, part_a, Ka, sel_a},
+         TailSecond<std::remove_const_t<std::remove_pointer_t<decltype(bp(out))>>>{bp(yrb), yrb_nstride,
+             recb, bp(xb), xb_nstride, wb, dxb, dxb_nstride, acc_b, part_b, Kb, sel_b},
+         N, J, S, stream))
 #define P_PBD(TT) (const float* dy, long long dy_nstride, const TT* y, long long y_nstride,         \
     const float* rec, const double* in_part, int npart, const TT* x, long long x_nstride,           \
     const float* w, float* dx, long long dx_nstride, int accumulate, float* part, int N, int J,     \

@@ -33,6 +33,8 @@ _SIGS = {
     "l3u_pw_bwd_nparts": [I, I, I, I],
     "l3u_pw_bwd": [P, L, P, L, P, P, I, P, L, P, P, L, I, P, I, I, I, I, P],
     "l3u_pw_bwd2_supported": [I, I],
+    "l3u_pw_bwd_tail_pair": [P, L, P, P, L, P, I, I, P, L, P, I, P, L, P, P, L, P, P, L, I, P, I, I,
+                             P, L, P, P, L, P, P, L, I, P, I, I, I, I, I, P],
     "l3u_pw_bwd2": [P, L, P, L, P, P, L, I, P, I, P, L, P, L, P, P, L, I, P, I, I, I, I, P],
     "l3u_in_finalize": [P, I, P, P, F, U64, P, I, P, I, I, P],
     "l3u_norm_act_nblocks": [I],
@@ -94,7 +96,7 @@ _SIGS = {
 # entry points with a _bf16 twin (same arguments; saved activations stored as bf16, gradients
 # fp32, include/l3u.h)
 BF16_TWINS = ("l3u_dw3_fwd", "l3u_dw3_bwd", "l3u_pw_fwd", "l3u_pw_fwd2", "l3u_pw_bwd_weight",
-              "l3u_pw_bwd", "l3u_pw_bwd2", "l3u_pw_bwd_tail", "l3u_convt_fwd", "l3u_convt_bwd",
+              "l3u_pw_bwd", "l3u_pw_bwd2", "l3u_pw_bwd_tail", "l3u_pw_bwd_tail_pair", "l3u_convt_fwd", "l3u_convt_bwd",
               "l3u_convt_bwd_fused", "l3u_norm_act_fwd", "l3u_norm_act_pool_fwd",
               "l3u_norm_act_bwd_reduce", "l3u_norm_act_bwd_apply", "l3u_norm_act_bwd",
               "l3u_in_bwd_apply", "l3u_maxpool2_fwd", "l3u_outconv_fwd", "l3u_outconv_bwd",

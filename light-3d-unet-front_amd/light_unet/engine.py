@@ -38,6 +38,8 @@ _DWPW = os.environ.get("L3U_DWPW", "1") != "0"
 # a block's conv2.pointwise and shortcut backwards as one launch at the 12^3 / 6^3 levels
 # (l3u_pw_bwd2); L3U_PAIR_BWD=0 keeps them separate
 _PAIR_BWD = os.environ.get("L3U_PAIR_BWD", "1") != "0"
+# ... and the fused block tail's two pointwise backwards (l3u_pw_bwd_tail_pair) up to this volume
+_PAIR_TAIL_MAX_S = int(os.environ.get("L3U_PAIR_TAIL_MAX_S", str(1 << 30)))
 _DWPW_MIN_S = int(os.environ.get("L3U_DWPW_MIN_S", "65536"))
 # the out_conv backward hands the last block d(pre-sigmoid) and w (out_conv is rank-1) instead
 # of the [N, C, S] output gradient (l3u_outconv_bwd_dz + the _r1 tail kernels); L3U_RANK1=0
@@ -921,9 +923,17 @@ class UNetEngine:
             # (1+2) the tail reduce, then conv2.pointwise backward with the tail's apply in its
             # prologue (dy2 is never written)
             pn, ntp = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev, fused=True)
-            self._pw_bwd_tail(flat, dout, sv["out"], V(y2, 0, cout * S, cout), rec2, pn, ntp, 1,
-                              V(z2, 0, cout * S, cout), pre + "conv2.pointwise.weight",
-                              V(dz2, 0, cout * S, cout), 0, N, S, st)
+            if _PAIR_BWD and shortcut and sv["r"].scale is None and S <= _PAIR_TAIL_MAX_S:
+                # ... with the shortcut backward in the same launch (it writes d(input) first)
+                self._pw_bwd_tail_pair(flat, dout, sv["out"], pn, ntp,
+                                       (V(y2, 0, cout * S, cout), rec2, V(z2, 0, cout * S, cout),
+                                        pre + "conv2.pointwise.weight", V(dz2, 0, cout * S, cout), 1),
+                                       (sv["r"], rec_r, x, pre + "shortcut.0.weight", dxv, 2), N, S, st)
+                sc_done = True
+            else:
+                self._pw_bwd_tail(flat, dout, sv["out"], V(y2, 0, cout * S, cout), rec2, pn, ntp, 1,
+                                  V(z2, 0, cout * S, cout), pre + "conv2.pointwise.weight",
+                                  V(dz2, 0, cout * S, cout), 0, N, S, st)
         else:
             dy2, drv = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev)
             # (2) conv2.pointwise backward; at the 12^3 / 6^3 levels paired in one launch with the
@@ -1024,6 +1034,29 @@ class UNetEngine:
                    dxb.ns, 0, A.ptr(parts[1][0]), xb.C, N, J, S, st)
         for off, npw, K, name in parts:
             self._seg(off, npw, J * K, 1, J * K, name)
+
+    def _pw_bwd_tail_pair(self, flat, dout, out, pn, ntp, a, b, N, S, st):
+        """The two _pw_bwd_tail calls of a block (a, b = (yr, rec, x, weight name, dx, sel)) in one
+        launch (l3u_pw_bwd_tail_pair); both dx are overwritten."""
+        J = out.C
+        A = self.bwd_arena
+        args, segs = [], []
+        for yr, rec, x, name, dx, sel in (a, b):
+            npw = nat.query("l3u_pw_bwd_nparts", N, J, x.C, S)
+            off = A.alloc(npw * J * x.C)
+            segs.append((off, npw, J * x.C, name))
+            args += [yr.p, yr.sns, rec, x.p, x.ns, self._w(flat, name), dx.p, dx.ns, 0, A.ptr(off), x.C,
+                     sel]
+        dscale = dout.scale
+        if dout.pool is not None:
+            dpool, idx, (d, h, w) = dout.pool
+            pool = [dpool.data_ptr(), J * (S // 8), idx.data_ptr(), h, w]
+        else:
+            pool = [None, 0, None, 0, 0]
+        self._call("l3u_pw_bwd_tail_pair", dout.p, dout.ns, dscale, *pool, out.p, out.ns, A.ptr(pn),
+                   ntp, *args, N, J, S, st)
+        for off, npw, n, name in segs:
+            self._seg(off, npw, n, 1, n, name)
 
     def _pw_bwd_tail(self, flat, dout, out, yr, rec, pn, ntp, sel, x, name, dx, accumulate, N, S,
                      st):

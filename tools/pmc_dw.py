@@ -14,12 +14,13 @@ S = L ** 3
 dev = torch.device("cuda:0")
 x = torch.rand(N, C, S, device=dev)
 dz = torch.rand(N, C, S, device=dev)
-dx = torch.empty_like(x)
+dx = torch.zeros_like(x)
+ACC = 1   # the step's call adds to the shortcut's d(input) (l3u_pw_bwd_tail_pair runs first)
 w = torch.rand(C, 27, device=dev)
 nch = nat.query("l3u_dw3_nchunk", N, C, L, L, L)
 dwp = torch.empty(C * N * nch * 27, device=dev)
 for _ in range(10):
     nat.call("l3u_dw3_bwd", dz.data_ptr(), C * S, x.data_ptr(), C * S, w.data_ptr(), None,
-             dx.data_ptr(), C * S, 0, dwp.data_ptr(), None, N, C, L, L, L, nat.stream())
+             dx.data_ptr(), C * S, ACC, dwp.data_ptr(), None, N, C, L, L, L, nat.stream())
 torch.cuda.synchronize()
 print("done", flush=True)

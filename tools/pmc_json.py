@@ -32,13 +32,13 @@ def main():
     write = per_kernel(d, "WRITE_SIZE")
     ks = {k: {"fetch_bytes": int(2 * fetch.get(k, 0)), "write_bytes": int(write.get(k, 0))}
           for k in sorted(set(fetch) | set(write))}
-    rec = {"call": "l3u_dw3_bwd [4,32,48^3] (accumulate=0, no IN record): 10 calls, calls 3-10 averaged",
+    rec = {"call": "l3u_dw3_bwd [4,32,48^3] (accumulate=1, no IN record): 10 calls, calls 3-10 averaged",
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes with "
                      "--kernel-trace only (tools/pmc.sh); FETCH_SIZE doubled per MI355X_MICROARCH.md "
                      "(gfx950 reports half the bytes of 16-B/lane streaming reads); values in bytes per call",
            "kernels": ks,
            "traffic_bytes": sum(v["fetch_bytes"] + v["write_bytes"] for v in ks.values()),
-           "algorithmic_bytes": 4 * 3 * 4 * 32 * 48 ** 3 + 4 * 27 * 32}
+           "algorithmic_bytes": 4 * 4 * 4 * 32 * 48 ** 3 + 4 * 27 * 32}
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
