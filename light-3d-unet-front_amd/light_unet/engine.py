@@ -39,7 +39,10 @@ _DWPW = os.environ.get("L3U_DWPW", "1") != "0"
 # (l3u_pw_bwd2); L3U_PAIR_BWD=0 keeps them separate
 _PAIR_BWD = os.environ.get("L3U_PAIR_BWD", "1") != "0"
 # ... and the fused block tail's two pointwise backwards (l3u_pw_bwd_tail_pair) up to this volume
-_PAIR_TAIL_MAX_S = int(os.environ.get("L3U_PAIR_TAIL_MAX_S", str(1 << 30)))
+# (48^3: -35 us/step at config 2; at config 5's 64^3 the pair and the accumulating depthwise
+# backward cost +100 us, tools/run_evidence.sh step lists) and K ratio (the pair shares one
+# column-block width)
+_PAIR_TAIL_MAX_S = int(os.environ.get("L3U_PAIR_TAIL_MAX_S", str(48 ** 3)))
 _DWPW_MIN_S = int(os.environ.get("L3U_DWPW_MIN_S", "65536"))
 # the out_conv backward hands the last block d(pre-sigmoid) and w (out_conv is rank-1) instead
 # of the [N, C, S] output gradient (l3u_outconv_bwd_dz + the _r1 tail kernels); L3U_RANK1=0
@@ -923,7 +926,8 @@ class UNetEngine:
             # (1+2) the tail reduce, then conv2.pointwise backward with the tail's apply in its
             # prologue (dy2 is never written)
             pn, ntp = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev, fused=True)
-            if _PAIR_BWD and shortcut and sv["r"].scale is None and S <= _PAIR_TAIL_MAX_S:
+            if (_PAIR_BWD and shortcut and sv["r"].scale is None and S <= _PAIR_TAIL_MAX_S
+                    and max(cin, cout) <= 2 * min(cin, cout)):
                 # ... with the shortcut backward in the same launch (it writes d(input) first)
                 self._pw_bwd_tail_pair(flat, dout, sv["out"], pn, ntp,
                                        (V(y2, 0, cout * S, cout), rec2, V(z2, 0, cout * S, cout),
