@@ -253,6 +253,21 @@ def call_bytes(name, a):
         jr = 1 if a[8] < 0 else J
         return ("gemm", f"pw_bwd_tail{a[12]} (+maxpool bwd) {J}->{K}{' (rank-1 r)' if a[8] < 0 else ''} [{N},{S}]",
                 N * S * (4 * J + 4 * J / 8 + J / 8 + e * (J + jr) + e * K + 4 * K * (1 + a[18])))
+    if base == "l3u_pw_bwd2":     # two plain pw_bwd problems: (dy, dyns, x, xns, w, dx, dxns, acc, part, K) x 2, N, J, S
+        N, J, S = a[20:23]
+        Ka, Kb = a[9], a[19]
+        return ("gemm", f"pw_bwd2 {J}->{Ka} + {J}->{Kb} [{N},{S}]",
+                N * S * sum(4 * J + e * K + 4 * K * (1 + acc) for K, acc in ((Ka, a[7]), (Kb, a[17]))))
+    if base == "l3u_pw_bwd_tail_pair":  # (dout, dns, dscale, dpool, dpns, idx, Hf, Wf, out, ons, pn, ntp, (yr, yns, rec, x, xns, w, dx, dxns, acc, part, K, sel) x 2, N, J, S)
+        N, J, S = a[36:39]
+        dj = 1 if a[2] is not None else J                      # rank-1 dout
+        pool = (4 * J / 8 + J / 8) if a[3] is not None else 0  # unpooled dpool + argmax bytes
+        form = " (rank-1 dout)" if a[2] is not None else (" (+maxpool bwd)" if a[3] is not None else "")
+        tot = 0
+        for o in (12, 24):   # each problem reads the tail operands (dout, out) itself
+            K, acc = a[o + 10], a[o + 8]
+            tot += N * S * (4 * dj + pool + e * 2 * J + e * K + 4 * K * (1 + acc))
+        return ("gemm", f"pw_bwd_tail pair{form} {J}->{a[22]} + {J}->{a[34]} [{N},{S}]", tot)
     if base == "l3u_pw_bwd_weight":  # (dy, dyns, x, xns, part, N, J, K, S)
         N, J, K, S = a[5:9]
         return "gemm", f"pw_bwd_weight {J}x{K} [{N},{S}]", N * S * (4 * J + e * K)
