@@ -54,3 +54,27 @@ def test_bench_self_launches_two_ranks(cuda):
     assert out["config"]["parallelism"] == "dp2"
     assert out["config"]["global_batch"] == 8
     assert out["value"] > 0 and out["final_loss"] == out["final_loss"]
+
+
+def test_paired_call_bytes_are_the_two_calls():
+    """CPU: the in-step byte model of a paired GEMM backward launch (l3u_pw_bwd2,
+    l3u_pw_bwd_tail_pair) is the sum of the two calls it replaces, so pairing does not move the
+    GEMM family's algorithmic bytes."""
+    sys.path.insert(0, ROOT)
+    import bench
+    N, J, S, Ka, Kb = 4, 64, 1728, 64, 32
+    p = 1   # any non-null pointer
+    one = lambda K, acc: bench.call_bytes(  # noqa: E731
+        "l3u_pw_bwd", (p, J * S, None, 0, None, None, 0, p, K * S, p, p, K * S, acc, p, N, J, K, S, p))[2]
+    pair = bench.call_bytes("l3u_pw_bwd2", (p, J * S, p, Ka * S, p, p, Ka * S, 0, p, Ka,
+                                            p, J * S, p, Kb * S, p, p, Kb * S, 0, p, Kb, N, J, S, p))
+    assert pair[0] == "gemm" and pair[2] == one(Ka, 0) + one(Kb, 0)
+    J, S, Ka, Kb = 16, 110592, 16, 32
+    tail = lambda yr, sel, K, acc: bench.call_bytes(  # noqa: E731
+        "l3u_pw_bwd_tail", (p, J * S, p, J * S, yr, J * S, p, p, 4, sel, p, K * S, p, p, K * S, acc, p,
+                            N, J, K, S, p))[2]
+    args = (p, J * S, None, None, 0, None, 0, 0, p, J * S, p, 4,
+            p, J * S, p, p, Ka * S, p, p, Ka * S, 0, p, Ka, 1,
+            p, J * S, p, p, Kb * S, p, p, Kb * S, 0, p, Kb, 2, N, J, S, p)
+    tp = bench.call_bytes("l3u_pw_bwd_tail_pair", args)
+    assert tp[0] == "gemm" and tp[2] == tail(p, 1, Ka, 0) + tail(p, 2, Kb, 0)
