@@ -1284,7 +1284,10 @@ int pw_nsw(int NC) { const int n = 4 / NC; return n < L3U_PW_NSW_MAX ? n : L3U_P
 #define L3U_PWKS8_MAX_WG 1024  // grids up to this many workgroups take all k-steps in flight
 #endif
 // K split across the 4 waves (pw_fwd_ks_kernel) for small volumes with a deep enough reduction
-bool pw_use_ks(int S, int K) { return S < 32768 && K >= L3U_PW_KS_MIN_K; }
+#ifndef L3U_PW_KS_MAX_S
+#define L3U_PW_KS_MAX_S 32768
+#endif
+bool pw_use_ks(int S, int K) { return S < L3U_PW_KS_MAX_S && K >= L3U_PW_KS_MIN_K; }
 
 }  // namespace
 
