@@ -182,8 +182,9 @@ int l3u_pw_bwd(const float* dy, long long dy_nstride, const float* y, long long 
 /* the block tail's two pointwise backwards (conv2.pointwise: sel 1, yr = y2; the Conv1x1
  * shortcut: sel 2, yr = r) of l3u_pw_bwd_tail in ONE launch, dout as l3u_pw_bwd_tail (dscale and
  * dpool NULL), l3u_pw_bwd_tail_r1 (dscale) or l3u_pw_bwd_tail_up (dpool, idx and the plane Hf x Wf);
- * no rank-1 yr; each problem's partials as l3u_pw_bwd_nparts(N, J, K, S), results bit-identical to
- * the two calls.                                                                                */
+ * a rank-1 yr (negative yrb_nstride, fp32) only for the second problem and only when J, Ka, Kb
+ * <= 16; each problem's partials as l3u_pw_bwd_nparts(N, J, K, S), results bit-identical to the
+ * two calls.                                                                                    */
 int l3u_pw_bwd_tail_pair(const float* dout, long long dout_nstride, const float* dscale,
                          const float* dpool, long long dpool_nstride, const unsigned char* idx,
                          int Hf, int Wf, const float* out, long long out_nstride,

@@ -585,7 +585,7 @@ struct TailSecond {
   float* dx; long long dxns; int accumulate; float* part; int K; int sel;
 };
 
-template <typename T, int NJ, int NK, int PRO, bool R1 = false>
+template <typename T, int NJ, int NK, int PRO, bool R1 = false, bool R1B = false>
 __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
@@ -650,8 +650,9 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     }
   }
   // R1 (yns < 0): a rank-1 normalised operand, channel j = rec[j][7] * one stored channel
-  // (include/l3u.h); a template flag so that the other variants keep their registers
-  constexpr bool yk = PRO && R1;
+  // (include/l3u.h); a template flag so that the other variants keep their registers.  R1B: only
+  // the paired launch's second problem (the first block's shortcut) has the rank-1 operand
+  const bool yk = R1B ? (PRO == 2 && blockIdx.z == 1) : (PRO && R1);
   if (PRO) {
     const T* yn = yin + (long long)n * (yk ? -yns : yns);
 #pragma unroll
@@ -1513,7 +1514,7 @@ int pw_bwd_tail_pair_impl(const float* dout, long long dout_nstride, const float
   L3U_REQUIRE(dout && out && tail_part && npart > 0);
   for (const TailSecond<T>* p : {&a, &b}) {
     L3U_REQUIRE(p->yr && p->rec && p->x && p->w && p->dx && p->part && (p->sel == 1 || p->sel == 2));
-    L3U_REQUIRE(p->yrns >= 0 && al4<T>(p->yr) && al4<T>(p->x) && al4<float>(p->dx) && p->yrns % 4 == 0 &&
+    L3U_REQUIRE((p->yrns >= 0 || (p == &b && sizeof(T) == 4)) && al4<T>(p->yr) && al4<T>(p->x) && al4<float>(p->dx) && p->yrns % 4 == 0 &&
                 p->xns % 4 == 0 && p->dxns % 4 == 0);
   }
   L3U_REQUIRE(al4<float>(dout) && al4<T>(out) && dout_nstride % 4 == 0 && out_nstride % 4 == 0);
@@ -1526,17 +1527,22 @@ int pw_bwd_tail_pair_impl(const float* dout, long long dout_nstride, const float
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK), 2), block(64 * nwv);
   const size_t dlds = (size_t)nwv * 16 * NJ * 68 * sizeof(float);   // dY tiles (DS = 68)
-#define PWTP(A_, B_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2>), grid, block, dlds, stream, \
+#define PWTP0(A_, B_, R_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2, false, R_>), grid, block, dlds, stream, \
       dout, dout_nstride, a.yr, a.yrns, a.rec, tail_part, npart, a.x, a.xns, a.w, a.dx, a.dxns, \
       a.accumulate, a.part, N, J, a.K, S, SCH, nsc, out, out_nstride, a.sel, dscale, dpool, dpns, pidx, \
       Hf, Wf, b)
-  if (NJ == 1 && NK == 1) PWTP(1, 1);
+#define PWTP(A_, B_) PWTP0(A_, B_, false)
+  // a rank-1 second operand (the first block's shortcut, K = 1, beside conv2's K = J <= 16)
+  L3U_REQUIRE(b.yrns >= 0 || (NJ == 1 && NK == 1));
+  if (b.yrns < 0) { if constexpr (sizeof(T) == 4) PWTP0(1, 1, true); }
+  else if (NJ == 1 && NK == 1) PWTP(1, 1);
   else if (NJ == 1 && NK == 2) PWTP(1, 2);
   else if (NJ == 1 && NK == 4) PWTP(1, 4);
   else if (NJ == 2 && NK == 1) PWTP(2, 1);
   else if (NJ == 2 && NK == 2) PWTP(2, 2);
   else PWTP(2, 4);
 #undef PWTP
+#undef PWTP0
   L3U_CHECK_LAUNCH();
 }
 

@@ -43,6 +43,8 @@ _PAIR_BWD = os.environ.get("L3U_PAIR_BWD", "1") != "0"
 # backward cost +100 us, tools/run_evidence.sh step lists) and K ratio (the pair shares one
 # column-block width)
 _PAIR_TAIL_MAX_S = int(os.environ.get("L3U_PAIR_TAIL_MAX_S", str(48 ** 3)))
+# ... and for single-column-block blocks of any channel ratio (the first block's 1 -> 16)
+_PAIR_TAIL_NARROW = os.environ.get("L3U_PAIR_TAIL_NARROW", "1") != "0"
 _DWPW_MIN_S = int(os.environ.get("L3U_DWPW_MIN_S", "65536"))
 # the out_conv backward hands the last block d(pre-sigmoid) and w (out_conv is rank-1) instead
 # of the [N, C, S] output gradient (l3u_outconv_bwd_dz + the _r1 tail kernels); L3U_RANK1=0
@@ -926,9 +928,13 @@ class UNetEngine:
             # (1+2) the tail reduce, then conv2.pointwise backward with the tail's apply in its
             # prologue (dy2 is never written)
             pn, ntp = self._tail_bwd(pre, sv, dout, dxv, N, cout, S, st, dev, fused=True)
-            if (_PAIR_BWD and shortcut and sv["r"].scale is None and S <= _PAIR_TAIL_MAX_S
-                    and max(cin, cout) <= 2 * min(cin, cout)):
-                # ... with the shortcut backward in the same launch (it writes d(input) first)
+            if (_PAIR_BWD and shortcut and S <= _PAIR_TAIL_MAX_S
+                    and (max(cin, cout) <= 2 * min(cin, cout)
+                         or (_PAIR_TAIL_NARROW and max(cin, cout) <= 16))
+                    and (sv["r"].scale is None or (_PAIR_TAIL_NARROW and max(cin, cout) <= 16))):
+                # ... with the shortcut backward in the same launch (it writes d(input) first);
+                # the column-block counts of the two may differ by 2x at most, a rank-1 shortcut
+                # operand (the first block's) only beside a single column block
                 self._pw_bwd_tail_pair(flat, dout, sv["out"], pn, ntp,
                                        (V(y2, 0, cout * S, cout), rec2, V(z2, 0, cout * S, cout),
                                         pre + "conv2.pointwise.weight", V(dz2, 0, cout * S, cout), 1),
