@@ -471,6 +471,14 @@ int l3u_adamw_tick(float* p, const float* g, float* m, float* v, long long numel
  * f64 != 0: the source is fp64 and offsets/strides count doubles from the same base.         */
 int l3u_reduce_segments(const float* src, const long long* items, int nitems, float* dst,
                         hipStream_t stream);
+/* the same reduction fused with the AdamW update (l3u_adamw_tick's arithmetic and step /
+ * counter2 / ticket protocol) of the parameters it produces, for one process (no gradient
+ * exchange between the two): requires that every one of the numel parameters is the output of
+ * exactly one item and that no item accumulates; g receives the reduced gradient as well      */
+int l3u_reduce_segments_adamw(const float* src, const long long* items, int nitems, float* g,
+                              float* p, float* m, float* v, const float* lr, float beta1,
+                              float beta2, float eps, float weight_decay, int* step,
+                              float grad_scale, int* ticket, int* counter2, hipStream_t stream);
 
 /* ---- whole-volume sliding-window inference (light_unet/utils.py:11-173) --------------------
  * gather: out[b] = volume[z:z+pd, y:y+ph, x:x+pw] of window b (pos[b] = {z, y, x}), zero past

@@ -350,6 +350,29 @@ __global__ __launch_bounds__(256) void ftl_bwd_kernel(
 }
 
 // ---------------------------------------------------------------- AdamW (torch.optim.AdamW)
+// The per-element update, shared by adamw_tick and the fused reduce + update below so that both
+// round identically.
+struct AdamWStep { float step_size, decay, bc2s, beta1, beta2, eps, gscale; };
+__device__ __forceinline__ AdamWStep adamw_step(float lrv, float beta1, float beta2, float eps,
+                                                float wd, int t, float gscale) {
+  AdamWStep c;
+  const float bc1 = 1.f - powf(beta1, (float)t);
+  c.bc2s = sqrtf(1.f - powf(beta2, (float)t));
+  c.step_size = lrv / bc1;
+  c.decay = 1.f - lrv * wd;
+  c.beta1 = beta1; c.beta2 = beta2; c.eps = eps; c.gscale = gscale;
+  return c;
+}
+__device__ __forceinline__ void adamw_update(const AdamWStep& c, float& pv, float gv, float& mv,
+                                             float& vv) {
+  gv *= c.gscale;
+  pv *= c.decay;
+  mv = mv + (1.f - c.beta1) * (gv - mv);                 // exp_avg.lerp_(grad, 1 - beta1)
+  vv = vv * c.beta2 + (1.f - c.beta2) * gv * gv;
+  const float denom = sqrtf(vv) / c.bc2s + c.eps;
+  pv = pv - c.step_size * (mv / denom);
+}
+
 // One launch: the update, and the step counter(s) advanced by the LAST workgroup to finish (ticket
 // order): every workgroup has read *step by the time it takes its ticket, so the increment
 // cannot race a read, and the separate one-thread launch disappears.  The ticket is reset.
@@ -361,20 +384,9 @@ __global__ __launch_bounds__(256) void adamw_tick_kernel(float* __restrict__ p, 
                                                          int* step, float gscale, int* ticket,
                                                          int* counter2) {
   L3U_STAMP_SCOPE(409);
-  const float lrv = lr[0];
   const int t = step[0] + 1;
-  const float bc1 = 1.f - powf(beta1, (float)t);
-  const float bc2s = sqrtf(1.f - powf(beta2, (float)t));
-  const float step_size = lrv / bc1;
-  const float decay = 1.f - lrv * wd;
-  auto upd = [&](float& pv, float gv, float& mv, float& vv) {
-    gv *= gscale;
-    pv *= decay;
-    mv = mv + (1.f - beta1) * (gv - mv);                 // exp_avg.lerp_(grad, 1 - beta1)
-    vv = vv * beta2 + (1.f - beta2) * gv * gv;
-    const float denom = sqrtf(vv) / bc2s + eps;
-    pv = pv - step_size * (mv / denom);
-  };
+  const AdamWStep c = adamw_step(lr[0], beta1, beta2, eps, wd, t, gscale);
+  auto upd = [&](float& pv, float gv, float& mv, float& vv) { adamw_update(c, pv, gv, mv, vv); };
   const long long st = (long long)gridDim.x * 256;
   if (VEC) {
     // float4 per thread: the four arrays' loads of a thread are one memory round trip (the scalar
@@ -422,12 +434,9 @@ __global__ void counter_add_kernel(int* c, int v) { c[0] += v; }
 #endif
 // item (8 x int64): src_off, count, istride, tstride, len, dst_off, accumulate, unused
 // dst[dst_off + t] (+)= sum_{i<count} src[src_off + i*istride + t*tstride], t < len (<= 256)
-__global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __restrict__ src,
-                                                              const long long* __restrict__ items,
-                                                              float* __restrict__ dst) {
-  L3U_STAMP_SCOPE(410);
-  __shared__ double red[256];
-  const long long* it = items + (long long)blockIdx.x * 8;
+// Returns, for thread t < len, the segment's sum for output t (red: 256 doubles of LDS).
+__device__ __forceinline__ double segment_sum(const float* __restrict__ src,
+                                              const long long* __restrict__ it, double* red) {
   const int t = threadIdx.x;
   const int len = (int)it[4];
   // TP threads per output: thread (k, o) sums terms i = k, k+TP, k+2TP, ... of output o
@@ -466,11 +475,57 @@ __global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __res
   }
   red[t] = s;
   __syncthreads();
-  if (t < len) {
-    double r = 0.0;
+  double r = 0.0;
+  if (t < len)
     for (int kk = 0; kk < TP; ++kk) r += red[kk * len + t];
+  return r;
+}
+
+__global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __restrict__ src,
+                                                              const long long* __restrict__ items,
+                                                              float* __restrict__ dst) {
+  L3U_STAMP_SCOPE(410);
+  __shared__ double red[256];
+  const long long* it = items + (long long)blockIdx.x * 8;
+  const double r = segment_sum(src, it, red);
+  const int t = threadIdx.x;
+  if (t < (int)it[4]) {
     float* d = dst + it[5] + t;
     *d = it[6] ? (float)((double)*d + r) : (float)r;
+  }
+}
+
+// One process, every parameter written by exactly one non-accumulating item: the segment's
+// reduced gradient goes straight into the AdamW update of its parameters (the gradient is still
+// stored).  The step counter(s) advance as in adamw_tick_kernel (ticket order).  The parameter /
+// moment loads are issued before the reduction so their round trip overlaps it.
+__global__ __launch_bounds__(256) void reduce_segments_adamw_kernel(
+    const float* __restrict__ src, const long long* __restrict__ items, float* __restrict__ g,
+    float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+    const float* __restrict__ lr, float beta1, float beta2, float eps, float wd, int* step,
+    float gscale, int* ticket, int* counter2) {
+  L3U_STAMP_SCOPE(416);
+  __shared__ double red[256];
+  const long long* it = items + (long long)blockIdx.x * 8;
+  const int tc = step[0] + 1;
+  const float lrv = lr[0];
+  const int t = threadIdx.x;
+  const bool mine = t < (int)it[4];
+  const long long j = it[5] + t;
+  float pv = 0.f, mv = 0.f, vv = 0.f;
+  if (mine) { pv = p[j]; mv = m[j]; vv = v[j]; }
+  const double r = segment_sum(src, it, red);
+  if (mine) {
+    const float gv = (float)r;
+    g[j] = gv;
+    adamw_update(adamw_step(lrv, beta1, beta2, eps, wd, tc, gscale), pv, gv, mv, vv);
+    p[j] = pv; m[j] = mv; v[j] = vv;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(ticket, 1) == (int)gridDim.x - 1) {
+    step[0] = tc;
+    if (counter2) counter2[0] += 1;
+    ticket[0] = 0;
   }
 }
 
@@ -881,6 +936,17 @@ int l3u_reduce_segments(const float* src, const long long* items, int nitems, fl
                         hipStream_t stream) {
   L3U_REQUIRE(nitems > 0);
   hipLaunchKernelGGL(reduce_segments_kernel, dim3(nitems), dim3(256), 0, stream, src, items, dst);
+  L3U_CHECK_LAUNCH();
+}
+
+int l3u_reduce_segments_adamw(const float* src, const long long* items, int nitems, float* g,
+                              float* p, float* m, float* v, const float* lr, float beta1,
+                              float beta2, float eps, float weight_decay, int* step,
+                              float grad_scale, int* ticket, int* counter2, hipStream_t stream) {
+  L3U_REQUIRE(nitems > 0 && step && ticket);
+  hipLaunchKernelGGL(reduce_segments_adamw_kernel, dim3(nitems), dim3(256), 0, stream, src, items,
+                     g, p, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale, ticket,
+                     counter2);
   L3U_CHECK_LAUNCH();
 }
 

@@ -61,6 +61,7 @@ _SIGS = {
     "l3u_ftl_loss": [P, D, D, D, D, P, P],
     "l3u_ftl_bwd": [P, P, L, P, D, D, D, D, P, I, P, P],
     "l3u_reduce_segments": [P, P, I, P, P],
+    "l3u_reduce_segments_adamw": [P, P, I, P, P, P, P, P, F, F, F, F, P, F, P, P, P],
     "l3u_pw_fwd2": [P, L, P, P, L, P, P, L, P, P, L, P, I, I, I, I, P],
     "l3u_adamw_tick": [P, P, P, P, L, P, F, F, F, F, P, F, P, P, P],
     "l3u_front_nblocks": [I],

@@ -57,6 +57,21 @@ _POOLFOLD = os.environ.get("L3U_POOLFOLD", "1") != "0"
 # never materialised; their consumers form them on load (include/l3u.h "Rank-1 operands", fp32
 # only); L3U_FRONT_R1=0 writes them as tensors
 _FRONT_R1 = os.environ.get("L3U_FRONT_R1", "1") != "0"
+# one process: the backward's final reduction launch also applies the AdamW update of the
+# parameters it produces (l3u_reduce_segments_adamw: no separate l3u_adamw_tick launch);
+# L3U_FUSE_ADAMW=0 keeps the two launches
+_FUSE_ADAMW = os.environ.get("L3U_FUSE_ADAMW", "1") != "0"
+
+
+def _items_cover_once(items, numel):
+    """True when every one of numel gradient elements is the output of exactly one
+    non-accumulating reduction item (the condition of l3u_reduce_segments_adamw)."""
+    cnt = torch.zeros(numel, dtype=torch.int32)
+    for it in items:
+        if it[6]:
+            return False
+        cnt[it[5]:it[5] + it[4]] += 1
+    return bool((cnt == 1).all())
 
 
 class V:
@@ -204,6 +219,8 @@ class UNetEngine:
         self.stream_id = None   # None: the torch.distributed rank at call time (0 without a group)
         self._arenas = {}
         self._items = {}
+        self._cover_once = {}
+        self.applied_update = False
         self._dry = False
         self._items_rec = None
         self.debug = None      # dict -> backward stashes each block's output-gradient view
@@ -635,9 +652,11 @@ class UNetEngine:
         return sv
 
     # ------------------------------------------------------------------ backward
-    def backward(self, flat, gflat, sv, dp, need_dx=False, ftl=None):
+    def backward(self, flat, gflat, sv, dp, need_dx=False, ftl=None, opt=None):
         """Given dL/dp write all parameter gradients into gflat (overwrite) and return dL/dx if
-        need_dx.  dp = None: the loss is FocalTversky and ftl = (target, global sums [3] fp64,
+        need_dx.  opt: the FlatAdamW over (flat, gflat) of a one-process step; when the gradient
+        reduction covers every parameter once, its launch also applies the update and
+        self.applied_update is True (the caller must then not call opt.step()).  dp = None: the loss is FocalTversky and ftl = (target, global sums [3] fp64,
         (alpha, beta, gamma, smooth)[, loss tensor[, partials, n_partials]]); its gradient is
         formed inside the out_conv backward, which also writes the loss value when a loss tensor
         is given.  sums = None: the out_conv backward reduces the forward's FocalTversky
@@ -660,14 +679,21 @@ class UNetEngine:
                 self._arenas[key] = torch.empty(max(self.bwd_arena.top, 64), dtype=torch.float32,
                                                 device=dev)
                 self._items[key] = torch.tensor(self._items_rec, dtype=torch.int64, device=dev)
+                self._cover_once[key] = _items_cover_once(self._items_rec, gflat.numel())
             self.bwd_arena.reset(self._arenas[key])
             self._items_rec = []
             dx = self._backward_impl(flat, gflat, sv, dp, need_dx, ftl)
         finally:
             self._grad_phase = False
         items = self._items[key]
-        nat.call("l3u_reduce_segments", self.bwd_arena.ptr(0), items.data_ptr(), items.shape[0],
-                 gflat.data_ptr(), nat.stream())
+        self.applied_update = (opt is not None and _FUSE_ADAMW and self._cover_once[key]
+                               and opt.g is gflat and opt.p is flat)
+        if self.applied_update:
+            nat.call("l3u_reduce_segments_adamw", self.bwd_arena.ptr(0), items.data_ptr(),
+                     items.shape[0], *opt.fused_args(), nat.stream())
+        else:
+            nat.call("l3u_reduce_segments", self.bwd_arena.ptr(0), items.data_ptr(),
+                     items.shape[0], gflat.data_ptr(), nat.stream())
         return dx
 
     def _backward_impl(self, flat, gflat, sv, dp, need_dx, ftl=None):

@@ -36,6 +36,14 @@ class FlatAdamW:
     def set_lr(self, lr):
         self.lr_t.fill_(float(lr))
 
+    def fused_args(self):
+        """(g, p, m, v, lr, beta1, beta2, eps, wd, step, grad_scale, ticket, counter2) of
+        l3u_reduce_segments_adamw: the update fused into the gradient reduction launch."""
+        return (self.g.data_ptr(), self.p.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                self.lr_t.data_ptr(), self.betas[0], self.betas[1], self.eps, self.wd,
+                self.step_t.data_ptr(), self.grad_scale, self.ticket.data_ptr(),
+                self.tick_counter.data_ptr() if self.tick_counter is not None else None)
+
     def step(self):
         nat.call("l3u_adamw_tick", self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(),
                  self.v.data_ptr(), self.p.numel(), self.lr_t.data_ptr(), self.betas[0],

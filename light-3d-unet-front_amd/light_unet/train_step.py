@@ -77,7 +77,10 @@ class TrainStep:
             ftl = (t, None, abgs, self.loss, sums[0], sums[1])
         else:
             ftl = (t, sums, abgs, self.loss)
-        self.engine.backward(self.flat, self.gflat, sv, None, need_dx=False, ftl=ftl)
+        # one process: the gradient reduction launch also applies the AdamW update
+        self.engine.backward(self.flat, self.gflat, sv, None, need_dx=False, ftl=ftl,
+                             opt=self.opt if self.world == 1 else None)
+        return self.engine.applied_update
 
     def _grad_exchange(self):
         if self.world > 1:
@@ -98,9 +101,9 @@ class TrainStep:
         self._check_flat()
         p, sv, sums = self._fwd(x, t)
         self._sums_exchange(sums)
-        self._bwd(p, sv, t, sums)
-        self._grad_exchange()
-        self.opt.step()
+        if not self._bwd(p, sv, t, sums):
+            self._grad_exchange()
+            self.opt.step()
         return self.loss
 
     # ----------------------------------------------------------------- hipGraph step

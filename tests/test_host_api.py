@@ -152,3 +152,14 @@ def test_variant_group_divisibility_error():
     from light_unet.models.unet3d import Lightweight3DUNet
     with pytest.raises(ValueError):
         Lightweight3DUNet(encoder_channels=[12, 20, 40, 80], use_depthwise_separable=False, groups=8)
+
+
+def test_fused_update_needs_exact_cover():
+    """l3u_reduce_segments_adamw is used only when the reduction items write every gradient
+    element exactly once and none accumulates (engine._items_cover_once)."""
+    from light_unet.engine import _items_cover_once
+    it = lambda dst, ln, acc=0: (0, 1, 1, 1, ln, dst, acc, 0)   # noqa: E731
+    assert _items_cover_once([it(0, 4), it(4, 6)], 10)
+    assert not _items_cover_once([it(0, 4), it(5, 5)], 10)          # element 4 not produced
+    assert not _items_cover_once([it(0, 6), it(4, 6)], 10)          # elements 4, 5 twice
+    assert not _items_cover_once([it(0, 4), it(4, 6, acc=1)], 10)   # accumulating item

@@ -190,6 +190,36 @@ def test_trainstep_eager_graph_and_autograd_agree(cuda, golden):
     assert torch.equal(pb, pc), "graph replay must be bitwise identical to eager"
 
 
+def test_trainstep_fused_update_bitwise(cuda, golden, monkeypatch):
+    """One process: the gradient reduction launch that also applies AdamW
+    (l3u_reduce_segments_adamw) gives bitwise the parameters, moments, gradients, step and
+    Dropout3d counters of the two-launch step (l3u_reduce_segments + l3u_adamw_tick)."""
+    from light_unet import engine as E
+    from light_unet.models.unet3d import Lightweight3DUNet
+    from light_unet.train_step import TrainStep
+    z = golden("model_b2_32.npz")
+    sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w/")}
+    x = torch.from_numpy(z["x"]).to(cuda)
+    t = torch.from_numpy(z["target"]).to(cuda)
+    runs = []
+    for fuse in (False, True):
+        monkeypatch.setattr(E, "_FUSE_ADAMW", fuse)
+        m = Lightweight3DUNet(dropout_p=0.1)
+        m.load_state_dict(sd)
+        m = m.to(cuda).train()
+        ts = TrainStep(m, lr=1e-3, weight_decay=1e-2)
+        losses = [ts(x, t).item() for _ in range(3)]
+        assert m.engine.applied_update == fuse
+        runs.append((losses, ts.flat.clone(), ts.gflat.clone(), ts.opt.m.clone(),
+                     ts.opt.v.clone(), int(ts.opt.step_t.item()), int(m._rng_counter.item()),
+                     int(ts.opt.ticket.item())))
+    a, b = runs
+    assert a[0] == b[0]
+    for u, w in zip(a[1:5], b[1:5]):
+        assert torch.equal(u, w)
+    assert a[5:] == b[5:] and b[5] == 3 and b[7] == 0
+
+
 def test_state_dict_roundtrip_and_reference_keys(cuda, golden):
     z = golden("model_b1_48.npz")
     model, sd = _model(z, (16, 32, 64, 128), cuda)
