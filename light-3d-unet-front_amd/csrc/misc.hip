@@ -365,6 +365,8 @@ __device__ __forceinline__ AdamWStep adamw_step(float lrv, float beta1, float be
 }
 __device__ __forceinline__ void adamw_update(const AdamWStep& c, float& pv, float gv, float& mv,
                                              float& vv) {
+  // no FMA contraction: the rounding must not depend on how the surrounding kernel is scheduled
+#pragma clang fp contract(off)
   gv *= c.gscale;
   pv *= c.decay;
   mv = mv + (1.f - c.beta1) * (gv - mv);                 // exp_avg.lerp_(grad, 1 - beta1)

@@ -215,8 +215,8 @@ def test_trainstep_fused_update_bitwise(cuda, golden, monkeypatch):
                      int(ts.opt.ticket.item())))
     a, b = runs
     assert a[0] == b[0]
-    for u, w in zip(a[1:5], b[1:5]):
-        assert torch.equal(u, w)
+    for name, u, w in zip(("params", "grads", "exp_avg", "exp_avg_sq"), a[1:5], b[1:5]):
+        assert torch.equal(u, w), (name, int((u != w).sum()), float((u - w).abs().max()))
     assert a[5:] == b[5:] and b[5] == 3 and b[7] == 0
 
 
