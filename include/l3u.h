@@ -474,7 +474,12 @@ int l3u_reduce_segments(const float* src, const long long* items, int nitems, fl
 /* the same reduction fused with the AdamW update (l3u_adamw_tick's arithmetic and step /
  * counter2 / ticket protocol) of the parameters it produces, for one process (no gradient
  * exchange between the two): requires that every one of the numel parameters is the output of
- * exactly one item and that no item accumulates; g receives the reduced gradient as well      */
+ * exactly one item and that no item accumulates; g receives the reduced gradient as well.
+ * ticket: L3U_ADAMW_TICKET_INTS zeroed ints (left zeroed; element 0 may be the l3u_adamw_tick
+ * ticket of the same optimizer)                                                                */
+#define L3U_TICKET_GROUPS 32
+#define L3U_TICKET_STRIDE 32
+#define L3U_ADAMW_TICKET_INTS (L3U_TICKET_STRIDE * (L3U_TICKET_GROUPS + 1))
 int l3u_reduce_segments_adamw(const float* src, const long long* items, int nitems, float* g,
                               float* p, float* m, float* v, const float* lr, float beta1,
                               float beta2, float eps, float weight_decay, int* step,

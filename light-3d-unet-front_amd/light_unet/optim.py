@@ -12,6 +12,8 @@ import torch
 
 from . import _native as nat
 
+ADAMW_TICKET_INTS = 32 * 33   # include/l3u.h L3U_ADAMW_TICKET_INTS
+
 
 class FlatAdamW:
     def __init__(self, flat_params, flat_grads, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
@@ -31,7 +33,9 @@ class FlatAdamW:
         self.wd = float(weight_decay)
         self.grad_scale = float(grad_scale)
         self.tick_counter = tick_counter
-        self.ticket = torch.zeros(1, dtype=torch.int32, device=flat_params.device)
+        # [0]: the update's ticket; the rest: the group tickets of the fused reduce + update
+        # (include/l3u.h L3U_ADAMW_TICKET_INTS)
+        self.ticket = torch.zeros(ADAMW_TICKET_INTS, dtype=torch.int32, device=flat_params.device)
 
     def set_lr(self, lr):
         self.lr_t.fill_(float(lr))
