@@ -476,8 +476,7 @@ int l3u_reduce_segments(const float* src, const long long* items, int nitems, fl
  * exchange between the two): requires that every one of the numel parameters is the output of
  * exactly one item and that no item accumulates; g receives the reduced gradient as well.
  * ticket: L3U_ADAMW_TICKET_INTS zeroed ints (left zeroed; element 0 may be the l3u_adamw_tick
- * ticket of the same optimizer).  ticket == NULL: an early part of the step's items (reads
- * *step, advances nothing); the step's last launch, with the ticket, advances the counters    */
+ * ticket of the same optimizer)                                                                */
 #define L3U_TICKET_GROUPS 32
 #define L3U_TICKET_STRIDE 32
 #define L3U_ADAMW_TICKET_INTS (L3U_TICKET_STRIDE * (L3U_TICKET_GROUPS + 1))

@@ -523,7 +523,6 @@ __global__ __launch_bounds__(256) void reduce_segments_adamw_kernel(
     adamw_update(adamw_step(lrv, beta1, beta2, eps, wd, tc, gscale), pv, gv, mv, vv);
     p[j] = pv; m[j] = mv; v[j] = vv;
   }
-  if (!ticket) return;   // an early part: the final launch advances the counters
   __syncthreads();
   // two-level ticket: thousands of workgroups taking one device-scope atomic serialize on that
   // address (measured +16 us at 2.6k workgroups); L3U_TICKET_GROUPS counters a cache line apart
@@ -958,7 +957,7 @@ int l3u_reduce_segments_adamw(const float* src, const long long* items, int nite
                               float* p, float* m, float* v, const float* lr, float beta1,
                               float beta2, float eps, float weight_decay, int* step,
                               float grad_scale, int* ticket, int* counter2, hipStream_t stream) {
-  L3U_REQUIRE(nitems > 0 && step);
+  L3U_REQUIRE(nitems > 0 && step && ticket);
   hipLaunchKernelGGL(reduce_segments_adamw_kernel, dim3(nitems), dim3(256), 0, stream, src, items,
                      g, p, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale, ticket,
                      counter2);

@@ -61,10 +61,6 @@ _FRONT_R1 = os.environ.get("L3U_FRONT_R1", "1") != "0"
 # parameters it produces (l3u_reduce_segments_adamw: no separate l3u_adamw_tick launch);
 # L3U_FUSE_ADAMW=0 keeps the two launches
 _FUSE_ADAMW = os.environ.get("L3U_FUSE_ADAMW", "1") != "0"
-# ... and the items of the decoder levels (complete once the backward reaches the bottleneck)
-# are reduced and applied on a side stream, overlapping the latency-bound small levels;
-# L3U_EARLY_REDUCE=0 reduces everything at the end
-_EARLY_REDUCE = os.environ.get("L3U_EARLY_REDUCE", "1") != "0"
 
 
 def _items_cover_once(items, numel):
@@ -224,10 +220,6 @@ class UNetEngine:
         self._arenas = {}
         self._items = {}
         self._cover_once = {}
-        self._mark = {}            # key -> number of items complete at the decoder / bottleneck seam
-        self._early = None         # (items of the early part, optimizer) during a fused backward
-        self._mark_now = 0
-        self._side = None
         self.applied_update = False
         self._dry = False
         self._items_rec = None
@@ -688,22 +680,15 @@ class UNetEngine:
                                                 device=dev)
                 self._items[key] = torch.tensor(self._items_rec, dtype=torch.int64, device=dev)
                 self._cover_once[key] = _items_cover_once(self._items_rec, gflat.numel())
-                self._mark[key] = self._mark_now
             self.bwd_arena.reset(self._arenas[key])
             self._items_rec = []
-            items = self._items[key]
-            self.applied_update = (opt is not None and _FUSE_ADAMW and self._cover_once[key]
-                                   and opt.g is gflat and opt.p is flat)
-            mark = self._mark[key] if (self.applied_update and _EARLY_REDUCE) else 0
-            self._early = (items[:mark], opt) if 0 < mark < items.shape[0] else None
             dx = self._backward_impl(flat, gflat, sv, dp, need_dx, ftl)
         finally:
             self._grad_phase = False
+        items = self._items[key]
+        self.applied_update = (opt is not None and _FUSE_ADAMW and self._cover_once[key]
+                               and opt.g is gflat and opt.p is flat)
         if self.applied_update:
-            if self._early is not None:
-                items = items[self._early[0].shape[0]:]
-                torch.cuda.current_stream().wait_stream(self._side)
-                self._early = None
             nat.call("l3u_reduce_segments_adamw", self.bwd_arena.ptr(0), items.data_ptr(),
                      items.shape[0], *opt.fused_args(), nat.stream())
         else:
@@ -793,11 +778,6 @@ class UNetEngine:
                 self._seg(pw, npw, ci * co * 8, 1, ci * co * 8, up + "up.weight")
                 self._seg(pb, npw, co, 1, co, up + "up.bias")
             dout = V(dprev, 0, ci * S[lvl + 1], ci)
-        # ---- the decoder's reduction items are complete: their fused reduce + update can run
-        # beside the rest of the backward
-        self._mark_now = len(self._items_rec)
-        if self._early is not None and not self._dry:
-            self._launch_early()
         # ---- bottleneck
         dx4 = e(N, c3, S[3])
         self._block_bwd(flat, "bottleneck.", sv["blk"]["bottleneck."], dout,
@@ -832,18 +812,6 @@ class UNetEngine:
         self._block_bwd(flat, "init_conv.", sv["blk"]["init_conv."], dout, V(dx, 0, S[0], 1),
                         st, dev)
         return dx if need_dx else None
-
-    def _launch_early(self):
-        items, opt = self._early
-        cur = torch.cuda.current_stream()
-        if self._side is None or self._side.device != cur.device:
-            self._side = torch.cuda.Stream(device=cur.device)
-        self._side.wait_stream(cur)
-        args = list(opt.fused_args())
-        args[11] = None   # no ticket: the step's final launch advances the counters
-        with torch.cuda.stream(self._side):
-            nat.call("l3u_reduce_segments_adamw", self.bwd_arena.ptr(0), items.data_ptr(),
-                     items.shape[0], *args, nat.stream())
 
     def _tail_fusable(self, sv, cin, cout, S):
         """The block tail's backward can ride in the prologues of the two pointwise backwards

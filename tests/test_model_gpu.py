@@ -193,8 +193,7 @@ def test_trainstep_eager_graph_and_autograd_agree(cuda, golden):
 def test_trainstep_fused_update_bitwise(cuda, golden, monkeypatch):
     """One process: the gradient reduction launch that also applies AdamW
     (l3u_reduce_segments_adamw) gives bitwise the parameters, moments, gradients, step and
-    Dropout3d counters of the two-launch step (l3u_reduce_segments + l3u_adamw_tick), also
-    with the decoder levels' items reduced early on a side stream."""
+    Dropout3d counters of the two-launch step (l3u_reduce_segments + l3u_adamw_tick)."""
     from light_unet import engine as E
     from light_unet.models.unet3d import Lightweight3DUNet
     from light_unet.train_step import TrainStep
@@ -203,10 +202,8 @@ def test_trainstep_fused_update_bitwise(cuda, golden, monkeypatch):
     x = torch.from_numpy(z["x"]).to(cuda)
     t = torch.from_numpy(z["target"]).to(cuda)
     runs = []
-    # (fused, early part on a side stream)
-    for fuse, early in ((False, False), (True, False), (True, True)):
+    for fuse in (False, True):
         monkeypatch.setattr(E, "_FUSE_ADAMW", fuse)
-        monkeypatch.setattr(E, "_EARLY_REDUCE", early)
         m = Lightweight3DUNet(dropout_p=0.1)
         m.load_state_dict(sd)
         m = m.to(cuda).train()
@@ -216,12 +213,11 @@ def test_trainstep_fused_update_bitwise(cuda, golden, monkeypatch):
         runs.append((losses, ts.flat.clone(), ts.gflat.clone(), ts.opt.m.clone(),
                      ts.opt.v.clone(), int(ts.opt.step_t.item()), int(m._rng_counter.item()),
                      int(ts.opt.ticket.abs().sum().item())))
-    a = runs[0]
-    for b in runs[1:]:
-        assert a[0] == b[0]
-        for name, u, w in zip(("params", "grads", "exp_avg", "exp_avg_sq"), a[1:5], b[1:5]):
-            assert torch.equal(u, w), (name, int((u != w).sum()), float((u - w).abs().max()))
-        assert a[5:] == b[5:] and b[5] == 3 and b[7] == 0
+    a, b = runs
+    assert a[0] == b[0]
+    for name, u, w in zip(("params", "grads", "exp_avg", "exp_avg_sq"), a[1:5], b[1:5]):
+        assert torch.equal(u, w), (name, int((u != w).sum()), float((u - w).abs().max()))
+    assert a[5:] == b[5:] and b[5] == 3 and b[7] == 0
 
 
 def test_state_dict_roundtrip_and_reference_keys(cuda, golden):
