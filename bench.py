@@ -38,7 +38,8 @@ METRIC = "train patches/sec (48³, bs=4/GPU) at 1/2/4/8 MI355X + fwd ms/patch"
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    # default: WORLD_SIZE under a launcher (torchrun --nproc-per-node N bench.py), else 1
+    ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=4)
@@ -57,6 +58,8 @@ def parse():
     ap.add_argument("--ftl-mode", default="exact", choices=["exact", "local"])
     ap.add_argument("--no-sliding", action="store_true", help="skip the config-4 inference timing")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (32->256, 64^3) timing")
+    ap.add_argument("--no-exchange", action="store_true",
+                    help="skip the one-GPU RCCL exchange probe (tools/rccl_probe.py)")
     ap.add_argument("--no-grouped", action="store_true",
                     help="skip the use_depthwise_separable=False (grouped) model timing")
     # multi-rank rehearsal on a one-GPU box: every rank on cuda:0, collectives over gloo
@@ -66,7 +69,10 @@ def parse():
                     help="write the recorded step's C-ABI calls (name, family, label, algorithmic "
                          "bytes) in launch order to this JSON file (tools/instep.py aligns them "
                          "with a rocprofv3 kernel trace of the graph-replayed step)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.gpus is None:
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
+    return args
 
 
 def synthetic_pool(n_pool, bs, size, rank, device):
@@ -90,18 +96,15 @@ def dw_bytes(N, C, S, e=4, acc=0):
 
 def pmc_traffic(N, C, size, acc=0):
     """Memory-side bytes per call of the dominant kernel from the committed rocprofv3 PMC passes
-    (tools/pmc.sh -> profiles/*_pmc_dw3_bwd.json), when they were taken at this exact shape."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_dw3_bwd.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        rec = json.load(f)
-    if f"[{N},{C},{size}^3]" not in rec.get("call", ""):
-        return None, None
-    if f"accumulate={acc}" not in rec.get("call", ""):   # taken in the step's mode
-        return None, None
-    return rec["traffic_bytes"], os.path.relpath(files[-1], ROOT) + " (FETCH_SIZE x2 + WRITE_SIZE)"
+    (tools/pmc.sh -> profiles/*_pmc_dw3_bwd.json) taken at this exact shape and mode, preferring
+    the record made on this product tree.  (bytes, source, tree_matches)."""
+    def ok(rec):
+        call = rec.get("call", "")
+        return f"[{N},{C},{size}^3]" in call and f"accumulate={acc}" in call
+    rec, fn, same = _pick_record("*_pmc_dw3_bwd.json", ok)
+    if rec is None or not ok(rec):
+        return None, None, False
+    return rec["traffic_bytes"], os.path.relpath(fn, ROOT) + " (FETCH_SIZE x2 + WRITE_SIZE)", same
 
 
 class KernelTimer:
@@ -320,42 +323,68 @@ def family_rooflines(nat_call, calls):
     return out
 
 
-def instep_evidence(workload, launches):
-    """In-step family rooflines from the newest committed tools/instep.py record of this workload
-    (a rocprofv3 kernel trace of the graph-replayed step aligned with its C-ABI calls:
-    profiles/*_instep_<workload>.json), used only when it has this step's launch count (the same
-    schedule); per family: launches, bytes, in-step us, achieved GB/s, fraction of 8 TB/s."""
+def _tree():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from treehash import product_tree
+    return product_tree()
+
+
+def _pick_record(pattern, ok=None):
+    """The committed evidence record (profiles/<pattern>) that describes THIS product tree: the
+    newest whose "tree" hash (tools/treehash.py, stored when the record was made) equals the
+    running tree's; failing that the newest one `ok(rec)` accepts (e.g. the same launch count),
+    flagged tree_matches = False.  (rec, path, tree_matches) or (None, None, False)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_instep_{workload}.json")))
-    for fn in reversed(files):
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    recs = []
+    for fn in files:
         with open(fn) as f:
-            rec = json.load(f)
-        ncalls = rec["dw"]["launches"] + rec["gemm"]["launches"]
-        out = {"source": os.path.relpath(fn, ROOT), "commit": rec.get("commit"),
-               "step_kernel_us": rec["step_kernel_us"], "launches": rec["launches"],
-               "under_10us": rec.get("under_10us")}
-        for fam in ("dw", "gemm"):
-            out[fam] = {k: rec[fam][k] for k in ("launches", "bytes", "us", "achieved", "frac")}
-        out["dominant"] = max(rec["dw"]["calls"] + rec["gemm"]["calls"], key=lambda r: r["us"])
-        out["family_calls"] = ncalls
-        out["matches_this_step"] = (rec.get("calls") == launches) if launches is not None else None
-        return out
-    return None
+            recs.append((json.load(f), fn))
+    cur = _tree()
+    for rec, fn in reversed(recs):
+        if rec.get("tree") == cur:
+            return rec, fn, True
+    for rec, fn in reversed(recs):
+        if ok is None or ok(rec):
+            return rec, fn, False
+    return None, None, False
+
+
+def instep_evidence(workload, launches):
+    """In-step family rooflines from the committed tools/instep.py record of this workload made on
+    this product tree (a rocprofv3 kernel trace of the graph-replayed step aligned with its C-ABI
+    calls: profiles/*_instep_<workload>.json); per family: launches, bytes, in-step us, achieved
+    GB/s, fraction of 8 TB/s.  `matches_this_step`: the record's tree hash is this tree's and it
+    has this step's launch count."""
+    rec, fn, same_tree = _pick_record(
+        f"*_instep_{workload}.json",
+        (lambda r: r.get("calls") == launches) if launches is not None else None)
+    if rec is None:
+        return None
+    ncalls = rec["dw"]["launches"] + rec["gemm"]["launches"]
+    out = {"source": os.path.relpath(fn, ROOT), "commit": rec.get("commit"), "tree": rec.get("tree"),
+           "tree_matches": same_tree,
+           "step_kernel_us": rec["step_kernel_us"], "launches": rec["launches"],
+           "under_10us": rec.get("under_10us")}
+    for fam in ("dw", "gemm"):
+        out[fam] = {k: rec[fam][k] for k in ("launches", "bytes", "us", "achieved", "frac")}
+    out["dominant"] = max(rec["dw"]["calls"] + rec["gemm"]["calls"], key=lambda r: r["us"])
+    out["family_calls"] = ncalls
+    out["matches_this_step"] = (same_tree and (launches is None or rec.get("calls") == launches))
+    return out
 
 
 def step_traffic_evidence(workload, ms_per_step):
-    """Whole-step HBM traffic of the eager step from the newest committed PMC record of this
-    workload (tools/pmc_step.sh -> profiles/*_pmc_step_<workload>.json: FETCH_SIZE x 2 +
-    WRITE_SIZE per launch, separate passes) and the average rate it implies at this step time."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_step_{workload}.json")))
-    if not files:
+    """Whole-step HBM traffic of the eager step from the committed PMC record of this workload
+    made on this product tree (tools/pmc_step.sh -> profiles/*_pmc_step_<workload>.json:
+    FETCH_SIZE x 2 + WRITE_SIZE per launch, separate passes) and the average rate it implies at
+    this step time."""
+    rec, fn, same_tree = _pick_record(f"*_pmc_step_{workload}.json")
+    if rec is None:
         return None
-    with open(files[-1]) as f:
-        rec = json.load(f)
     b = rec["step_traffic_bytes"]
-    out = {"source": os.path.relpath(files[-1], ROOT), "commit": rec.get("commit"),
-           "bytes": b, "launches": rec.get("launches")}
+    out = {"source": os.path.relpath(fn, ROOT), "commit": rec.get("commit"), "tree": rec.get("tree"),
+           "tree_matches": same_tree, "bytes": b, "launches": rec.get("launches")}
     if ms_per_step:
         out["avg_tb_s"] = round(b / (ms_per_step * 1e-3) / 1e12, 3)
         out["frac_of_8tb_s"] = round(out["avg_tb_s"] / 8.0, 4)
@@ -364,21 +393,16 @@ def step_traffic_evidence(workload, ms_per_step):
 
 def gemm_mfma_evidence(top=5):
     """MFMA-busy fractions of the step's GEMM launches from the committed rocprofv3 passes
-    (tools/pmc_step.sh + tools/pmc_gemm.sh -> tools/pmc_launch_json.py -> profiles/*_pmc_step.json)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_step.json")))
-    items, src = [], None
-    for fn in reversed(files):   # the newest pass that carries the MFMA counters
-        with open(fn) as f:
-            rec = json.load(f)
-        items = [i for i in rec.get("items", []) if "mfma_util" in i and i.get("mfma_busy_cycles", 0) > 0]
-        if items:
-            src = fn
-            break
-    if not items:
+    (tools/pmc_step.sh + tools/pmc_gemm.sh -> tools/pmc_launch_json.py -> profiles/*_pmc_step.json),
+    the record made on this product tree first."""
+    def ok(rec):
+        return any("mfma_util" in i and i.get("mfma_busy_cycles", 0) > 0 for i in rec.get("items", []))
+    rec, src, same = _pick_record("r*_pmc_step.json", ok)
+    if rec is None or not ok(rec):
         return None
+    items = [i for i in rec["items"] if "mfma_util" in i and i.get("mfma_busy_cycles", 0) > 0]
     items.sort(key=lambda i: -i["pmc_dur_us"])
-    return {"source": os.path.relpath(src, ROOT),
+    return {"source": os.path.relpath(src, ROOT), "tree_matches": same,
             "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)",
             "ceiling_note": "fp32 MFMA at the HBM roofline: 5.5 flop/B x 8 TB/s = 44 TFLOP/s = 0.28 of "
                             "the 157 TFLOP/s fp32 matrix peak",
@@ -808,6 +832,26 @@ def bf16_bench(device, args, enc, world, rank, pool):
                          "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None}}
 
 
+def exchange_probe(timeout=240):
+    """The world > 1 step's exchange on ONE GPU (tools/rccl_probe.py in a child process: a
+    one-rank RCCL group; the single-graph step vs the three graph segments with eager RCCL
+    all-reduces vs the all-reduces captured in the graph).  exchange_us = segmented (captured)
+    step minus single-graph step: what the data-parallel protocol adds per step before any link
+    time."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        try:
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "rccl_probe.py"), d,
+                                str(_free_port())], capture_output=True, text=True, timeout=timeout)
+        except subprocess.TimeoutExpired:
+            return {"error": f"timeout after {timeout} s"}
+        if r.returncode != 0:
+            return {"error": (r.stderr or r.stdout)[-600:]}
+        with open(os.path.join(d, "rccl.json")) as f:
+            return json.load(f)
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -931,6 +975,7 @@ def main():
     dropin = dropin_bench(device) if (rank == 0 and not args.no_dropin) else None
     lesion_r = lesion_bench(device) if (rank == 0 and not args.no_data) else None
     patches_r = patches_bench(device) if (rank == 0 and not args.no_data) else None
+    exch = exchange_probe() if (world == 1 and not args.no_exchange) else None
     fwd1 = fwd_ms_per_patch(model, 1, args.size, device) if rank == 0 else None
     fwd4 = fwd_ms_per_patch(model, args.batch, args.size, device) if rank == 0 else None
     out = None
@@ -940,7 +985,7 @@ def main():
         dacc = int(bool(dom_calls[0][1][8])) if dom_calls else 0   # accumulates into d(input)
         dbytes = dw_bytes(N, cdom, S, e=2 if args.dtype == "bf16" else 4, acc=dacc)
         achieved = dbytes / (dom_ms * 1e-3) / 1e9 if dom_ms else None
-        traffic, traffic_src = pmc_traffic(N, cdom, args.size, dacc)
+        traffic, traffic_src, traffic_tree = pmc_traffic(N, cdom, args.size, dacc)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -971,6 +1016,7 @@ def main():
             "lesion_256": lesion_r,
             "patches": patches_r,
             "launches_per_step": n_launch_calls,
+            "exchange": exch,
             "roofline": {
                 "kernel": f"l3u_dw3_bwd [{N},{cdom},{args.size}^3] (up3.res_block.conv1.depthwise "
                           "backward: one single-pass launch, data and weight gradients from one "
@@ -983,6 +1029,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "traffic_tree_matches": traffic_tree,
                 "algorithmic_bytes": dbytes,
                 "avg_launch_ms": round(dom_ms, 5) if dom_ms else None,
                 "cache_exceeding": dw_bwd_cache_exceeding(device),

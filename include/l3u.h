@@ -38,6 +38,10 @@ extern "C" {
 
 typedef unsigned short l3u_bf16;   /* bfloat16 bit pattern (torch.bfloat16 storage) */
 
+/* ABI version of this header (L3U_ABI_VERSION); the ctypes binding refuses a library that reports
+ * another.  3: l3u_norm_src.rank1, L3U_ADAMW_TICKET_INTS tickets, the l3u_sblock_* entry points
+ * removed (round 3); the round-4 entry points. */
+#define L3U_ABI_VERSION 3
 int l3u_abi_version(void);
 
 /* Where an InstanceNorm record comes from when a consumer kernel finalizes it itself (no separate

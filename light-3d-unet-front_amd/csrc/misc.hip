@@ -969,7 +969,7 @@ int l3u_counter_add(int* counter, int value, hipStream_t stream) {
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_abi_version(void) { return 2; }
+int l3u_abi_version(void) { return L3U_ABI_VERSION; }
 
 }  // extern "C"
 

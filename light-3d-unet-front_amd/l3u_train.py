@@ -28,14 +28,25 @@ import sys
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def share_validation(trainer, rank, dist):
+# how long ranks > 0 may wait for rank 0's validation (sliding-window inference + lesion metrics
+# over the whole validation split, trainer.py:349-458)
+VALIDATION_TIMEOUT_S = float(os.environ.get("L3U_VALIDATION_TIMEOUT_S", str(6 * 3600)))
+
+
+def share_validation(trainer, rank, dist, timeout_s=None):
     """Trainer.validate on rank 0 only, its (val_loss, metrics) broadcast to every rank; no
-    checkpoint files from ranks > 0."""
+    checkpoint files from ranks > 0.  The broadcast goes over a gloo side group with its own long
+    timeout (VALIDATION_TIMEOUT_S): ranks > 0 wait there, on the host, for the whole of rank 0's
+    validation, never inside an NCCL collective that the RCCL watchdog would abort (its default
+    timeout is 10 minutes)."""
+    import datetime
     ref_validate = trainer.validate
+    side = dist.new_group(backend="gloo", timeout=datetime.timedelta(
+        seconds=VALIDATION_TIMEOUT_S if timeout_s is None else timeout_s))
 
     def validate(epoch):
         out = [ref_validate(epoch) if rank == 0 else None]
-        dist.broadcast_object_list(out, src=0)
+        dist.broadcast_object_list(out, src=0, group=side)
         return out[0]
     trainer.validate = validate
     if rank > 0:

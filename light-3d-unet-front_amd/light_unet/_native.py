@@ -12,6 +12,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "L3U_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libl3u_hip.so"))
 
+# include/l3u.h L3U_ABI_VERSION: the library must report exactly this
+ABI_VERSION = 3
+
 P = ctypes.c_void_p
 I = ctypes.c_int
 L = ctypes.c_longlong
@@ -162,6 +165,10 @@ def load():
             raise NativeError(f"{LIB_PATH} does not export {name}: rebuild the library")
         fn.argtypes = args
         fn.restype = I
+    ver = lib.l3u_abi_version()
+    if ver != ABI_VERSION and not os.environ.get("L3U_LIB"):
+        raise NativeError(f"{LIB_PATH} reports ABI version {ver}, this binding expects "
+                          f"{ABI_VERSION}: rebuild the library")
     _lib = lib
     return lib
 

@@ -588,7 +588,8 @@ class UNetEngine:
                 and nat.query("l3u_dwpw_supported", cout, cout, d, h, w, 0)
                 and nat.query("l3u_dw3_bwd_rank1", N, cout, d, h, w)
                 and nat.query("l3u_pw_bwd_supported", cout, 1, S)
-                and _TAIL_FUSE and nat.query("l3u_norm_act_nblocks", S) > 1 and cout <= 32
+                # the rank-1 pointwise backward variants take one 16-column block (J = cout <= 16)
+                and _TAIL_FUSE and nat.query("l3u_norm_act_nblocks", S) > 1 and cout <= 16
                 and nat.query("l3u_pw_bwd_supported", cout, cout, S))
 
     def _conv_w(self, flat, pre, which):

@@ -30,17 +30,18 @@ def world_size(group=None):
     return 1
 
 
-def exchange_ftl_sums(sums, mode, group=None):
-    """In place: the (tp, fp, fn) sums of this rank's shard -> the global-batch sums (exact)."""
-    if world_size(group) > 1 and mode == "exact":
+def exchange_ftl_sums(sums, mode, group=None, force=False):
+    """In place: the (tp, fp, fn) sums of this rank's shard -> the global-batch sums (exact).
+    force: issue the collective even in a one-rank group (tests the RCCL path on one GPU)."""
+    if (world_size(group) > 1 or force) and mode == "exact":
         dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
     return sums
 
 
-def exchange_grads(gflat, mode, group=None):
+def exchange_grads(gflat, mode, group=None, force=False):
     """In place: this rank's flat gradient -> the gradient of the global objective."""
     w = world_size(group)
-    if w > 1:
+    if w > 1 or force:
         if mode == "local":
             dist.all_reduce(gflat, op=dist.ReduceOp.SUM, group=group)
             gflat.div_(w)

@@ -22,10 +22,15 @@ from .optim import FlatAdamW
 
 class TrainStep:
     def __init__(self, model, loss_cfg=None, lr=1e-4, weight_decay=1e-5, betas=(0.9, 0.999),
-                 eps=1e-8, group=None, ftl_mode="exact", distributed=True, dtype=None):
+                 eps=1e-8, group=None, ftl_mode="exact", distributed=True, dtype=None,
+                 force_exchange=False, capture_collectives=False):
         """dtype: activation storage of the step (torch.float32 or torch.bfloat16; default the
         model's compute_dtype, else fp32).  Master weights, AdamW state, gradients and the loss
-        stay fp32."""
+        stay fp32.
+        force_exchange: run the data-parallel step (FocalTversky sums and gradient all-reduces,
+        separate update launch) even in a one-rank process group -- the RCCL path on one GPU.
+        capture_collectives: capture() records the collectives into the step's one hipGraph
+        instead of enqueuing them eagerly between three graph segments."""
         loss_cfg = loss_cfg or {}
         self.alpha = float(loss_cfg.get("alpha", 0.7))
         self.beta = float(loss_cfg.get("beta", 0.3))
@@ -45,6 +50,10 @@ class TrainStep:
         self.group = group
         # distributed=False: a rank-local step (no exchange) even inside a process group
         self.world = world_size(group) if distributed else 1
+        self.force = bool(force_exchange and distributed)
+        # the exchange protocol runs (collectives, no fused update) on > 1 rank or when forced
+        self.exchange = self.world > 1 or self.force
+        self.capture_collectives = bool(capture_collectives)
         self.ftl_mode = ftl_mode
         dev = self.flat.device
         self.loss = torch.zeros((), dtype=torch.float32, device=dev)
@@ -62,7 +71,7 @@ class TrainStep:
                                     counter=self.model._rng_counter, bump_counter=False,
                                     save=True, target=t,
                                     ftl_part=part)
-        if self.world == 1:
+        if not self.exchange:
             # one process: the out_conv backward reduces the partials itself (no reduce launch)
             return p, sv, (part, nparts)
         sums = torch.empty(3, dtype=torch.float64, device=p.device)
@@ -79,16 +88,16 @@ class TrainStep:
             ftl = (t, sums, abgs, self.loss)
         # one process: the gradient reduction launch also applies the AdamW update
         self.engine.backward(self.flat, self.gflat, sv, None, need_dx=False, ftl=ftl,
-                             opt=self.opt if self.world == 1 else None)
+                             opt=None if self.exchange else self.opt)
         return self.engine.applied_update
 
     def _grad_exchange(self):
-        if self.world > 1:
-            exchange_grads(self.gflat, self.ftl_mode, self.group)
+        if self.exchange:
+            exchange_grads(self.gflat, self.ftl_mode, self.group, force=self.force)
 
     def _sums_exchange(self, sums):
-        if self.world > 1:
-            exchange_ftl_sums(sums, self.ftl_mode, self.group)
+        if self.exchange:
+            exchange_ftl_sums(sums, self.ftl_mode, self.group, force=self.force)
 
     def _check_flat(self):
         if self.model._flat is not self.flat:
@@ -108,9 +117,10 @@ class TrainStep:
 
     # ----------------------------------------------------------------- hipGraph step
     def capture(self, x_static, t_static, warmup=2):
-        """Capture the step into hipGraphs over static input buffers.  Collectives stay eager
-        between graph segments: [fwd+sums] -> allreduce(sums) -> [loss+bwd] -> allreduce(grads)
-        -> [adamw].  On one GPU the three segments are one graph."""
+        """Capture the step into hipGraphs over static input buffers.  With the exchange, the
+        collectives stay eager between graph segments: [fwd+sums] -> allreduce(sums) ->
+        [loss+bwd] -> allreduce(grads) -> [adamw], unless capture_collectives (RCCL captured in
+        the one graph).  Without it (one process) the step is one graph."""
         self.xs, self.ts = x_static, t_static
         # warm-up runs full steps (arena sizing, kernel loading); they must leave no trace: the
         # parameters, the AdamW state and counters and the Dropout3d counter are restored, so
@@ -131,7 +141,7 @@ class TrainStep:
                 t.copy_(c)
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
-        if self.world == 1:
+        if not self.exchange or self.capture_collectives:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
                 self(self.xs, self.ts)

@@ -44,7 +44,7 @@ def test_bench_self_launches_two_ranks(cuda):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
            "--warmup", "1", "--dist-backend", "gloo", "--one-device", "--no-cpu-baseline",
-           "--no-config5", "--no-sliding", "--no-grouped", "--no-bf16", "--no-dropin", "--no-data"]
+           "--no-config5", "--no-sliding", "--no-grouped", "--no-bf16", "--no-dropin", "--no-data", "--no-exchange"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -125,13 +125,17 @@ def test_mode_validation():
         check_mode("sum")
 
 
-def _share_validation_worker(rank, world, port, q):
+def _share_validation_worker(rank, world, port, q, slow_s=0.0):
+    import datetime
     import sys as _s
+    import time as _t
     _s.path.insert(0, PKG)
     import torch.distributed as dist
     import l3u_train
+    # the main group's collectives time out after 3 s: a validation longer than that must not
+    # reach them (the RCCL watchdog stands in here)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
-                            world_size=world)
+                            world_size=world, timeout=datetime.timedelta(seconds=3))
 
     class T:
         calls = 0
@@ -139,6 +143,7 @@ def _share_validation_worker(rank, world, port, q):
 
         def validate(self, epoch):
             T.calls += 1
+            _t.sleep(slow_s)
             return 0.0, {"best_recall": 0.5 + epoch, "rank": rank}
 
         def save_checkpoint(self, epoch, is_best=False):
@@ -153,12 +158,14 @@ def _share_validation_worker(rank, world, port, q):
 
 def test_validation_on_rank0_broadcast():
     """l3u_train: Trainer.validate runs on rank 0 only and every rank receives its result (same
-    scheduler / early-stopping decisions); ranks > 0 write no checkpoints."""
+    scheduler / early-stopping decisions); ranks > 0 write no checkpoints.  Rank 0's validation
+    takes 4 s, longer than the main group's 3 s collective timeout: rank 1 waits on the side
+    group, so nothing times out."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_share_validation_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_share_validation_worker, args=(r, 2, port, q, 4.0)) for r in range(2)]
     for p in ps:
         p.start()
     got = sorted(q.get(timeout=60) for _ in ps)

@@ -14,7 +14,7 @@ if [ "${AB_TESTS:-1}" != "0" ]; then
 fi
 run() {
   env $2 L3U_LIB=$PWD/light-3d-unet-front_amd/lib/var_$1.so timeout -k 10 300 python bench.py --steps 60 --warmup 10 \
-      --no-cpu-baseline --no-config5 --no-sliding --no-grouped --no-bf16 --no-dropin --no-data $AB_ARGS 2>&1 | grep metric | \
+      --no-cpu-baseline --no-config5 --no-sliding --no-grouped --no-bf16 --no-dropin --no-data --no-exchange $AB_ARGS 2>&1 | grep metric | \
       python -c "import sys,json; d=json.loads(sys.stdin.read()); print('$1', d['value'], d['ms_per_step'])"
 }
 for i in $(seq $REPS); do

@@ -10,8 +10,12 @@ dropped before the alignment, which must then match one kernel per call.
 """
 import csv
 import json
+import os
 import re
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from treehash import product_tree  # noqa: E402
 
 PEAK = 8000.0
 
@@ -102,7 +106,7 @@ def main():
                                  "frac": round(ach / PEAK, 4)})
     rec = {"what": "in-step durations (rocprofv3 kernel trace of the graph-replayed step, mean over "
                    f"{nsteps} steps) against the calls' algorithmic bytes",
-           "commit": commit, "workload": workload,
+           "commit": commit, "tree": product_tree(), "workload": workload,
            "step_kernel_us": round(sum(u for _, u in ks), 1), "launches": len(ks),
            "calls": len(calls)}
     for f, rows in fam.items():

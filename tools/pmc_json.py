@@ -11,6 +11,10 @@ import glob
 import json
 import re
 import sys
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from treehash import product_tree  # noqa: E402
 
 
 def per_kernel(d, counter):
@@ -39,6 +43,7 @@ def main():
            "kernels": ks,
            "traffic_bytes": sum(v["fetch_bytes"] + v["write_bytes"] for v in ks.values()),
            "algorithmic_bytes": 4 * 4 * 4 * 32 * 48 ** 3 + 4 * 27 * 32}
+    rec["tree"] = product_tree()
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 

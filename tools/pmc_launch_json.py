@@ -12,6 +12,10 @@ import csv
 import json
 import re
 import sys
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from treehash import product_tree  # noqa: E402
 
 
 def launches(path, counter):
@@ -27,7 +31,7 @@ def launches(path, counter):
 
 
 def last_step(seq):
-    ends = [i for i, x in enumerate(seq) if x["kernel"].startswith("adamw")]
+    ends = [i for i, x in enumerate(seq) if "adamw" in x["kernel"]]
     return seq[ends[-2] + 1:ends[-1] + 1]
 
 
@@ -54,6 +58,7 @@ def main():
                    "(SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)) of one eager bs-4 "
                    "48^3 training step, separate rocprofv3 passes", "launches": len(items),
            "step_traffic_bytes": tot, "items": items}
+    rec["tree"] = product_tree()
     json.dump(rec, open(out, "w"), indent=1)
     print(f"{len(items)} launches, {tot / 1e9:.3f} GB per step")
     for i, it in enumerate(items):

@@ -12,6 +12,6 @@ cd /tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/$c -o run -- \
     python3 $R/bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --no-config5 --no-sliding \
-    --no-grouped --no-bf16 --no-dropin --no-data "$@" > $OUT/$c.log 2>&1 || { echo "pass $c failed"; exit 1; }
+    --no-grouped --no-bf16 --no-dropin --no-data --no-exchange "$@" > $OUT/$c.log 2>&1 || { echo "pass $c failed"; exit 1; }
 done
 python3 $R/tools/pmc_step_json.py $OUT $OUT/pmc_step.json

@@ -8,6 +8,10 @@ import csv
 import json
 import re
 import sys
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from treehash import product_tree  # noqa: E402
 
 
 def launches(d, counter):
@@ -22,7 +26,7 @@ def launches(d, counter):
 
 
 def last_step(seq):
-    ends = [i for i, (n, _, _) in enumerate(seq) if n.startswith("adamw")]
+    ends = [i for i, (n, _, _) in enumerate(seq) if "adamw" in n]
     a, b = ends[-2], ends[-1]
     return seq[a + 1:b + 1]
 
@@ -38,6 +42,7 @@ def main():
     rec = {"what": "HBM bytes per launch of one eager bs-4 48^3 training step (FETCH_SIZE x2 + "
                    "WRITE_SIZE, separate rocprofv3 passes)", "launches": len(items),
            "step_traffic_bytes": tot, "items": items}
+    rec["tree"] = product_tree()
     json.dump(rec, open(out, "w"), indent=1)
     print(f"{len(items)} launches, {tot / 1e9:.3f} GB per step")
     for i in sorted(items, key=lambda i: -i["traffic"])[:25]:

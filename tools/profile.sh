@@ -11,7 +11,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run -- \
-  python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-config5 --no-sliding --no-grouped --no-bf16 --no-dropin --no-data --dump-calls $OUT/calls.json "$@" > $OUT/bench.log 2>&1
+  python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-config5 --no-sliding --no-grouped --no-bf16 --no-dropin --no-data --no-exchange --dump-calls $OUT/calls.json "$@" > $OUT/bench.log 2>&1
 rc=$?
 echo "rocprofv3 rc=$rc"
 [ $rc -eq 0 ] || exit $rc
