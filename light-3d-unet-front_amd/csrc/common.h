@@ -416,6 +416,14 @@ struct StampScope {   // the slot is taken at wave begin (the atomic's return ov
 #define L3U_STAMP_MARK(K) ((void)0)
 #endif
 
+// ConvTranspose3d(k2, s2) backward tile kernel (convt.hip): weight/bias partial count (0: shape
+// not taken) and the launch; same partial layout as l3u_convt_bwd_fused
+int convt_tile_nparts(int N, int Ci, int Co, int D, int H, int W);
+template <typename T>
+int convt_tile_launch(const float* dy, long long dy_nstride, const T* x, long long x_nstride,
+                      const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
+                      int N, int Ci, int Co, int D, int H, int W, hipStream_t stream);
+
 }  // namespace l3u
 
 // C-ABI twins: every activation entry point exists for fp32 and, with the suffix _bf16, for bf16

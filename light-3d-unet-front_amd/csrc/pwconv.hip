@@ -1639,6 +1639,9 @@ int convt_bwd_fused_impl(const float* dy, long long dy_nstride, const T* x, long
                          const float* w, float* dx, long long dx_nstride, float* wpart, float* bpart,
                          int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
   L3U_REQUIRE(l3u_convt_bwd_fused_nparts(N, Ci, Co, D, H, W) > 0 && dy && x && w && dx && wpart);
+  if (convt_tile_nparts(N, Ci, Co, D, H, W) > 0)   // the one-read tile kernel (convt.hip)
+    return convt_tile_launch<T>(dy, dy_nstride, x, x_nstride, w, dx, dx_nstride, wpart, bpart, N, Ci,
+                                Co, D, H, W, stream);
   const int S = D * H * W, J = Co * 8;
   const bool vec = W % 4 == 0 && S % 4 == 0 && dy_nstride % 4 == 0 && x_nstride % 4 == 0 &&
                    dx_nstride % 4 == 0 && al4<float>(dy) && al4<T>(x) && al4<float>(dx);
@@ -1788,6 +1791,8 @@ int l3u_pw_bwd_nparts(int N, int J, int K, int S) {
 // path is as fast (the gathered A-layout reads coalesce poorly at that volume) and at 6^3
 // (W % 4 != 0: scalar gathers) it is faster.
 int l3u_convt_bwd_fused_nparts(int N, int Ci, int Co, int D, int H, int W) {
+  const int nt = convt_tile_nparts(N, Ci, Co, D, H, W);
+  if (nt > 0) return nt;
   if (!(N > 0 && Ci > 0 && (Co == 8 || Co == 16 || Co == 32 || Co == 64) && D > 0 && H > 0 && W > 0))
     return 0;
   if ((!L3U_CONVT_ONEPASS_ANYW && W % 4 != 0) || D * H * W > L3U_CONVT_ONEPASS_MAX_S) return 0;

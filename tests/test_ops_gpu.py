@@ -734,7 +734,12 @@ def test_outconv_ftl_fused(cuda, case):
 # (N, Ci, Co, D, H, W): the network's three up-blocks (low-res volumes) plus ragged ones
 CONVT_ONEPASS = [(2, 32, 16, 8, 8, 8), (2, 64, 32, 6, 6, 8), (1, 128, 64, 3, 3, 4),
                  (2, 24, 8, 5, 6, 4), (4, 64, 32, 12, 12, 12), (2, 16, 8, 4, 4, 12),
-                 (1, 128, 64, 16, 16, 16)]   # config 5's 16^3 -> 32^3: two tiles per workgroup
+                 (1, 128, 64, 16, 16, 16),   # config 5's 16^3 -> 32^3: two tiles per workgroup
+                 # the one-read tile kernel (Co 16 / 32): the model's 24^3 up3 (two tiles per
+                 # workgroup), ragged volumes (a tile past the end), 16 / 32 / 64-channel blocks,
+                 # config 5's 32^3 up3 (four tiles per workgroup)
+                 (4, 32, 16, 24, 24, 24), (2, 64, 32, 5, 6, 6), (1, 16, 16, 5, 4, 6),
+                 (2, 32, 32, 7, 5, 4), (1, 64, 32, 32, 32, 32)]
 
 
 @pytest.mark.parametrize("case", CONVT_ONEPASS)
@@ -757,7 +762,7 @@ def test_convt_bwd_onepass(cuda, case):
     xd, wd = x.float().to(cuda), w.float().to(cuda)
     dx = torch.full((N, Ci, Si), float("nan"), device=cuda)
     P = nat().query("l3u_convt_bwd_fused_nparts", N, Ci, Co, D, H, W)
-    assert 0 < P <= N * ((Si + 63) // 64)   # one partial per workgroup of 64-voxel tiles
+    assert 0 < P <= N * ((Si + 31) // 32)   # one partial per workgroup of >= 32-voxel tiles
     wp = torch.full((P * Ci * Co * 8,), float("nan"), device=cuda)
     bp = torch.full((P * Co,), float("nan"), device=cuda)
     nat().call("l3u_convt_bwd_fused", dcat.data_ptr(), 2 * Co * So, xd.data_ptr(), Ci * Si,

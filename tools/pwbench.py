@@ -123,14 +123,15 @@ def main():
 
 def convt(iters):
     dev = torch.device("cuda:0")
-    for (N, Ci, Co, L) in [(4, 32, 16, 24), (4, 64, 32, 12), (4, 128, 64, 6)]:
+    for (N, Ci, Co, L) in [(4, 32, 16, 24), (4, 64, 32, 12), (4, 128, 64, 6), (4, 64, 32, 32),
+                           (4, 128, 64, 16)]:
         Si = L ** 3
         dcat = torch.randn(N, 2 * Co, 8 * Si, device=dev)
         x = torch.randn(N, Ci, Si, device=dev)
         w = torch.randn(Ci, Co * 8, device=dev)
         dx = torch.empty(N, Ci, Si, device=dev)
-        P = N * ((Si + 63) // 64)
-        if nat.query("l3u_convt_bwd_fused_nparts", N, Ci, Co, L, L, L) == 0:
+        P = nat.query("l3u_convt_bwd_fused_nparts", N, Ci, Co, L, L, L)
+        if P == 0:
             print(f"convT bwd Ci{Ci} Co{Co} {L}^3: one-launch form not offered")
             continue
         wp, bp = torch.empty(P * Ci * Co * 8, device=dev), torch.empty(P * Co, device=dev)
@@ -148,8 +149,10 @@ def convt(iters):
                      w.data_ptr(), dx.data_ptr(), Ci * Si, wp2.data_ptr(), bp2.data_ptr(), N, Ci, Co,
                      L, L, L, torch.cuda.current_stream().cuda_stream)
 
-        print(f"convT bwd Ci{Ci} Co{Co} {L}^3: one launch {graph_time(fused, iters):7.2f} us  "
-              f"three launches {graph_time(unfused, iters):7.2f} us", flush=True)
+        tf, tu = graph_time(fused, iters), graph_time(unfused, iters)
+        byt = 4 * N * Si * (8 * Co + 2 * Ci)   # dY + X + dX (algorithmic)
+        print(f"convT bwd Ci{Ci} Co{Co} {L}^3: one launch {tf:7.2f} us ({byt / tf / 1e3:6.0f} GB/s, "
+              f"{P} partials)  three launches {tu:7.2f} us", flush=True)
 
 
 if __name__ == "__main__":
