@@ -397,6 +397,18 @@ int l3u_ccl_stats(int* label, const int* remap, const float* prob, unsigned long
                   int ncomp, int D, int H, int W, hipStream_t stream);
 int l3u_ccl_pairs(const int* label_a, const int* label_b, int nb, unsigned int* inter, long long n,
                   hipStream_t stream);
+/* The batched forms (get_connected_components / match_components / calculate_lesion_metrics on a
+ * [B, D, H, W] array, metrics.py:38-63,99-124): ndimage.label's default structure in 4 dims adds
+ * the batch axis as a fourth face neighbour (voxel (b, z, y, x) touches (b - 1, z, y, x)), with the
+ * same C-order numbering over the whole array; workspace and label sized B*D*H*W.  l3u_ccl_stats_b
+ * records the array's three LEADING coordinates: (z, y, x) with lead4 = 0 (a 3-dimensional array,
+ * B = 1) and (b, z, y) with lead4 = 1 (a 4-dimensional array, any B) -- the reference keeps the
+ * first three of center_of_mass's coordinates whatever the rank.  l3u_ccl_label / l3u_ccl_stats
+ * are the B = 1, lead4 = 0 forms. */
+int l3u_ccl_label_b(const float* src, float threshold, int* parent, int* label, int* chunk_count,
+                    int B, int D, int H, int W, hipStream_t stream);
+int l3u_ccl_stats_b(int* label, const int* remap, const float* prob, unsigned long long* stats,
+                    int ncomp, int B, int D, int H, int W, int lead4, hipStream_t stream);
 
 /* ---- UpBlock pad / crop (light_unet/models/unet3d.py:130-138) -----------------------------
  * dst[n][c][z][y][x] = src[n][c][z-oz][y-oy][x-ox] inside src's (sd, sh, sw) box, 0 elsewhere,

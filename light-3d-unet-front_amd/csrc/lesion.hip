@@ -1,7 +1,11 @@
-// Lesion post-processing on the device: 3D connected-component labelling and per-component
+// Lesion post-processing on the device: connected-component labelling and per-component
 // statistics.  Replaces the host scipy/numpy work of
-//   light_unet/models/metrics.py:38-63   get_connected_components (ndimage.label, 6-connectivity,
-//                                        the default structure for 3 dims; min_size filter + relabel)
+//   light_unet/models/metrics.py:38-63   get_connected_components (ndimage.label with its default
+//                                        structure: face connectivity in every dimension of the
+//                                        array -- 6 neighbours for a [D, H, W] volume, 8 for a
+//                                        batched [B, D, H, W] array, where the same voxel of
+//                                        consecutive batch items is connected; min_size filter +
+//                                        relabel)
 //   light_unet/models/metrics.py:107-213 component centres of mass, pairwise overlap (IoU) counts
 //   light_unet/core/inferencer.py:62-111 bounding boxes, volumes and peak probability per component
 // (host-bound with real volumes).  Integer work, bit-exact:
@@ -48,15 +52,19 @@ L3U_DEV void uf_union(int* parent, int a, int b) {
   }
 }
 
-__global__ __launch_bounds__(256) void ccl_merge_kernel(int* __restrict__ parent, int D, int H,
+// face neighbours of [B][D][H][W]: x, y, z within an item and b (the same voxel of the previous
+// item, offset S = D*H*W) -- ndimage.label's default structure for a 4-dimensional array
+__global__ __launch_bounds__(256) void ccl_merge_kernel(int* __restrict__ parent, int B, int D, int H,
                                                         int W) {
-  const long long n = (long long)D * H * W, HW = (long long)H * W;
+  const long long S = (long long)D * H * W, n = B * S, HW = (long long)H * W;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     if (parent[i] < 0) continue;
-    const int x = (int)(i % W), y = (int)((i / W) % H), z = (int)(i / HW);
+    const long long r = i % S;
+    const int x = (int)(r % W), y = (int)((r / W) % H), z = (int)(r / HW);
     if (x > 0 && parent[i - 1] >= 0) uf_union(parent, (int)i, (int)(i - 1));
     if (y > 0 && parent[i - W] >= 0) uf_union(parent, (int)i, (int)(i - W));
     if (z > 0 && parent[i - HW] >= 0) uf_union(parent, (int)i, (int)(i - HW));
+    if (i >= S && parent[i - S] >= 0) uf_union(parent, (int)i, (int)(i - S));
   }
 }
 
@@ -136,15 +144,18 @@ __global__ __launch_bounds__(256) void ccl_label_kernel(const int* __restrict__ 
   }
 }
 
-// per component l (1-based): stats[(l-1)*12 + k], k = 0 size, 1..3 sum of z, y, x, 4..6 min z, y,
-// x, 7..9 max z, y, x, 10 max prob (float bits; prob >= 0).  remap (optional) renumbers the
-// labels in place first (0 drops the voxel).
+// per component l (1-based): stats[(l-1)*12 + k], k = 0 size, 1..3 sum of the three leading
+// coordinates (c0, c1, c2), 4..6 their minima, 7..9 their maxima, 10 max prob (float bits;
+// prob >= 0).  The leading coordinates are (z, y, x) of a 3-dimensional array and (b, z, y) of a
+// 4-dimensional one (lead4): the reference keeps the first three of ndimage.center_of_mass's
+// coordinates whatever the rank (metrics.py:99-124).  remap (optional) renumbers the labels in
+// place first (0 drops the voxel).
 __global__ __launch_bounds__(256) void ccl_stats_kernel(int* __restrict__ label,
                                                         const int* __restrict__ remap,
                                                         const float* __restrict__ prob,
                                                         unsigned long long* __restrict__ stats,
-                                                        int D, int H, int W) {
-  const long long n = (long long)D * H * W, HW = (long long)H * W;
+                                                        int B, int D, int H, int W, int lead4) {
+  const long long S = (long long)D * H * W, n = B * S, HW = (long long)H * W;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     int l = label[i];
     if (l <= 0) continue;
@@ -153,18 +164,20 @@ __global__ __launch_bounds__(256) void ccl_stats_kernel(int* __restrict__ label,
       label[i] = l;
       if (l <= 0) continue;
     }
-    const unsigned long long x = i % W, y = (i / W) % H, z = i / HW;
+    const long long r = i % S;
+    const unsigned long long x = r % W, y = (r / W) % H, z = r / HW, b = i / S;
+    const unsigned long long c0 = lead4 ? b : z, c1 = lead4 ? z : y, c2 = lead4 ? y : x;
     unsigned long long* s = stats + (long long)(l - 1) * 12;
     atomicAdd(s + 0, 1ull);
-    atomicAdd(s + 1, z);
-    atomicAdd(s + 2, y);
-    atomicAdd(s + 3, x);
-    atomicMin(s + 4, z);
-    atomicMin(s + 5, y);
-    atomicMin(s + 6, x);
-    atomicMax(s + 7, z);
-    atomicMax(s + 8, y);
-    atomicMax(s + 9, x);
+    atomicAdd(s + 1, c0);
+    atomicAdd(s + 2, c1);
+    atomicAdd(s + 3, c2);
+    atomicMin(s + 4, c0);
+    atomicMin(s + 5, c1);
+    atomicMin(s + 6, c2);
+    atomicMax(s + 7, c0);
+    atomicMax(s + 8, c1);
+    atomicMax(s + 9, c2);
     if (prob) atomicMax(s + 10, (unsigned long long)__float_as_uint(fmaxf(prob[i], 0.f)));
   }
 }
@@ -199,15 +212,15 @@ extern "C" {
 
 int l3u_ccl_nchunks(long long n) { return (int)((n + kCh - 1) / kCh); }
 
-int l3u_ccl_label(const float* src, float threshold, int* parent, int* label, int* chunk_count,
-                  int D, int H, int W, hipStream_t stream) {
-  L3U_REQUIRE(src && parent && label && chunk_count && D > 0 && H > 0 && W > 0);
-  const long long n = (long long)D * H * W;
+int l3u_ccl_label_b(const float* src, float threshold, int* parent, int* label, int* chunk_count,
+                    int B, int D, int H, int W, hipStream_t stream) {
+  L3U_REQUIRE(src && parent && label && chunk_count && B > 0 && D > 0 && H > 0 && W > 0);
+  const long long n = (long long)B * D * H * W;
   L3U_REQUIRE(n < (1ll << 31));
   const int nb = l3u_ccl_nchunks(n);
   hipLaunchKernelGGL(ccl_init_kernel, dim3(blocks_for(n)), dim3(256), 0, stream, src, threshold,
                      parent, n);
-  hipLaunchKernelGGL(ccl_merge_kernel, dim3(blocks_for(n)), dim3(256), 0, stream, parent, D, H, W);
+  hipLaunchKernelGGL(ccl_merge_kernel, dim3(blocks_for(n)), dim3(256), 0, stream, parent, B, D, H, W);
   hipLaunchKernelGGL(ccl_flatten_kernel, dim3(nb), dim3(256), 0, stream, parent, n, chunk_count);
   hipLaunchKernelGGL(ccl_scan_kernel, dim3(1), dim3(256), 0, stream, chunk_count, nb);
   hipLaunchKernelGGL(ccl_root_label_kernel, dim3(nb), dim3(256), 0, stream, parent, n, chunk_count,
@@ -216,15 +229,26 @@ int l3u_ccl_label(const float* src, float threshold, int* parent, int* label, in
   L3U_CHECK_LAUNCH();
 }
 
-int l3u_ccl_stats(int* label, const int* remap, const float* prob, unsigned long long* stats,
-                  int ncomp, int D, int H, int W, hipStream_t stream) {
-  L3U_REQUIRE(label && stats && ncomp > 0 && D > 0 && H > 0 && W > 0);
-  const long long n = (long long)D * H * W;
+int l3u_ccl_label(const float* src, float threshold, int* parent, int* label, int* chunk_count,
+                  int D, int H, int W, hipStream_t stream) {
+  return l3u_ccl_label_b(src, threshold, parent, label, chunk_count, 1, D, H, W, stream);
+}
+
+int l3u_ccl_stats_b(int* label, const int* remap, const float* prob, unsigned long long* stats,
+                    int ncomp, int B, int D, int H, int W, int lead4, hipStream_t stream) {
+  L3U_REQUIRE(label && stats && ncomp > 0 && B > 0 && D > 0 && H > 0 && W > 0);
+  L3U_REQUIRE(lead4 == 0 ? B == 1 : lead4 == 1);
+  const long long n = (long long)B * D * H * W;
   hipLaunchKernelGGL(ccl_stats_init_kernel, dim3(blocks_for(ncomp * 12ll)), dim3(256), 0, stream,
                      stats, ncomp);
   hipLaunchKernelGGL(ccl_stats_kernel, dim3(blocks_for(n)), dim3(256), 0, stream, label, remap,
-                     prob, stats, D, H, W);
+                     prob, stats, B, D, H, W, lead4);
   L3U_CHECK_LAUNCH();
+}
+
+int l3u_ccl_stats(int* label, const int* remap, const float* prob, unsigned long long* stats,
+                  int ncomp, int D, int H, int W, hipStream_t stream) {
+  return l3u_ccl_stats_b(label, remap, prob, stats, ncomp, 1, D, H, W, 0, stream);
 }
 
 int l3u_ccl_pairs(const int* label_a, const int* label_b, int nb, unsigned int* inter, long long n,

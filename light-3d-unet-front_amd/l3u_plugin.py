@@ -57,23 +57,6 @@ LESION = ("get_connected_components", "match_components", "calculate_lesion_metr
           "calculate_metrics")
 
 
-def _lesion_entry(device_fn, reference_fn, batched_error):
-    """The device function, except for inputs it does not define: batched [B, D, H, W] volumes
-    (B > 1), which scipy.ndimage.label connects across the batch axis (4D connectivity), go to
-    the reference's own host function unchanged (the device kernels label 3D volumes)."""
-    reference_fn = getattr(reference_fn, "_l3u_reference", reference_fn)   # install() twice
-
-    def entry(*args, **kwargs):
-        try:
-            return device_fn(*args, **kwargs)
-        except batched_error:
-            return reference_fn(*args, **kwargs)
-    entry.__name__, entry.__doc__ = device_fn.__name__, device_fn.__doc__
-    entry.__module__, entry.__wrapped__ = device_fn.__module__, device_fn
-    entry._l3u_reference = reference_fn
-    return entry
-
-
 def _bind_lesion(done):
     """The device lesion post-processing (light_unet/lesion.py) into the reference's metrics
     module (metrics.py:38-404) and into the modules that imported those names already
@@ -86,8 +69,10 @@ def _bind_lesion(done):
     except ImportError:
         return
     names = [n for n in LESION if hasattr(metrics, n)]
-    bound = {n: _lesion_entry(getattr(les, n), getattr(metrics, n), les.BatchedVolumeError)
-             for n in names}
+    # every input form the reference functions take -- [D, H, W] volumes and batched
+    # [B, D, H, W] arrays (labelled as one 4-dimensional array, as ndimage.label does) -- runs on
+    # the device (csrc/lesion.hip); nothing is handed back to the host functions
+    bound = {n: getattr(les, n) for n in names}
     for n in names:
         setattr(metrics, n, bound[n])
     done["light_unet.models.metrics"] = names

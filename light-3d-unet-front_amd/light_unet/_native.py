@@ -84,6 +84,8 @@ _SIGS = {
     "l3u_ccl_label": [P, F, P, P, P, I, I, I, P],
     "l3u_ccl_stats": [P, P, P, P, I, I, I, I, P],
     "l3u_ccl_pairs": [P, P, I, P, L, P],
+    "l3u_ccl_label_b": [P, F, P, P, P, I, I, I, I, P],
+    "l3u_ccl_stats_b": [P, P, P, P, I, I, I, I, I, I, P],
     "l3u_cast_bf16_f32": [P, P, L, P],
     "l3u_outconv_bwd_dz": [P, P, P, P, D, D, D, D, P, P, L, P, P, L, P, P, I, I, I, P],
     "l3u_outconv_bwd_ftl_dz": [P, P, P, I, D, D, D, D, P, P, L, P, P, L, P, P, I, I, I, P],

@@ -33,40 +33,28 @@ def _device():
     return torch.device("cuda", torch.cuda.current_device())
 
 
-class BatchedVolumeError(ValueError):
-    """A labelled or thresholded input with more than three non-unit axes ([B, D, H, W], B > 1).
-    scipy.ndimage.label connects such arrays across the leading axis (4D connectivity); the
-    device kernels label 3D volumes only, so l3u_plugin hands these calls back to the reference's
-    own host function (the contract of this module is 3D)."""
+def _dims(shape):
+    """(B, D, H, W, lead4) of a labelled / thresholded array, in ndimage.label's own terms: a
+    [D, H, W] volume (B = 1, coordinates z, y, x) or a [B, D, H, W] array labelled as ONE
+    4-dimensional array (the batch axis is a fourth face neighbour; the reference's centres keep
+    the leading coordinates b, z, y, metrics.py:99-124).  Other ranks are not taken."""
+    shape = tuple(int(v) for v in shape)
+    if len(shape) == 3:
+        return (1,) + shape + (0,)
+    if len(shape) == 4:
+        return shape + (1,)
+    raise ValueError(f"expected a [D, H, W] volume or a [B, D, H, W] array, got shape {shape}")
 
 
 def _volume(a, dev, keep_f64=False):
-    """[D, H, W] float32 on the device from a numpy array / tensor ([1, D, H, W] accepted).
-    keep_f64: a float64 input stays float64 (the reference thresholds float64 maps in float64)."""
+    """The array (3- or 4-dimensional, shape kept) as float32 on the device.  keep_f64: a float64
+    input stays float64 (the reference thresholds float64 maps in float64)."""
     t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(np.asarray(a)))
-    while t.dim() > 3 and t.shape[0] == 1:
-        t = t[0]
-    if t.dim() > 3:
-        raise BatchedVolumeError(f"expected a 3D volume [D, H, W], got shape {tuple(t.shape)}")
-    if t.dim() != 3:
-        raise ValueError(f"expected a 3D volume [D, H, W], got shape {tuple(t.shape)}")
+    _dims(t.shape)
     if t.dtype == torch.bool:
         t = t.to(torch.uint8)
     dt = torch.float64 if (keep_f64 and t.dtype == torch.float64) else torch.float32
     return t.to(device=dev, dtype=dt).contiguous()
-
-
-def _require_3d(*arrays):
-    """Raise BatchedVolumeError for an input with more than three non-unit leading axes, before
-    any device work (shape only)."""
-    for a in arrays:
-        if a is None or isinstance(a, Components):
-            continue
-        shape = tuple(a.shape) if hasattr(a, "shape") else np.shape(a)
-        while len(shape) > 3 and shape[0] == 1:
-            shape = shape[1:]
-        if len(shape) > 3:
-            raise BatchedVolumeError(f"expected a 3D volume [D, H, W], got shape {tuple(shape)}")
 
 
 def _foreground(vol, threshold, dev):
@@ -81,8 +69,8 @@ def _foreground(vol, threshold, dev):
 
 
 class Components:
-    """A labelling on the device: `labels` int32 [D, H, W], `num` components, `stats` uint64
-    [num, 12] (host) as l3u_ccl_stats writes them."""
+    """A labelling on the device: `labels` int32 (the input's [D, H, W] or [B, D, H, W] shape),
+    `num` components, `stats` uint64 [num, 12] (host) as l3u_ccl_stats_b writes them."""
 
     def __init__(self, labels, num, stats):
         self.labels, self.num, self.stats = labels, int(num), stats
@@ -92,7 +80,8 @@ class Components:
         return self.stats[:, _SIZE].astype(np.int64)
 
     def centers(self):
-        """Centres of mass in voxels, scipy.ndimage.center_of_mass's float64 sum / count."""
+        """Centres of mass in voxels, scipy.ndimage.center_of_mass's float64 sum / count (the
+        three leading coordinates of the array, as metrics.py:99-124 keeps them)."""
         if self.num == 0:
             return np.empty((0, 3), dtype=np.float64)
         return self.stats[:, _SUM].astype(np.float64) / self.stats[:, _SIZE:_SIZE + 1].astype(np.float64)
@@ -108,20 +97,20 @@ def label(vol, threshold=0.5, min_size=0, prob=None):
     per-component maximum lands in stats[:, 10] (float32 bits)."""
     dev = _device()
     v, threshold = _foreground(vol, threshold, dev)
-    D, H, W = v.shape
+    B, D, H, W, lead4 = _dims(v.shape)
     n = v.numel()
     st = nat.stream()
     parent = torch.empty(n, dtype=torch.int32, device=dev)
-    lab = torch.empty((D, H, W), dtype=torch.int32, device=dev)
+    lab = torch.empty(v.shape, dtype=torch.int32, device=dev)
     nch = nat.query("l3u_ccl_nchunks", n)
     cnt = torch.empty(nch + 1, dtype=torch.int32, device=dev)
-    nat.call("l3u_ccl_label", v.data_ptr(), float(threshold), parent.data_ptr(), lab.data_ptr(),
-             cnt.data_ptr(), D, H, W, st)
+    nat.call("l3u_ccl_label_b", v.data_ptr(), float(threshold), parent.data_ptr(), lab.data_ptr(),
+             cnt.data_ptr(), B, D, H, W, st)
     num = int(cnt[nch].item())
     if num == 0:
         return Components(lab, 0, np.zeros((0, 12), dtype=np.uint64))
     pv = _volume(prob, dev, keep_f64=True) if prob is not None else None
-    if pv is not None and tuple(pv.shape) != (D, H, W):
+    if pv is not None and tuple(pv.shape) != tuple(v.shape):
         raise ValueError("prob must have the labelled volume's shape")
     pv64 = None
     if pv is not None and pv.dtype == torch.float64:
@@ -129,8 +118,8 @@ def label(vol, threshold=0.5, min_size=0, prob=None):
         # (float(prob_map[component_mask].max()) in inferencer.py:98), taken below
         pv64, pv = pv, None
     stats = torch.empty(num * 12, dtype=torch.int64, device=dev)
-    nat.call("l3u_ccl_stats", lab.data_ptr(), None, pv.data_ptr() if pv is not None else None,
-             stats.data_ptr(), num, D, H, W, st)
+    nat.call("l3u_ccl_stats_b", lab.data_ptr(), None, pv.data_ptr() if pv is not None else None,
+             stats.data_ptr(), num, B, D, H, W, lead4, st)
     s = stats.view(num, 12).cpu().numpy().view(np.uint64)
     if min_size > 0:
         keep = s[:, _SIZE] >= min_size
@@ -141,12 +130,13 @@ def label(vol, threshold=0.5, min_size=0, prob=None):
             rm = torch.from_numpy(remap).to(dev)
             if num == 0:   # every component dropped: the remap pass only clears the labels
                 stats = torch.empty(12, dtype=torch.int64, device=dev)
-                nat.call("l3u_ccl_stats", lab.data_ptr(), rm.data_ptr(), None, stats.data_ptr(), 1,
-                         D, H, W, st)
+                nat.call("l3u_ccl_stats_b", lab.data_ptr(), rm.data_ptr(), None, stats.data_ptr(), 1,
+                         B, D, H, W, lead4, st)
                 return Components(lab, 0, np.zeros((0, 12), dtype=np.uint64))
             stats = torch.empty(num * 12, dtype=torch.int64, device=dev)
-            nat.call("l3u_ccl_stats", lab.data_ptr(), rm.data_ptr(),
-                     pv.data_ptr() if pv is not None else None, stats.data_ptr(), num, D, H, W, st)
+            nat.call("l3u_ccl_stats_b", lab.data_ptr(), rm.data_ptr(),
+                     pv.data_ptr() if pv is not None else None, stats.data_ptr(), num, B, D, H, W,
+                     lead4, st)
             s = stats.view(num, 12).cpu().numpy().view(np.uint64)
     c = Components(lab, num, s)
     if pv64 is not None:
@@ -157,8 +147,8 @@ def label(vol, threshold=0.5, min_size=0, prob=None):
 
 
 def get_connected_components(mask, min_size=0):
-    """metrics.py:38-63: (labeled int32 [D, H, W] numpy, num_components); foreground = mask != 0."""
-    _require_3d(mask)
+    """metrics.py:38-63: (labeled int32 numpy of the mask's shape, num_components); foreground =
+    mask != 0; a [B, D, H, W] mask is labelled as one 4-dimensional array, as ndimage.label does."""
     m = np.asarray(mask) if not isinstance(mask, torch.Tensor) else mask
     fg = (m != 0)
     c = label(fg.astype(np.float32) if isinstance(fg, np.ndarray) else fg.float(), 0.5, min_size)
@@ -171,17 +161,14 @@ def _as_components(lab_or_comp):
     dev = _device()
     t = lab_or_comp if isinstance(lab_or_comp, torch.Tensor) else torch.from_numpy(
         np.ascontiguousarray(np.asarray(lab_or_comp)))
-    while t.dim() > 3 and t.shape[0] == 1:
-        t = t[0]
-    if t.dim() != 3:
-        raise BatchedVolumeError(f"expected a labelled 3D volume [D, H, W], got shape {tuple(t.shape)}")
+    B, D, H, W, lead4 = _dims(t.shape)
     t = t.to(device=dev, dtype=torch.int32).contiguous()
     num = int(t.max().item()) if t.numel() else 0
     if num == 0:
         return Components(t, 0, np.zeros((0, 12), dtype=np.uint64))
-    D, H, W = t.shape
     stats = torch.empty(num * 12, dtype=torch.int64, device=dev)
-    nat.call("l3u_ccl_stats", t.data_ptr(), None, None, stats.data_ptr(), num, D, H, W, nat.stream())
+    nat.call("l3u_ccl_stats_b", t.data_ptr(), None, None, stats.data_ptr(), num, B, D, H, W, lead4,
+             nat.stream())
     return Components(t, num, stats.view(num, 12).cpu().numpy().view(np.uint64))
 
 
@@ -202,8 +189,7 @@ def _sizes0(c):
 def match_components(pred_labeled, target_labeled, iou_threshold=0.1, distance_threshold_mm=10.0,
                      spacing=(4.0, 4.0, 4.0)):
     """metrics.py:127-213: greedy matching of predicted to target components by IoU or centre
-    distance.  Labelled volumes (numpy / device) or Components."""
-    _require_3d(pred_labeled, target_labeled)
+    distance.  Labelled arrays (numpy / device, [D, H, W] or [B, D, H, W]) or Components."""
     pc, tc = _as_components(pred_labeled), _as_components(target_labeled)
     num_pred, num_target = pc.num, tc.num
     if num_pred == 0 or num_target == 0:
@@ -254,7 +240,6 @@ def calculate_lesion_metrics(pred, target, threshold=0.5, min_size_voxels=0, iou
                              distance_threshold_mm=10.0, spacing=(4.0, 4.0, 4.0)):
     """metrics.py:216-287: lesion-wise recall / precision / f1 and tp / fp / fn counts."""
     pred, target = _squeeze(pred), _squeeze(target)
-    _require_3d(pred, target)
     pc = label(pred, threshold, min_size_voxels)
     tc = label(target, 0.5, min_size_voxels)
     if tc.num == 0:
@@ -275,8 +260,9 @@ def calculate_metrics(predictions, labels, threshold=0.5, spacing=(4.0, 4.0, 4.0
     voxel counts come from the same device labelling (foreground sizes and overlaps)."""
     pred_list, label_list = _case_list(predictions, "predictions"), _case_list(labels, "labels")
     spacings = _spacing_per_case(spacing, len(pred_list))
-    for pred, target in zip(pred_list, label_list):
-        _require_3d(_squeeze(np.asarray(pred)), _squeeze(np.asarray(target)))
+    for pred, target in zip(pred_list, label_list):   # shapes first: no device work on a bad list
+        _dims(_squeeze(np.asarray(pred)).shape)
+        _dims(_squeeze(np.asarray(target)).shape)
     smooth = 1e-6
     tot_tp = tot_fp = tot_fn = 0
     inter_sum = union_sum = 0.0
@@ -343,6 +329,8 @@ def extract_bboxes(prob_map, threshold=0.3, min_volume_cc=0.5, spacing=(4.0, 4.0
     ceil(min_volume_cc / voxel cc) voxels, expanded and clipped to the volume."""
     pm = prob_map if isinstance(prob_map, torch.Tensor) else np.asarray(prob_map)
     shape = tuple(pm.shape)
+    if len(shape) != 3:
+        raise ValueError(f"extract_bboxes takes a [D, H, W] probability map, got shape {shape}")
     voxel_volume_cc = spacing[0] * spacing[1] * spacing[2] / 1000.0
     min_voxels = int(np.ceil(min_volume_cc / voxel_volume_cc))
     c = label(pm, threshold, min_voxels, prob=pm)

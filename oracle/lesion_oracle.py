@@ -3,11 +3,13 @@ oracle/__init__).  Checker for light_unet/lesion.py (HIP kernels csrc/lesion.hip
 
 Follows:
   get_connected_components   light_unet/models/metrics.py:38-63 — scipy.ndimage.label with its
-                             default 3-D structure (the 6 face neighbours), components numbered in
-                             the order of their first voxel in a C-order scan; min_size drops
-                             smaller components and relabels (:52-61)
-  match_components           metrics.py:127-213 (IoU matrix in float32, centres of mass in mm,
-                             greedy matching in predicted-component order)
+                             default structure for the array's rank (face neighbours: 6 for a
+                             [D, H, W] volume, 8 for a batched [B, D, H, W] array), components
+                             numbered in the order of their first voxel in a C-order scan;
+                             min_size drops smaller components and relabels (:52-61)
+  match_components           metrics.py:127-213 (IoU matrix in float32, centres of mass in mm --
+                             the three LEADING coordinates of the array, :99-124 -- greedy
+                             matching in predicted-component order)
   calculate_lesion_metrics   metrics.py:216-287
   bounding boxes             light_unet/core/inferencer.py:62-111
 The labelling is restated as min-label propagation over the face neighbours with pointer jumping
@@ -19,19 +21,20 @@ import numpy as np
 
 
 def label6(mask):
-    """(labels int32, n): 6-connected components of mask != 0, numbered by first voxel."""
+    """(labels int32, n): face-connected components of mask != 0 (any rank), numbered by first
+    voxel."""
     m = np.asarray(mask) != 0
     n_vox = m.size
     idx = np.arange(n_vox, dtype=np.int64).reshape(m.shape)
     lab = np.where(m, idx, n_vox)                      # background: a sentinel above every index
     while True:
         new = lab.copy()
-        for ax in range(3):
+        for ax in range(m.ndim):
             for sh in (1, -1):
                 nb = np.roll(lab, sh, axis=ax)
                 valid = np.roll(m, sh, axis=ax)
                 # np.roll wraps around: the wrapped slab is not a neighbour
-                sl = [slice(None)] * 3
+                sl = [slice(None)] * m.ndim
                 sl[ax] = slice(0, 1) if sh == 1 else slice(-1, None)
                 valid[tuple(sl)] = False
                 new = np.where(m & valid, np.minimum(new, nb), new)
@@ -61,9 +64,10 @@ def get_connected_components(mask, min_size=0):
 
 
 def centers(lab, n):
+    """Per-component centres of mass over the array's three leading coordinates."""
     if n == 0:
         return np.empty((0, 3), np.float64)
-    coords = np.indices(lab.shape).reshape(3, -1).astype(np.float64)
+    coords = np.indices(lab.shape).reshape(lab.ndim, -1).astype(np.float64)
     cnt = np.bincount(lab.ravel(), minlength=n + 1)[1:].astype(np.float64)
     return np.stack([np.bincount(lab.ravel(), weights=coords[d], minlength=n + 1)[1:] / cnt
                      for d in range(3)], axis=1)
@@ -93,8 +97,19 @@ def match_components(pl, tl, iou_threshold=0.1, distance_threshold_mm=10.0, spac
     return matches, [i for i in range(1, npred + 1) if i not in mp], [i for i in range(1, ntgt + 1) if not taken[i - 1]]
 
 
+def squeeze(a):
+    """metrics.py:236-244: [B, 1, D, H, W] -> [B, D, H, W]; [1, D, H, W] -> [D, H, W]."""
+    a = np.asarray(a)
+    if a.ndim == 5:
+        a = a[:, 0]
+    if a.ndim == 4 and a.shape[0] == 1:
+        a = a[0]
+    return a
+
+
 def lesion_metrics(pred, target, threshold=0.5, min_size_voxels=0, iou_threshold=0.1,
                    distance_threshold_mm=10.0, spacing=(4.0, 4.0, 4.0)):
+    pred, target = squeeze(pred), squeeze(target)
     pl, npred = get_connected_components(np.asarray(pred) >= threshold, min_size_voxels)
     tl, ntgt = get_connected_components(np.asarray(target) >= 0.5, min_size_voxels)
     if ntgt == 0:

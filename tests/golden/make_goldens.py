@@ -333,6 +333,47 @@ def lesion_goldens():
         rec[f"bb/{cid}/confidence"] = np.array(prob[cm].max())
     rec["bb/prob"] = prob
     rec["bb/boxes"] = np.array(boxes, dtype=np.int64).reshape(-1, 7)
+    # batched [B, D, H, W] arrays: ndimage.label labels them as ONE 4-dimensional array (the batch
+    # axis is a fourth face neighbour) and the centres keep the leading coordinates (b, z, y)
+    rb = np.random.default_rng(50)
+    m4 = rb.random((2, 12, 14, 16)) < 0.3
+    m4[1] |= m4[0] & (rb.random((12, 14, 16)) < 0.5)   # shared voxels join items across the batch
+    lab4, num4 = metrics.get_connected_components(m4.astype(np.int32))
+    rec["b4/cc/mask"] = m4
+    rec["b4/cc/labels"] = lab4.astype(np.int32)
+    rec["b4/cc/num"] = np.array(num4)
+    lab4m, num4m = metrics.get_connected_components(m4.astype(np.int32), min_size=5)
+    rec["b4/cc/labels_min5"] = lab4m.astype(np.int32)
+    rec["b4/cc/num_min5"] = np.array(num4m)
+    shape = (24, 20, 28)
+    preds, tgts = [], []
+    for k in range(2):
+        tcen = [[rb.uniform(0, s) for s in shape] for _ in range(6)]
+        hit = [[c + rb.uniform(-3, 3) for c in cc] for cc in tcen[:4]]
+        pcen = hit + [[rb.uniform(0, s) for s in shape] for _ in range(4)]
+        preds.append(_blobs(rb, shape, len(pcen), 3.5, pcen))
+        tgts.append((_blobs(rb, shape, len(tcen), 3.0, tcen) >= 0.5).astype(np.float32))
+    pred4, tgt4 = np.stack(preds)[:, None], np.stack(tgts)[:, None]   # [2, 1, D, H, W]
+    rec["b4/lm/pred"], rec["b4/lm/target"] = pred4, tgt4
+    for thr in (0.3, 0.5):
+        m = metrics.calculate_lesion_metrics(pred4, tgt4, threshold=thr, spacing=(4.0, 4.0, 4.0))
+        for k, v in m.items():
+            rec[f"b4/lm/thr{thr}/{k}"] = np.array(v)
+    m2 = metrics.calculate_lesion_metrics(pred4[:, 0], tgt4[:, 0], threshold=0.3, min_size_voxels=4,
+                                          iou_threshold=0.2, distance_threshold_mm=6.0,
+                                          spacing=(2.0, 3.0, 4.0))
+    for k, v in m2.items():
+        rec[f"b4/lm/opts/{k}"] = np.array(v)
+    pl4, _ = metrics.get_connected_components((pred4[:, 0] >= 0.3).astype(np.int32))
+    tl4, _ = metrics.get_connected_components((tgt4[:, 0] >= 0.5).astype(np.int32))
+    for nm, (a, b) in (("b2", (pl4, tl4)), ("b1", (pl4[:1], tl4[:1]))):   # b1: [1, D, H, W] arrays
+        mt, up, ut = metrics.match_components(a, b, 0.1, 10.0, (4.0, 4.0, 4.0))
+        rec[f"b4/match/{nm}/matches"] = np.array(mt, dtype=np.int64).reshape(-1, 2)
+        rec[f"b4/match/{nm}/unmatched_pred"] = np.array(up, dtype=np.int64)
+        rec[f"b4/match/{nm}/unmatched_target"] = np.array(ut, dtype=np.int64)
+    agg = metrics.calculate_metrics(pred4, tgt4, threshold=0.3)   # [B, 1, D, H, W]: one case per item
+    for k, v in agg.items():
+        rec[f"b4/agg/{k}"] = np.array(v)
     np.savez_compressed(os.path.join(OUT, "lesion.npz"), **rec)
     print("lesion.npz", len(rec), "arrays")
 

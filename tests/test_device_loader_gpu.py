@@ -11,9 +11,10 @@ num_workers=0).  Device side: the same factories after install().  Compared per 
 fl_epoch_plus_dlbcl, probabilistic): batch count and shapes (ragged last batch), images
 <= 1e-6, labels (nearest-neighbour ties) <= 1e-4 of the voxels, the RNG states after the epoch
 (numpy, python, torch), the mixed dataset's domain counts; and Trainer.train_epoch (the
-fast_step loop) consuming both loaders gives the same per-step losses.  The draw ORDER itself is
-restated from patch_dataset.py:114-220 (parity unpinned: the reference module cannot be
-imported here)."""
+fast_step loop) consuming both loaders gives the same per-step losses.  This test covers the
+install() plumbing against a stand-in package; the draw ORDER and the batches themselves are
+pinned to the reference's own loaders by tests/test_reference_loops_gpu.py (and, on CPU,
+tests/test_loops_oracle.py) over reference-generated fixtures (tests/golden/loops.npz)."""
 import os
 import subprocess
 import sys

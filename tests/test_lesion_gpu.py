@@ -47,6 +47,45 @@ def test_matching_and_metrics_match_reference(cuda, golden, i):
     assert list(ut) == z[f"lm/{i}/unmatched_target"].tolist()
 
 
+def test_batched_arrays_match_reference(cuda, golden):
+    """[B, D, H, W] inputs (no host fallback): one 4-dimensional labelling with the batch axis as
+    a fourth face neighbour, bit-exact labels / counts vs the reference's ndimage.label; lesion
+    metrics on [B, 1, D, H, W] maps and matching of batched and [1, D, H, W] labelled arrays with
+    the reference's (b, z, y) centres; calculate_metrics over a [B, 1, D, H, W] array."""
+    from light_unet import lesion
+    z = golden("lesion.npz")
+    lab, n = lesion.get_connected_components(z["b4/cc/mask"].astype(np.int32))
+    assert lab.shape == z["b4/cc/labels"].shape and n == int(z["b4/cc/num"])
+    assert np.array_equal(lab, z["b4/cc/labels"])
+    lab5, n5 = lesion.get_connected_components(z["b4/cc/mask"], min_size=5)
+    assert n5 == int(z["b4/cc/num_min5"]) and np.array_equal(lab5, z["b4/cc/labels_min5"])
+    pred, tgt = z["b4/lm/pred"], z["b4/lm/target"]
+    for thr in (0.3, 0.5):
+        for k, v in lesion.calculate_lesion_metrics(pred, tgt, threshold=thr).items():
+            assert v == z[f"b4/lm/thr{thr}/{k}"].item(), (thr, k)
+    m = lesion.calculate_lesion_metrics(pred[:, 0], tgt[:, 0], threshold=0.3, min_size_voxels=4,
+                                        iou_threshold=0.2, distance_threshold_mm=6.0,
+                                        spacing=(2.0, 3.0, 4.0))
+    for k, v in m.items():
+        assert v == z[f"b4/lm/opts/{k}"].item(), k
+    pl, _ = lesion.get_connected_components(pred[:, 0] >= 0.3)
+    tl, _ = lesion.get_connected_components(tgt[:, 0] >= 0.5)
+    for nm, (a, b) in (("b2", (pl, tl)), ("b1", (pl[:1], tl[:1]))):
+        mt, up, ut = lesion.match_components(a, b)
+        assert np.array_equal(np.array(mt, np.int64).reshape(-1, 2), z[f"b4/match/{nm}/matches"]), nm
+        assert list(up) == z[f"b4/match/{nm}/unmatched_pred"].tolist()
+        assert list(ut) == z[f"b4/match/{nm}/unmatched_target"].tolist()
+    agg = lesion.calculate_metrics(pred, tgt, threshold=0.3)
+    for k, v in agg.items():
+        assert v == z[f"b4/agg/{k}"].item(), k
+    # a larger batched array against the oracle (percolation-level density, 3 items)
+    rng = np.random.default_rng(3)
+    m4 = rng.random((3, 20, 24, 28)) < 0.3
+    lab, n = lesion.get_connected_components(m4)
+    labo, no = L.get_connected_components(m4)
+    assert n == no and np.array_equal(lab, labo)
+
+
 def test_calculate_metrics_matches_reference(cuda, golden):
     from light_unet import lesion
     z = golden("lesion.npz")
