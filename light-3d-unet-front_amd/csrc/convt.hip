@@ -250,9 +250,13 @@ static bool convt_tile_shape(int N, int Ci, int Co, int D, int H, int W, ConvtTi
   if (W % 2 != 0 || S % 4 != 0 || S > (1ll << 26)) return false;
   const int PP = D * H * (W / 2);
   // 16 input channels per block; 2 blocks per workgroup (up to 32 channels) with 32-pair tiles,
-  // 4 blocks with 16-pair tiles for the wider layers (same LDS footprint)
-  if (Ci % 64 == 0) { t.pb = 1; t.cib = 4; }
-  else if (Ci % 32 == 0) { t.pb = 2; t.cib = 2; }
+  // 4 blocks with 16-pair tiles for the wider layers (same LDS footprint) when the volume has
+  // tiles enough for several per workgroup; a small wide layer (the 12^3 up2) takes one block per
+  // workgroup over 64-pair tiles instead: the same time (tools/pwbench.py --convt-only, 12.5 vs
+  // 12.1 us) with a quarter of the weight-partial bytes (3.5 vs 14 MB at 12^3)
+  const int PP0 = D * H * (W / 2);
+  if (Ci % 64 == 0 && (long long)N * ((PP0 + 15) / 16) >= 1024) { t.pb = 1; t.cib = 4; }
+  else if (Ci % 32 == 0 && Ci % 64 != 0) { t.pb = 2; t.cib = 2; }
   else { t.pb = 4; t.cib = 1; }
   const int P = 16 * t.pb;
   t.ntile = (PP + P - 1) / P;

@@ -90,9 +90,9 @@ def test_host_queries_without_gpu():
         _native.query("l3u_pw_bwd_weight_nparts", 4, 48 ** 3)
     assert _native.query("l3u_pw_bwd_nparts", 4, 64, 128, 12 ** 3) == 4 * 27
     assert _native.query("l3u_pw_bwd_nparts", 4, 48, 32, 12 ** 3) == 0
-    # the one-read tile kernel: one partial per workgroup (12^3: 16-pair tiles, 24^3: 32-pair
+    # the one-read tile kernel: one partial per tile group (12^3: 64-pair tiles, 24^3: 32-pair
     # tiles, two per workgroup)
-    assert _native.query("l3u_convt_bwd_fused_nparts", 4, 64, 32, 12, 12, 12) == 4 * 54
+    assert _native.query("l3u_convt_bwd_fused_nparts", 4, 64, 32, 12, 12, 12) == 4 * 14
     assert _native.query("l3u_convt_bwd_fused_nparts", 4, 32, 16, 24, 24, 24) == 4 * 108
     assert _native.query("l3u_convt_bwd_fused_nparts", 4, 128, 64, 6, 6, 6) == 0
     assert _native.query("l3u_convt_bwd_fused_nparts", 4, 256, 128, 6, 6, 6) == 0
