@@ -1005,6 +1005,9 @@ def main():
                        "patch": [args.size] * 3, "dropout_p": args.dropout,
                        "ftl_mode": args.ftl_mode,
                        "parallelism": f"dp{world}" if world > 1 else "single",
+                       "collectives": (("captured in the step graph" if step.capture_collectives
+                                        else "eager between graph segments") if step.exchange
+                                       else None),
                        "graph": not args.no_graph},
             "fwd_ms_per_patch": {"bs1": round(fwd1, 4), f"bs{args.batch}": round(fwd4, 4)},
             "final_loss": round(final_loss, 6),

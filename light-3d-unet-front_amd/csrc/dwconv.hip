@@ -303,34 +303,12 @@ int pick_tz(int D) { return D <= 8 ? D : 4; }
 // 4-byte LDS reads.  Planes outside the volume are committed as zeros, so the stencil never
 // branches on z; input planes are staged through registers PD steps ahead of their use.
 // ------------------------------------------------------------------------------------------------
-// occupancy target (waves per SIMD; the IN-fused MODE 1 needs more registers and runs at 2) and
-// register prefetch depth of the quad backward kernel; dW taps as scalar or x-pair partial sums
-// (measured on MI355X, tools/kbench.py: scalar / 3 waves / depth 1 is the fastest at the model's
-// shapes)
-#ifndef L3U_DWB_WAVES
-#define L3U_DWB_WAVES 3
-#endif
-#ifndef L3U_DWB_PD
-#define L3U_DWB_PD 1
-#endif
-#ifndef L3U_GW_SCALAR
-#define L3U_GW_SCALAR 1
-#endif
-
-// register prefetch depth (planes in flight) of the quad forward stencil
-#ifndef L3U_DWQ_PD
-#define L3U_DWQ_PD 2
-#endif
-
-// TZ = 24 slabs for D % 24 == 0 (two slabs at 48^3): measured variant switch
-#ifndef L3U_TZ24
-#define L3U_TZ24 0
-#endif
-#if L3U_TZ24
-#define TZ24(X) if (g.TZ == 24) X; else
-#else
-#define TZ24(X)
-#endif
+// Tuning constants, each the fastest measured value (tools/kbench.py, step A/B; the rejected
+// alternatives are listed in profiles/NOTES.md):
+constexpr int kDwqPd = 2;          // register prefetch depth (planes in flight), quad forward stencil
+constexpr int kDwNwMin = 1;        // fewest waves per workgroup of the quad kernels
+constexpr int kTz16MinD = 48;      // 16-plane z slabs from this depth on
+constexpr int kDwMinBlocks = 1024; // thinner z slabs until the grid has this many workgroups
 
 struct QGeom {
   int WQ, RPW, NW, RB, ny, TZ, nz, threads;
@@ -343,12 +321,9 @@ QGeom qgeom(int N, int C, int D, int H, int W) {
   g.RPW = 64 / g.WQ;
   int best = 1;
   double beff = -1.0;
-#ifndef L3U_DW_NWMIN
-#define L3U_DW_NWMIN 1
-#endif
   for (int nw = 1; nw <= 4; ++nw) {
     if ((nw - 1) * g.RPW >= H) break;   // a wave with no row at all
-    if (nw < L3U_DW_NWMIN && nw * g.RPW < H) continue;
+    if (nw < kDwNwMin && nw * g.RPW < H) continue;
     const int rb = nw * g.RPW, ny = (H + rb - 1) / rb;
     const double eff = (double)H / (ny * rb);
     if (eff > beff + 1e-9) { beff = eff; best = nw; }
@@ -357,24 +332,12 @@ QGeom qgeom(int N, int C, int D, int H, int W) {
   g.RB = best * g.RPW;
   g.ny = (H + g.RB - 1) / g.RB;
   g.threads = 64 * best;
-#ifndef L3U_TZ16_MIN_D
-#define L3U_TZ16_MIN_D 48
-#endif
-  g.TZ = D >= L3U_TZ16_MIN_D ? 16 : (D >= 32 ? 8 : (D > 8 ? 4 : 8));   // compile-time in the kernels
-  if (L3U_TZ24 && D >= 48 && D % 24 == 0) g.TZ = 24;
-#ifndef L3U_DW_MIN_BLOCKS
-#define L3U_DW_MIN_BLOCKS 1024
-#endif
-  while (g.TZ != 24 && g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < L3U_DW_MIN_BLOCKS) g.TZ >>= 1;   // {16, 8, 4, 2}
+  g.TZ = D >= kTz16MinD ? 16 : (D >= 32 ? 8 : (D > 8 ? 4 : 8));   // compile-time in the kernels
+  while (g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < kDwMinBlocks) g.TZ >>= 1;   // {16, 8, 4, 2}
   g.nz = (D + g.TZ - 1) / g.TZ;
   return g;
 }
 
-#ifndef L3U_DW_SPLIT_MIN_PLANE
-#define L3U_DW_SPLIT_MIN_PLANE 0
-#endif
-// backward as two passes (data gradient, weight gradient) for planes of at least this size
-bool dw_split(int H, int W) { return H * W >= L3U_DW_SPLIT_MIN_PLANE; }
 
 bool use_quads(int H, int W) {
   if (W % 4 != 0 || W < 4 || W > 256 || H < 1) return false;
@@ -730,55 +693,32 @@ __global__ __launch_bounds__(256) void dw3q_dw_kernel(
 // skip the work that only touches planes outside the slab: per owned voxel the kernel issues
 // exactly the 27 + 27 tap products.
 // ------------------------------------------------------------------------------------------------
-#ifndef L3U_DWP_WAVES
-#define L3U_DWP_WAVES 3
-#endif
-#ifndef L3U_DWP_PD
-#define L3U_DWP_PD 2
-#endif
-#ifndef L3U_DWP_NT
-#define L3U_DWP_NT 1   // non-temporal dX stores in the LDS-DMA backward (kbench [4,32,48^3] 36.4 -> 35.6 us; step neutral)
-#endif
-#ifndef L3U_DWP_PIN
-#define L3U_DWP_PIN 1
-#endif
-#ifndef L3U_DW_FUSED
-#define L3U_DW_FUSED 1
-#endif
+// the single-pass backward: occupancy target and register prefetch depth of the register-staged
+// form; the LDS-DMA form's DMA ring depth and occupancy (the IN-fused MODE 1: 3 waves, 4 spill)
+constexpr int kDwpWaves = 3, kDwpPd = 2;
+constexpr int kDwgPd = 1, kDwgWaves = 4, kDwgWaves1 = 3;
 
 template <class F, int... I>
 L3U_DEV void run_steps(F& f, std::integer_sequence<int, I...>) {
   (f(std::integral_constant<int, I>{}), ...);
 }
 
-// LDS row image of the packed kernel: pitch W + 8 floats, x at offset 4, four zero floats on each
-// side (the conv's zero padding; never written after the initial clear).  A row read returns the
-// quad m = x..x+3 (ds_read_b128) and the aligned pairs n2 = (x-2, x-1), p2 = (x+4, x+5)
-// (ds_read_b64): the x-neighbours come from LDS with no lane exchange and no row-end selects.
-// L3U_DWP_LDSNB = 0 (default, measured faster): unpadded rows, the neighbours by DPP from the
-// adjacent lanes (one ds_read_b128 per row; ds_read2_b64 costs 8 LDS cycles vs 4 for b128, and
-// the LDS pipe also carries the ds_write_b128 commits at ~13 cycles each).
-#ifndef L3U_DWP_LDSNB
-#define L3U_DWP_LDSNB 0
-#endif
-constexpr int kLPad = L3U_DWP_LDSNB ? 8 : 0, kLOfs = L3U_DWP_LDSNB ? 4 : 0;
-constexpr int kNH = L3U_DWP_LDSNB ? 1 : 0;   // half of n2 holding x-1
+// LDS row image of the packed kernel: unpadded rows (pitch W), one ds_read_b128 per row quad, the
+// x-neighbours by DPP from the adjacent lanes (measured faster than a padded image read with
+// ds_read_b64 neighbour pairs: ds_read2_b64 costs 8 LDS cycles vs 4 for b128, and the LDS pipe
+// also carries the ds_write_b128 commits at ~13 cycles each)
+constexpr int kLPad = 0, kLOfs = 0;
+constexpr int kNH = 0;   // half of n2 holding x-1
 
 // row read: n2[kNH] = x-1, m = x..x+3, p2.x = x+4 (zero beyond the row)
 L3U_DEV void q_row3(const float* plane, int row, int lp, int ox, bool el, bool er, f2& n2, f4& m,
                     f2& p2) {
   const float* q = plane + row * lp + ox;
-#if L3U_DWP_LDSNB
-  n2 = *reinterpret_cast<const f2*>(q + kLOfs - 2);
-  m = *reinterpret_cast<const f4*>(q + kLOfs);
-  p2 = *reinterpret_cast<const f2*>(q + kLOfs + 4);
-#else
   m = *reinterpret_cast<const f4*>(q);
   const float pl = lane_prev(m[3]), pr = lane_next(m[0]);
   const float l = el ? 0.f : pl, r = er ? 0.f : pr;
   n2 = f2{l, l};
   p2 = f2{r, r};
-#endif
 }
 
 // the same from an already-read quad m0 (neighbours by DPP, or from LDS in the padded layout)
@@ -786,16 +726,10 @@ template <typename LT>
 L3U_DEV void q_nbr3(const f4& m0, const LT* plane, int row, int lp, int ox, bool el, bool er,
                     f2& n2, f4& m, f2& p2) {
   m = m0;
-#if L3U_DWP_LDSNB
-  const float* q = plane + row * lp + ox;
-  n2 = *reinterpret_cast<const f2*>(q + kLOfs - 2);
-  p2 = *reinterpret_cast<const f2*>(q + kLOfs + 4);
-#else
   const float pl = lane_prev(m[3]), pr = lane_next(m[0]);
   const float l = el ? 0.f : pl, r = er ? 0.f : pr;
   n2 = f2{l, l};
   p2 = f2{r, r};
-#endif
 }
 
 // acc + a * {b[H], b[H]}: the product with one half of an aligned register pair broadcast to both
@@ -808,24 +742,13 @@ L3U_DEV f2 pk_bc(f2 acc, f2 a, f2 b) {
 }
 // scalar FMAs kept scalar: left to the SLP vectorizer, neighbouring ones get packed with v_mov
 // pairing that costs more than it saves
-#ifndef L3U_DWP_ASMS
-#define L3U_DWP_ASMS 1
-#endif
 L3U_DEV float sfma_s(float acc, float a, float b) {   // a wave-uniform
-#if L3U_DWP_ASMS
   asm("v_fmac_f32 %0, %1, %2" : "+v"(acc) : "s"(a), "v"(b));
   return acc;
-#else
-  return fmaf(a, b, acc);
-#endif
 }
 L3U_DEV float sfma_v(float acc, float a, float b) {
-#if L3U_DWP_ASMS
   asm("v_fmac_f32 %0, %1, %2" : "+v"(acc) : "v"(a), "v"(b));
   return acc;
-#else
-  return fmaf(a, b, acc);
-#endif
 }
 template <int H>
 L3U_DEV f2 pk_bc_s(f2 acc, f2 a, f2 b) {   // a wave-uniform (SGPR pair)
@@ -841,21 +764,6 @@ L3U_DEV f2 pk_bc_s(f2 acc, f2 a, f2 b) {   // a wave-uniform (SGPR pair)
 // the tile (slot-1 tail) read a zero page instead, so every wave issues exactly 2 DMAs per
 // tensor per step and the waits are static counts.  The DMA is inline asm (M0 is written in the
 // same statement), so its completion is counted here, not by the compiler: see dw_wait_vm.
-#ifndef L3U_DWG
-#define L3U_DWG 1
-#endif
-#ifndef L3U_DWG_PD
-#define L3U_DWG_PD 1
-#endif
-#ifndef L3U_DWG_WAVES
-#define L3U_DWG_WAVES 4
-#endif
-#ifndef L3U_DWG_WAVES1
-#define L3U_DWG_WAVES1 3   // the IN-fused MODE 1 (measured: 3 > 4, which spills)
-#endif
-#ifndef L3U_DWG_MODE1
-#define L3U_DWG_MODE1 1    // MODE 1 on the LDS-DMA single pass (0: the split passes)
-#endif
 __device__ __attribute__((aligned(16))) float g_l3u_zero_page[256];   // 1 KiB of zeros (64 lanes x 16 B)
 
 L3U_DEV void glds16(const void* gsrc, unsigned lds_dst) {
@@ -884,7 +792,7 @@ L3U_DEV void dw_wait_vm() {   // at most NOUT vector-memory operations still out
 // slot per plane covers the 128-quad tile (needs an even quad count per row, W % 8 == 0, so a
 // lane's pair never straddles a row); that LDS image is bf16 and its rows widen at the read.
 template <typename T, int MODE, int TZC, bool GL = false, bool XR1 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE == 1 ? L3U_DWG_WAVES1 : L3U_DWG_WAVES) : L3U_DWP_WAVES))) void dw3p_bwd_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE == 1 ? kDwgWaves1 : kDwgWaves) : kDwpWaves))) void dw3p_bwd_kernel(
     const float* __restrict__ dz, long long dzns, const T* __restrict__ x, long long xns,
     const float* __restrict__ w, const float* __restrict__ rec, float* __restrict__ dx,
     long long dxns, float* __restrict__ dw_part, double* __restrict__ in_part,
@@ -903,7 +811,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
   const float* dzp = dz + (long long)b.n * dzns + cofs;
   const T* xp = x + (long long)b.n * (xk ? -xns : xns) + (xk ? 0ll : cofs);
   float* dxp = dx + (long long)b.n * dxns + cofs;
-  constexpr int GNB = L3U_DWG_PD + 1;                  // DMA ring buffers per tensor
+  constexpr int GNB = kDwgPd + 1;                  // DMA ring buffers per tensor
   const int GPSD = (RB + 2) * W;                       // dZ elements per ring buffer (nq quads)
   const int GPSA = BH ? 512 : (RB + 2) * W;            // A elements per ring buffer
   float* const dzl = lds;                              // dZ planes
@@ -938,7 +846,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
   const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
   const long long qofs = (long long)(b.y0 + b.oy) * W + b.ox;
   // register staging PD planes ahead (sets alternate by step parity when PD = 2)
-  constexpr int PD = GL ? 1 : L3U_DWP_PD;
+  constexpr int PD = GL ? 1 : kDwpPd;
   QPre<float> pzs[PD];
   QPre<T> pas[PD];
   const QMap qm = q_map(b.y0, b.rows, H, W, WQ, LP, kLOfs);
@@ -984,7 +892,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
     }
   };
   if constexpr (GL) {
-    run_steps(gissue, std::make_integer_sequence<int, L3U_DWG_PD>{});
+    run_steps(gissue, std::make_integer_sequence<int, kDwgPd>{});
   } else {
 #pragma unroll
     for (int k = 0; k < PD; ++k) {
@@ -1011,8 +919,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
       // issue plane s + PD (its ring buffer was last read in step s - 1), then wait for plane s:
       // younger than plane s's 4 DMAs are those of planes s+1 .. s+PD (stores between them only
       // make the wait longer)
-      if constexpr (s + L3U_DWG_PD < TZC + 3) gissue(std::integral_constant<int, s + L3U_DWG_PD>{});
-      dw_wait_vm<gl_younger<TZC, L3U_DWG_PD, 2, NSA>(s)>();
+      if constexpr (s + kDwgPd < TZC + 3) gissue(std::integral_constant<int, s + kDwgPd>{});
+      dw_wait_vm<gl_younger<TZC, kDwgPd, 2, NSA>(s)>();
     } else {
       q_commit<false>(pz, dbuf, qm, in_rng(zd), 1.f, 0.f, 0.f);
       q_commit<MODE == 1>(pa, (float*)abuf, qm, in_rng(za), sc, mean, sh);
@@ -1140,11 +1048,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
       }
       if (st) {
         float* dst = dxp + (long long)zf * HW + qofs;
-        if (GL && L3U_DWP_NT) stv4_nt(dst, o);   // streamed out, not re-read
+        if (GL) stv4_nt(dst, o);   // streamed out, not re-read (non-temporal: -0.8 us at [4,32,48^3])
         else stv4(dst, o);
       }
     }
-#if L3U_DWP_PIN
     // keep each step's accumulation inside the step (no sinking of FMAs past later barriers)
 #pragma unroll
     for (int t = 0; t < 9; ++t) { pin(GA[t]); pin(GB[t]); }
@@ -1153,7 +1060,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
     pin(S01);
     pin(S23);
     if constexpr (MODE == 1 && fin) { pin(s1); pin(s2); }   // else the IN sums sink to the end
-#endif
     P[0] = f2{P[0].y, S01.x};
     P[1] = f2{P[1].y, S01.y};
     P[2] = f2{P[2].y, S23.x};
@@ -1203,19 +1109,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
 // one barrier instead of a chain of plane steps: these volumes are latency-, not
 // bandwidth-bound.  nchunk = 1 (one partial per (n, c)).
 // ------------------------------------------------------------------------------------------------
-#ifndef L3U_VOL_MAX
-#define L3U_VOL_MAX 600   // measured: the 6^3 level gains, at 12^3 the plane kernels are faster
-#endif
-bool use_volume(int D, int H, int W) { return (long long)(D + 2) * (H + 2) * (W + 2) <= L3U_VOL_MAX; }
-#ifndef L3U_DWV_FUSED
-#define L3U_DWV_FUSED 1   // whole-volume backward as one launch (data + weight gradient)
-#endif
+constexpr int kVolMax = 600;   // measured: the 6^3 level gains, at 12^3 the plane kernels are faster
+bool use_volume(int D, int H, int W) { return (long long)(D + 2) * (H + 2) * (W + 2) <= kVolMax; }
 
 // The padded LDS image of volume `src` (transformed if XF; the halo is zero) for the 256-thread
-// whole-volume kernels (padded volume <= L3U_VOL_MAX), in two phases: v_fetch issues every load
+// whole-volume kernels (padded volume <= kVolMax), in two phases: v_fetch issues every load
 // of the thread's slots at once (raw values; it does not wait on the InstanceNorm record, so it
 // goes before the record merge), v_put transforms and writes them.
-constexpr int kVR = (L3U_VOL_MAX + 255) / 256;
+constexpr int kVR = (kVolMax + 255) / 256;
 template <typename T>
 L3U_DEV void v_fetch(float (&raw)[kVR], const T* __restrict__ src, int D, int H, int W) {
   const int PW = W + 2, PH = H + 2, PV = (D + 2) * PH * PW;
@@ -1439,7 +1340,7 @@ namespace {
 
 // the LDS-DMA single-pass backward takes one-wave tiles of <= 128 quads; bf16 moves quad pairs
 bool dw_gl(const QGeom& g, int W, int esize) {
-  return L3U_DWG && g.threads == 64 && (g.RB + 2) * g.WQ <= 128 && g.WQ * 4 == W &&
+  return g.threads == 64 && (g.RB + 2) * g.WQ <= 128 && g.WQ * 4 == W &&
          (esize == 4 || g.WQ % 2 == 0);
 }
 
@@ -1464,11 +1365,11 @@ int dw3_fwd_impl(const T* x, long long x_nstride, const float* w, const float* r
     size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
     if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);   // reduction scratch
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
-#define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<T, T, M_, 0, T_, L3U_DWQ_PD>), grid, block, lds, stream, x, \
+#define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<T, T, M_, 0, T_, kDwqPd>), grid, block, lds, stream, x, \
       x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W, g.RB, g.RPW, \
       g.ny, g.TZ, g.nz)
-    if (xf) { TZ24(DWQF(1, 24)) if (g.TZ == 16) DWQF(1, 16); else if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
-    else { TZ24(DWQF(0, 24)) if (g.TZ == 16) DWQF(0, 16); else if (g.TZ == 8) DWQF(0, 8); else if (g.TZ == 4) DWQF(0, 4); else DWQF(0, 2); }
+    if (xf) { if (g.TZ == 16) DWQF(1, 16); else if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
+    else { if (g.TZ == 16) DWQF(0, 16); else if (g.TZ == 8) DWQF(0, 8); else if (g.TZ == 4) DWQF(0, 4); else DWQF(0, 2); }
 #undef DWQF
     L3U_CHECK_LAUNCH();
   }
@@ -1496,7 +1397,7 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
   // a rank-1 input (x_nstride < 0) is taken by the fp32 LDS-DMA single pass with rec only
   const bool xr1 = x_nstride < 0;
   L3U_REQUIRE(!xr1 || (E == 4 && rec != nullptr && !use_volume(D, H, W) && use_quads(H, W) &&
-                       dw_gl(qgeom(N, C, D, H, W), W, E) && L3U_DW_FUSED && L3U_DWG_MODE1));
+                       dw_gl(qgeom(N, C, D, H, W), W, E)));
   if (use_volume(D, H, W)) {   // data + weight gradient in one launch
     size_t lds2 = 2 * (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
     if (lds2 < 160 * sizeof(float)) lds2 = 160 * sizeof(float);
@@ -1513,24 +1414,24 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
     const bool gl = dw_gl(g, W, E);
     // MODE 1 (IN-fused) only on the LDS-DMA variant: register-staged it measured faster split
-    if (L3U_DW_FUSED && (rec == nullptr || (gl && L3U_DWG_MODE1))) {
+    if (rec == nullptr || gl) {
       // single pass: data + weight gradient from one read of dZ and A
       size_t lds = 4 * (size_t)(g.RB + 2) * (W + kLPad) * sizeof(float);
       if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch
-      if (gl) lds = (L3U_DWG_PD + 1) * ((size_t)(g.RB + 2) * g.WQ * 16 + (E == 4 ? (size_t)(g.RB + 2) * g.WQ * 16 : 1024));
+      if (gl) lds = (kDwgPd + 1) * ((size_t)(g.RB + 2) * g.WQ * 16 + (E == 4 ? (size_t)(g.RB + 2) * g.WQ * 16 : 1024));
 #define DWPB(M_, T_) do { if (gl) hipLaunchKernelGGL((dw3p_bwd_kernel<T, M_, T_, true>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
       g.RPW, g.ny, g.TZ, g.nz); \
       else hipLaunchKernelGGL((dw3p_bwd_kernel<T, M_, T_>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
       g.RPW, g.ny, g.TZ, g.nz); } while (0)
-#define DWPB_T(M_) do { TZ24(DWPB(M_, 24)) if (g.TZ == 16) DWPB(M_, 16); else if (g.TZ == 8) DWPB(M_, 8); else if (g.TZ == 4) DWPB(M_, 4); else DWPB(M_, 2); } while (0)
+#define DWPB_T(M_) do { if (g.TZ == 16) DWPB(M_, 16); else if (g.TZ == 8) DWPB(M_, 8); else if (g.TZ == 4) DWPB(M_, 4); else DWPB(M_, 2); } while (0)
       if (xr1) {   // rank-1 input: the LDS-DMA IN-fused variant only (checked above)
         if constexpr (E == 4) {
 #define DWPR(T_) hipLaunchKernelGGL((dw3p_bwd_kernel<T, 1, T_, true, true>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
       g.RPW, g.ny, g.TZ, g.nz)
-          TZ24(DWPR(24)) if (g.TZ == 16) DWPR(16); else if (g.TZ == 8) DWPR(8); else if (g.TZ == 4) DWPR(4); else DWPR(2);
+          if (g.TZ == 16) DWPR(16); else if (g.TZ == 8) DWPR(8); else if (g.TZ == 4) DWPR(4); else DWPR(2);
 #undef DWPR
         }
       } else if (rec) DWPB_T(1);
@@ -1550,7 +1451,7 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
 #define DWQX(T_) hipLaunchKernelGGL((dw3q_fwd_kernel<float, T, 0, 1, T_>), grid, block, lds, stream, dz, \
       dz_nstride, w, rec, z, 0, dx, dx_nstride, x, x_nstride, in_part, N, C, D, H, W, g.RB, g.RPW, \
       g.ny, g.TZ, g.nz)
-      TZ24(DWQX(24)) if (g.TZ == 16) DWQX(16); else if (g.TZ == 8) DWQX(8); else if (g.TZ == 4) DWQX(4); else DWQX(2);
+      if (g.TZ == 16) DWQX(16); else if (g.TZ == 8) DWQX(8); else if (g.TZ == 4) DWQX(4); else DWQX(2);
 #undef DWQX
     }
     {
@@ -1558,7 +1459,7 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
       if (lds2 < 128 * sizeof(float)) lds2 = 128 * sizeof(float);
 #define DWQW(T_) hipLaunchKernelGGL((dw3q_dw_kernel<T, 1, T_>), grid, block, lds2, stream, dz, \
       dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
-      TZ24(DWQW(24)) if (g.TZ == 16) DWQW(16); else if (g.TZ == 8) DWQW(8); else if (g.TZ == 4) DWQW(4); else DWQW(2);
+      if (g.TZ == 16) DWQW(16); else if (g.TZ == 8) DWQW(8); else if (g.TZ == 4) DWQW(4); else DWQW(2);
 #undef DWQW
     }
     L3U_CHECK_LAUNCH();
@@ -1580,7 +1481,7 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
 // 1 when l3u_dw3_bwd takes a rank-1 input (x_nstride < 0) with rec at this shape (the fp32
 // LDS-DMA single pass, include/l3u.h "Rank-1 operands")
 extern "C" int l3u_dw3_bwd_rank1(int N, int C, int D, int H, int W) {
-  return N > 0 && C > 0 && !use_volume(D, H, W) && use_quads(H, W) && L3U_DW_FUSED && L3U_DWG_MODE1 &&
+  return N > 0 && C > 0 && !use_volume(D, H, W) && use_quads(H, W) &&
          dw_gl(qgeom(N, C, D, H, W), W, 4);
 }
 

@@ -336,9 +336,7 @@ size_t dp_lds(int K, int NB, int RB, int W) {
          (size_t)16 * 16 * 2 * sizeof(double) + (size_t)K * 27 * sizeof(float);
 }
 
-#ifndef L3U_DWPW_TZ
-#define L3U_DWPW_TZ 8
-#endif
+constexpr int kDwpwTz = 8;
 
 DPGeom dp_geom(int K, int Nout, int D, int H, int W, int sc) {
   DPGeom g{};
@@ -353,7 +351,7 @@ DPGeom dp_geom(int K, int Nout, int D, int H, int W, int sc) {
   if ((g.RB + 2) * WQ > 128) return g;                // <= 2 staged quads per lane
   if (sc && W + 256 > (g.RB + 2) * W) return g;       // shortcut B reads stay in the plane image
   g.ny = (H + g.RB - 1) / g.RB;
-  g.TZ = L3U_DWPW_TZ;
+  g.TZ = kDwpwTz;
   g.nz = (D + g.TZ - 1) / g.TZ;
   const int NB = 2 + sc;
   if (dp_lds(K, NB, g.RB, W) > 160 * 1024) return g;
@@ -380,7 +378,7 @@ int dwpw_fwd_impl(const T* x, long long x_nstride, const float* w_dw, const floa
   const int NB = 2 + sc;
   const size_t lds = dp_lds(K, NB, g.RB, W);
   dim3 grid(N * g.nz * g.ny), block(1024);
-#define DPF0(XF_, CPW_, NC_, SC_, R_) hipLaunchKernelGGL((dwpw_fwd_kernel<T, XF_, CPW_, NC_, SC_, L3U_DWPW_TZ, R_>), grid, \
+#define DPF0(XF_, CPW_, NC_, SC_, R_) hipLaunchKernelGGL((dwpw_fwd_kernel<T, XF_, CPW_, NC_, SC_, kDwpwTz, R_>), grid, \
       block, lds, stream, x, x_nstride, w_dw, rec, s, src ? 1 : 0, w_pw, y, y_nstride, y_stat, w_sc, r, \
       r_nstride, r_stat, z, z_nstride, D, H, W, g.RB, g.ny, g.nz)
 #define DPF(XF_, CPW_, NC_, SC_) DPF0(XF_, CPW_, NC_, SC_, false)

@@ -431,9 +431,7 @@ __global__ __launch_bounds__(256) void adamw_tick_kernel(float* __restrict__ p, 
 __global__ void counter_add_kernel(int* c, int v) { c[0] += v; }
 
 // ---------------------------------------------------------------- segmented partial reduction
-#ifndef L3U_SEG_BATCH
-#define L3U_SEG_BATCH 8   // measured: 8 < 16 < 32 us/step
-#endif
+constexpr int kSegBatch = 8;   // measured: 8 < 16 < 32 us/step
 // item (8 x int64): src_off, count, istride, tstride, len, dst_off, accumulate, unused
 // dst[dst_off + t] (+)= sum_{i<count} src[src_off + i*istride + t*tstride], t < len (<= 256)
 // Returns, for thread t < len, the segment's sum for output t (red: 256 doubles of LDS).
@@ -452,7 +450,7 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
     const long long base = it[0] + o * it[3];
     const long long stp = is * TP;
     long long i = k;
-    constexpr int B = L3U_SEG_BATCH;   // loads in flight per thread
+    constexpr int B = kSegBatch;   // loads in flight per thread
     if (it[7]) {
       const double* sd = reinterpret_cast<const double*>(src) + base;
       for (; i + (B - 1) * TP < cnt; i += B * TP) {

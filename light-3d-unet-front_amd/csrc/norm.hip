@@ -177,9 +177,7 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
 }
 
 // partials per (c, n, block): [sum g, sum g*xhat2, sum g*xhat_r],  g = dout * lrelu'(out)
-#ifndef L3U_NABR_U
-#define L3U_NABR_U 2
-#endif
+constexpr int kNabrU = 2;
 template <typename T, bool VEC, bool RK = false>
 __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     const float* __restrict__ dout, long long dns, const T* __restrict__ out, long long ons,
@@ -209,7 +207,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
   if (VEC) {
     // U grid-stride tiles per round: all their loads in flight before the first use, the sums
     // still taken tile by tile in index order (same bits as one tile per round)
-    constexpr int U = L3U_NABR_U;
+    constexpr int U = kNabrU;
     const int step = nb * 1024;
     for (int i0 = (blockIdx.x * 256 + threadIdx.x) * 4; i0 < S; i0 += U * step) {
       f4 ov[U], dv[U], yv[U], rv[U];
@@ -478,17 +476,13 @@ __global__ __launch_bounds__(256) void in_bwd_apply_kernel(
   }
 }
 
-#ifndef L3U_ELEM_PER_BLOCK
-#define L3U_ELEM_PER_BLOCK 4096
-#endif
-#ifndef L3U_ELEM_MAX_BLOCKS
-#define L3U_ELEM_MAX_BLOCKS 16
-#endif
+constexpr int kElemPerBlock = 4096;
+constexpr int kElemMaxBlocks = 16;
 // workgroups per (n, c) plane of the elementwise IN kernels: few enough that the per-workgroup
 // record merge (in-kernel finalize) stays small next to the streaming work
 int elem_blocks(int S) {
-  int b = (S + L3U_ELEM_PER_BLOCK - 1) / L3U_ELEM_PER_BLOCK;
-  return b > L3U_ELEM_MAX_BLOCKS ? L3U_ELEM_MAX_BLOCKS : (b < 1 ? 1 : b);
+  int b = (S + kElemPerBlock - 1) / kElemPerBlock;
+  return b > kElemMaxBlocks ? kElemMaxBlocks : (b < 1 ? 1 : b);
 }
 
 }  // namespace

@@ -1255,40 +1255,24 @@ __global__ __launch_bounds__(256) void convt_pair_bwd_kernel(
   }
 }
 
-#ifndef L3U_PW_SCH_MAX
-#define L3U_PW_SCH_MAX 512
-#endif
-#ifndef L3U_PW_NSW_MAX
-#define L3U_PW_NSW_MAX 1
-#endif
-#ifndef L3U_PW_SCH_MID
-#define L3U_PW_SCH_MID 256   // voxel chunk of the mid-size levels (4096 <= S < 65536: 24^3); 512: +10 us/step
-#endif
+constexpr int kPwSchMax = 512;
+constexpr int kPwNswMax = 1;
+constexpr int kPwSchMid = 256;   // voxel chunk of the mid-size levels (4096 <= S < 65536: 24^3); 512: +10 us/step
 int pw_sch(int S) {
-  return S >= 65536 ? L3U_PW_SCH_MAX : (S >= 4096 ? L3U_PW_SCH_MID : (S >= 1024 ? 512 : 256));
+  return S >= 65536 ? kPwSchMax : (S >= 4096 ? kPwSchMid : (S >= 1024 ? 512 : 256));
 }
 
 // voxel sub-tiles per wave of pw_fwd_kernel: fewer for narrow outputs so that big volumes
 // still launch enough workgroups (>= 4 per CU at one sample)
-int pw_nsw(int NC) { const int n = 4 / NC; return n < L3U_PW_NSW_MAX ? n : L3U_PW_NSW_MAX; }
+int pw_nsw(int NC) { const int n = 4 / NC; return n < kPwNswMax ? n : kPwNswMax; }
 
-#ifndef L3U_PW_MIN_BLOCKS
-#define L3U_PW_MIN_BLOCKS 1024   // measured: 0 / 512 / 1024 within 2 us, 1024 best
-#endif
-#ifndef L3U_PW_KS_MIN_K
-#define L3U_PW_KS_MIN_K 0
-#endif
-#ifndef L3U_CONVT_KS_MIN_K
-#define L3U_CONVT_KS_MIN_K 64  // ConvTranspose3d forward: shallower K takes the unsplit kernel (up3: 19.3 -> 14.5 us)
-#endif
-#ifndef L3U_PWKS8_MAX_WG
-#define L3U_PWKS8_MAX_WG 1024  // grids up to this many workgroups take all k-steps in flight
-#endif
+constexpr int kPwMinBlocks = 1024;   // measured: 0 / 512 / 1024 within 2 us, 1024 best
+constexpr int kPwKsMinK = 0;
+constexpr int kConvtKsMinK = 64;   // ConvTranspose3d forward: shallower K takes the unsplit kernel (up3: 19.3 -> 14.5 us)
+constexpr int kPwks8MaxWg = 1024;   // grids up to this many workgroups take all k-steps in flight
 // K split across the 4 waves (pw_fwd_ks_kernel) for small volumes with a deep enough reduction
-#ifndef L3U_PW_KS_MAX_S
-#define L3U_PW_KS_MAX_S 32768
-#endif
-bool pw_use_ks(int S, int K) { return S < L3U_PW_KS_MAX_S && K >= L3U_PW_KS_MIN_K; }
+constexpr int kPwKsMaxS = 32768;
+bool pw_use_ks(int S, int K) { return S < kPwKsMaxS && K >= kPwKsMinK; }
 
 }  // namespace
 
@@ -1312,7 +1296,7 @@ int pw_launch(const T* x, long long x_nstride, const float* w, int w_layout, con
   L3U_REQUIRE(N > 0 && K > 0 && Nout > 0 && S > 0);
   const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (y_nstride % 4 == 0) &&
                    (xm == 0 || Wq % 4 == 0);
-  if (pw_use_ks(S, K) && !(xm == 1 && K < L3U_CONVT_KS_MIN_K)) {
+  if (pw_use_ks(S, K) && !(xm == 1 && K < kConvtKsMinK)) {
     // co tile: as wide as possible while keeping >= 256 workgroups
     const int nsb = (S + 63) / 64;
     int NC = Nout <= 16 ? 1 : (Nout <= 32 ? 2 : 4);
@@ -1320,7 +1304,7 @@ int pw_launch(const T* x, long long x_nstride, const float* w, int w_layout, con
     const size_t lds = 4 * 64 * (size_t)NC * 16 * sizeof(float);
     dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), NZ), block(256);
     // the whole grid in one round of waves: the latency-bound form (all k-steps of a wave in flight)
-    const bool ks8 = NC <= 2 && xm != 2 && (long long)grid.x * grid.y * grid.z <= L3U_PWKS8_MAX_WG;
+    const bool ks8 = NC <= 2 && xm != 2 && (long long)grid.x * grid.y * grid.z <= kPwks8MaxWg;
 #define PWK(NC_, V_, X_) do { if (ks8) hipLaunchKernelGGL((pw_fwd_ks_kernel<T, NC_, V_, X_, 8>), grid, block, lds, \
       stream, x, x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq, \
       p2.x, p2.xns, p2.w, p2.y, p2.yns, p2.stat, N); \
@@ -1338,10 +1322,10 @@ int pw_launch(const T* x, long long x_nstride, const float* w, int w_layout, con
     L3U_CHECK_LAUNCH();
   }
   int CO_BLK = Nout <= 16 ? 16 : (Nout <= 32 ? 32 : 64);
-  // narrower output tiles while the grid is short of L3U_PW_MIN_BLOCKS workgroups (the 24^3 ->
+  // narrower output tiles while the grid is short of kPwMinBlocks workgroups (the 24^3 ->
   // 48^3 ConvTranspose3d: 432 -> 864)
   while (CO_BLK > 16 && (long long)((S + 255) / 256) * ((Nout + CO_BLK - 1) / CO_BLK) * NZ <
-                        L3U_PW_MIN_BLOCKS) CO_BLK >>= 1;
+                        kPwMinBlocks) CO_BLK >>= 1;
   const int NC = CO_BLK / 16, NSW = pw_nsw(NC), TSB = 256 * NSW;
   const int nsb = (S + TSB - 1) / TSB;
   const int WS = (CO_BLK % 32 == 16) ? CO_BLK : CO_BLK + 16;
@@ -1407,46 +1391,27 @@ int pw_bwd_weight_launch(const TD* dy, long long dy_nstride, const TX* x, long l
   L3U_CHECK_LAUNCH();
 }
 
-#ifndef L3U_CONVT_PAIR
-#define L3U_CONVT_PAIR 1   // ConvTranspose3d backward in the x-pair layout (even W) ...
-#endif
-#ifndef L3U_CONVT_PAIR1
-#define L3U_CONVT_PAIR1 1   // both pair-layout halves as one launch (convt_pair_bwd_kernel)
-#endif
-#ifndef L3U_CONVT_PAIR_MAX_S
-#define L3U_CONVT_PAIR_MAX_S 8192   // ... for input volumes up to this size (rocprof r2s: at 6^3
-#endif                              // 35.4 -> 19.8 us; at 24^3 34.3 -> 37.1 us, so not there)
-#ifndef L3U_CTW_MIN_BLOCKS
-#define L3U_CTW_MIN_BLOCKS 512
-#endif
-#ifndef L3U_CONVT_ONEPASS_ANYW
-#define L3U_CONVT_ONEPASS_ANYW 0   // 1: W % 4 != 0 (6^3) by scalar gathers (measured 8 us slower)
-#endif
-#ifndef L3U_CONVT_ONEPASS_MAX_S
-#define L3U_CONVT_ONEPASS_MAX_S 8192
-#endif
-#ifndef L3U_PWBF_MIN_BLOCKS
-#define L3U_PWBF_MIN_BLOCKS 256   // A/B r3: 256 -4 us/step (3 of 3), 128 +17 us, vs 512
-#endif
+constexpr int kConvtPair = 1;   // ConvTranspose3d backward in the x-pair layout (even W) ...
+constexpr int kConvtPair1 = 1;   // both pair-layout halves as one launch (convt_pair_bwd_kernel)
+// ... for input volumes up to this size (rocprof r2s: at 6^3 35.4 -> 19.8 us; at 24^3 34.3 -> 37.1 us)
+constexpr int kConvtPairMaxS = 8192;
+constexpr int kCtwMinBlocks = 512;
+constexpr int kConvtOnepassAnyw = 0;   // 1: W % 4 != 0 (6^3) by scalar gathers (measured 8 us slower)
+constexpr int kConvtOnepassMaxS = 8192;
+constexpr int kPwbfMinBlocks = 256;   // A/B r3: 256 -4 us/step (3 of 3), 128 +17 us, vs 512
 
 // wide form: J a multiple of 64 (<= 128), any K; narrow form: J <= 32, K <= 64
-#ifndef L3U_PW_BWD_WIDE
-#define L3U_PW_BWD_WIDE 1
-#endif
-bool pw_bwd_wide(int J) { return L3U_PW_BWD_WIDE && (J == 64 || J == 128); }
-#ifndef L3U_PWBF_NK_MAX
-#define L3U_PWBF_NK_MAX 4   // K columns per fused-backward workgroup, in 16s
-#endif
-#ifndef L3U_PWW_TPB_MAX
-#define L3U_PWW_TPB_MAX 8
-#endif
+constexpr int kPwBwdWide = 1;
+bool pw_bwd_wide(int J) { return kPwBwdWide && (J == 64 || J == 128); }
+constexpr int kPwbfNkMax = 4;   // K columns per fused-backward workgroup, in 16s
+constexpr int kPwwTpbMax = 8;
 // 64-voxel tiles per workgroup of pw_bwd_wide_kernel: one at the latency-bound small levels, up
-// to L3U_PWW_TPB_MAX on big volumes (fewer weight-gradient partials to write and reduce) while
+// to kPwwTpbMax on big volumes (fewer weight-gradient partials to write and reduce) while
 // each sample keeps >= 32 workgroups per column block
 int pww_tpb(int S) {
   const int ntile = (S + 63) / 64;
   int t = 1;
-  while (2 * t <= L3U_PWW_TPB_MAX && ntile / (2 * t) >= 32) t *= 2;
+  while (2 * t <= kPwwTpbMax && ntile / (2 * t) >= 32) t *= 2;
   return t;
 }
 int pww_nblk(int S) { const int t = pww_tpb(S); return ((S + 63) / 64 + t - 1) / t; }
@@ -1475,8 +1440,8 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
   const int NJ = J <= 16 ? 1 : 2;
   int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
-  if (NK > L3U_PWBF_NK_MAX) NK = L3U_PWBF_NK_MAX;
-  while (NK > 1 && (long long)N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < L3U_PWBF_MIN_BLOCKS) NK >>= 1;
+  if (NK > kPwbfNkMax) NK = kPwbfNkMax;
+  while (NK > 1 && (long long)N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < kPwbfMinBlocks) NK >>= 1;
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
@@ -1521,8 +1486,8 @@ int pw_bwd_tail_pair_impl(const float* dout, long long dout_nstride, const float
   const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
   const int NJ = J <= 16 ? 1 : 2, K = a.K > b.K ? a.K : b.K;
   int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
-  if (NK > L3U_PWBF_NK_MAX) NK = L3U_PWBF_NK_MAX;
-  while (NK > 1 && 2ll * N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < L3U_PWBF_MIN_BLOCKS) NK >>= 1;
+  if (NK > kPwbfNkMax) NK = kPwbfNkMax;
+  while (NK > 1 && 2ll * N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < kPwbfMinBlocks) NK >>= 1;
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK), 2), block(64 * nwv);
@@ -1575,8 +1540,8 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
   const int NJ = J <= 16 ? 1 : 2;
   // K columns per workgroup: all of them unless the grid would be too small to fill the chip
   int NK = K <= 16 ? 1 : (K <= 32 ? 2 : 4);
-  if (NK > L3U_PWBF_NK_MAX) NK = L3U_PWBF_NK_MAX;
-  while (NK > 1 && (long long)N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < L3U_PWBF_MIN_BLOCKS) NK >>= 1;
+  if (NK > kPwbfNkMax) NK = kPwbfNkMax;
+  while (NK > 1 && (long long)N * nsc * ((K + 16 * NK - 1) / (16 * NK)) < kPwbfMinBlocks) NK >>= 1;
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);   // one sweep of the chunk per workgroup
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
@@ -1668,11 +1633,11 @@ int convt_bwd_impl(const float* dy, long long dy_nstride, const T* x, long long 
                    int N, int Ci, int Co, int D, int H, int W, hipStream_t stream) {
   L3U_REQUIRE(N > 0 && Ci > 0 && Co > 0 && D > 0 && H > 0 && W > 0);
   const int S = D * H * W;
-  const bool pdx = L3U_CONVT_PAIR && S <= L3U_CONVT_PAIR_MAX_S && W % 2 == 0 && dy_nstride % 4 == 0 &&
+  const bool pdx = kConvtPair && S <= kConvtPairMaxS && W % 2 == 0 && dy_nstride % 4 == 0 &&
                    dx_nstride % 2 == 0 && al4<float>(dy) && ((uintptr_t)dx & 7) == 0;
-  const bool pdw = L3U_CONVT_PAIR && S <= L3U_CONVT_PAIR_MAX_S && W % 2 == 0 && x_nstride % 2 == 0 &&
+  const bool pdw = kConvtPair && S <= kConvtPairMaxS && W % 2 == 0 && x_nstride % 2 == 0 &&
                    dy_nstride % 4 == 0 && al4<float>(dy) && ((uintptr_t)x & (2 * sizeof(T) - 1)) == 0;
-  if (L3U_CONVT_PAIR1 && pdx && pdw && Co >= 16) {
+  if (kConvtPair1 && pdx && pdw && Co >= 16) {
     // one launch for both halves (same tile choices as the two launches below)
     const int P = D * H * (W / 2);
     const int NC = Ci % 32 == 0 && (long long)N * ((P + 15) / 16) * (Ci / 32) >= 256 ? 2 : 1;
@@ -1682,7 +1647,7 @@ int convt_bwd_impl(const float* dy, long long dy_nstride, const T* x, long long 
     for (;;) {
       const long long nb = (long long)N * nsc * ((Ci + 16 * NJ - 1) / (16 * NJ)) *
                            ((Co + 4 * NG - 1) / (4 * NG));
-      if (nb >= L3U_CTW_MIN_BLOCKS || (NJ == 1 && NG == 1)) break;
+      if (nb >= kCtwMinBlocks || (NJ == 1 && NG == 1)) break;
       if (NG > 1) NG >>= 1; else NJ >>= 1;
     }
     const int gwx = N * nsc, gwy = ((Ci + 16 * NJ - 1) / (16 * NJ)) * ((Co + 4 * NG - 1) / (4 * NG));
@@ -1701,7 +1666,7 @@ int convt_bwd_impl(const float* dy, long long dy_nstride, const T* x, long long 
   // dX[ci][s] = sum_{co,abc} w[ci][co*8+abc] dY[co][up(s, abc)] (all gradients: fp32): in the
   // x-pair layout for even W (8-byte aligned rows), else the GEMM with X gathered
   int rc;
-  if (L3U_CONVT_PAIR && S <= L3U_CONVT_PAIR_MAX_S && W % 2 == 0 && dy_nstride % 4 == 0 &&
+  if (kConvtPair && S <= kConvtPairMaxS && W % 2 == 0 && dy_nstride % 4 == 0 &&
       dx_nstride % 2 == 0 && al4<float>(dy) &&
       ((uintptr_t)dx & 7) == 0) {
     const int P = D * H * (W / 2);
@@ -1721,16 +1686,16 @@ int convt_bwd_impl(const float* dy, long long dy_nstride, const T* x, long long 
   if (rc != 0) return rc;
   // dW[ci][co*8+abc] = sum_s x[ci][s] dY[co][up(s, abc)] and, in the same launch,
   // db[co] = sum of dY over the up-sampled volume: bpart[N*nsc][Co]
-  if (L3U_CONVT_PAIR && S <= L3U_CONVT_PAIR_MAX_S && W % 2 == 0 && x_nstride % 2 == 0 &&
+  if (kConvtPair && S <= kConvtPairMaxS && W % 2 == 0 && x_nstride % 2 == 0 &&
       dy_nstride % 4 == 0 && al4<float>(dy) &&
       ((uintptr_t)x & (2 * sizeof(T) - 1)) == 0) {
     const int SCH = pw_sch(S), nsc = (S + SCH - 1) / SCH;
-    // as many (ci, co) tiles per workgroup as keep >= L3U_CTW_MIN_BLOCKS workgroups
+    // as many (ci, co) tiles per workgroup as keep >= kCtwMinBlocks workgroups
     int NJ = Ci % 32 == 0 ? 2 : 1, NG = Co % 16 == 0 ? 4 : (Co % 8 == 0 ? 2 : 1);
     for (;;) {
       const long long nb = (long long)N * nsc * ((Ci + 16 * NJ - 1) / (16 * NJ)) *
                            ((Co + 4 * NG - 1) / (4 * NG));
-      if (nb >= L3U_CTW_MIN_BLOCKS || (NJ == 1 && NG == 1)) break;
+      if (nb >= kCtwMinBlocks || (NJ == 1 && NG == 1)) break;
       if (NG > 1) NG >>= 1; else NJ >>= 1;
     }
     dim3 grid(N * nsc, ((Ci + 16 * NJ - 1) / (16 * NJ)) * ((Co + 4 * NG - 1) / (4 * NG))), block(256);
@@ -1795,7 +1760,7 @@ int l3u_convt_bwd_fused_nparts(int N, int Ci, int Co, int D, int H, int W) {
   if (nt > 0) return nt;
   if (!(N > 0 && Ci > 0 && (Co == 8 || Co == 16 || Co == 32 || Co == 64) && D > 0 && H > 0 && W > 0))
     return 0;
-  if ((!L3U_CONVT_ONEPASS_ANYW && W % 4 != 0) || D * H * W > L3U_CONVT_ONEPASS_MAX_S) return 0;
+  if ((!kConvtOnepassAnyw && W % 4 != 0) || D * H * W > kConvtOnepassMaxS) return 0;
   return N * pww_nblk(D * H * W);
 }
 

@@ -55,7 +55,7 @@ def main():
     dt = [torch.from_numpy(t).to(dev) for _, t in bt]
     res, times = {}, {}
     for name, kw in (("single", dict(distributed=False)),
-                     ("segmented", dict(force_exchange=True)),
+                     ("segmented", dict(force_exchange=True, capture_collectives=False)),
                      ("captured", dict(force_exchange=True, capture_collectives=True))):
         torch.manual_seed(42)
         m = Lightweight3DUNet(dropout_p=0.1).to(dev).train()
