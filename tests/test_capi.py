@@ -95,6 +95,7 @@ def test_host_queries_without_gpu():
     assert _native.query("l3u_convt_bwd_fused_nparts", 4, 64, 32, 12, 12, 12) == 4 * 14
     assert _native.query("l3u_convt_bwd_fused_nparts", 4, 32, 16, 24, 24, 24) == 4 * 108
     assert _native.query("l3u_convt_bwd_fused_nparts", 4, 128, 64, 6, 6, 6) == 0
+    assert _native.query("l3u_convt_bwd_fused_nparts", 4, 128, 64, 16, 16, 16) == 4 * 8
     assert _native.query("l3u_convt_bwd_fused_nparts", 4, 256, 128, 6, 6, 6) == 0
     assert _native.query("l3u_dw3_nchunk", 4, 32, 24, 24, 24) == 18   # 6 z-slabs x 3 y-strips
     assert _native.query("l3u_dw3_nchunk", 4, 128, 6, 6, 6) == 1

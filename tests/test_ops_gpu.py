@@ -739,7 +739,10 @@ CONVT_ONEPASS = [(2, 32, 16, 8, 8, 8), (2, 64, 32, 6, 6, 8), (1, 128, 64, 3, 3, 
                  # workgroup), ragged volumes (a tile past the end), 16 / 32 / 64-channel blocks,
                  # config 5's 32^3 up3 (four tiles per workgroup)
                  (4, 32, 16, 24, 24, 24), (2, 64, 32, 5, 6, 6), (1, 16, 16, 5, 4, 6),
-                 (2, 32, 32, 7, 5, 4), (1, 64, 32, 32, 32, 32)]
+                 (2, 32, 32, 7, 5, 4), (1, 64, 32, 32, 32, 32),
+                 # the Co = 64 staged form (>= 4096 pairs): ragged with a single 16-channel
+                 # block, and 8 blocks
+                 (2, 16, 64, 16, 15, 18), (2, 128, 64, 16, 16, 16)]
 
 
 @pytest.mark.parametrize("case", CONVT_ONEPASS)
