@@ -334,6 +334,9 @@ QGeom qgeom(int N, int C, int D, int H, int W) {
   g.threads = 64 * best;
   g.TZ = D >= kTz16MinD ? 16 : (D >= 32 ? 8 : (D > 8 ? 4 : 8));   // compile-time in the kernels
   while (g.TZ > 2 && (long long)N * C * g.ny * ((D + g.TZ - 1) / g.TZ) < kDwMinBlocks) g.TZ >>= 1;   // {16, 8, 4, 2}
+  // 12-plane slabs where 16-plane ones leave under two tiles per SIMD (the 48^3 IN-fused
+  // backward of the 16-channel blocks: 1920 -> 2560 one-wave tiles, -8 us/step A/B)
+  if (g.TZ == 16 && (long long)N * C * g.ny * ((D + 15) / 16) < 2 * kDwMinBlocks) g.TZ = 12;
   g.nz = (D + g.TZ - 1) / g.TZ;
   return g;
 }
@@ -1368,8 +1371,8 @@ int dw3_fwd_impl(const T* x, long long x_nstride, const float* w, const float* r
 #define DWQF(M_, T_) hipLaunchKernelGGL((dw3q_fwd_kernel<T, T, M_, 0, T_, kDwqPd>), grid, block, lds, stream, x, \
       x_nstride, w, rec, s, has, y, y_nstride, nullptr, 0, nullptr, N, C, D, H, W, g.RB, g.RPW, \
       g.ny, g.TZ, g.nz)
-    if (xf) { if (g.TZ == 16) DWQF(1, 16); else if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
-    else { if (g.TZ == 16) DWQF(0, 16); else if (g.TZ == 8) DWQF(0, 8); else if (g.TZ == 4) DWQF(0, 4); else DWQF(0, 2); }
+    if (xf) { if (g.TZ == 16) DWQF(1, 16); else if (g.TZ == 12) DWQF(1, 12); else if (g.TZ == 8) DWQF(1, 8); else if (g.TZ == 4) DWQF(1, 4); else DWQF(1, 2); }
+    else { if (g.TZ == 16) DWQF(0, 16); else if (g.TZ == 12) DWQF(0, 12); else if (g.TZ == 8) DWQF(0, 8); else if (g.TZ == 4) DWQF(0, 4); else DWQF(0, 2); }
 #undef DWQF
     L3U_CHECK_LAUNCH();
   }
@@ -1425,13 +1428,13 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
       else hipLaunchKernelGGL((dw3p_bwd_kernel<T, M_, T_>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
       g.RPW, g.ny, g.TZ, g.nz); } while (0)
-#define DWPB_T(M_) do { if (g.TZ == 16) DWPB(M_, 16); else if (g.TZ == 8) DWPB(M_, 8); else if (g.TZ == 4) DWPB(M_, 4); else DWPB(M_, 2); } while (0)
+#define DWPB_T(M_) do { if (g.TZ == 16) DWPB(M_, 16); else if (g.TZ == 12) DWPB(M_, 12); else if (g.TZ == 8) DWPB(M_, 8); else if (g.TZ == 4) DWPB(M_, 4); else DWPB(M_, 2); } while (0)
       if (xr1) {   // rank-1 input: the LDS-DMA IN-fused variant only (checked above)
         if constexpr (E == 4) {
 #define DWPR(T_) hipLaunchKernelGGL((dw3p_bwd_kernel<T, 1, T_, true, true>), grid, block, lds, stream, dz, \
       dz_nstride, x, x_nstride, w, rec, dx, dx_nstride, dw_part, in_part, N, C, D, H, W, g.RB, \
       g.RPW, g.ny, g.TZ, g.nz)
-          if (g.TZ == 16) DWPR(16); else if (g.TZ == 8) DWPR(8); else if (g.TZ == 4) DWPR(4); else DWPR(2);
+          if (g.TZ == 16) DWPR(16); else if (g.TZ == 12) DWPR(12); else if (g.TZ == 8) DWPR(8); else if (g.TZ == 4) DWPR(4); else DWPR(2);
 #undef DWPR
         }
       } else if (rec) DWPB_T(1);
@@ -1451,7 +1454,7 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
 #define DWQX(T_) hipLaunchKernelGGL((dw3q_fwd_kernel<float, T, 0, 1, T_>), grid, block, lds, stream, dz, \
       dz_nstride, w, rec, z, 0, dx, dx_nstride, x, x_nstride, in_part, N, C, D, H, W, g.RB, g.RPW, \
       g.ny, g.TZ, g.nz)
-      if (g.TZ == 16) DWQX(16); else if (g.TZ == 8) DWQX(8); else if (g.TZ == 4) DWQX(4); else DWQX(2);
+      if (g.TZ == 16) DWQX(16); else if (g.TZ == 12) DWQX(12); else if (g.TZ == 8) DWQX(8); else if (g.TZ == 4) DWQX(4); else DWQX(2);
 #undef DWQX
     }
     {
@@ -1459,7 +1462,7 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
       if (lds2 < 128 * sizeof(float)) lds2 = 128 * sizeof(float);
 #define DWQW(T_) hipLaunchKernelGGL((dw3q_dw_kernel<T, 1, T_>), grid, block, lds2, stream, dz, \
       dz_nstride, x, x_nstride, rec, dw_part, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
-      if (g.TZ == 16) DWQW(16); else if (g.TZ == 8) DWQW(8); else if (g.TZ == 4) DWQW(4); else DWQW(2);
+      if (g.TZ == 16) DWQW(16); else if (g.TZ == 12) DWQW(12); else if (g.TZ == 8) DWQW(8); else if (g.TZ == 4) DWQW(4); else DWQW(2);
 #undef DWQW
     }
     L3U_CHECK_LAUNCH();

@@ -127,8 +127,8 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
   const int oy = own ? lr : 0, ox = 4 * qx;
   const bool el = qx == 0, er = qx == WQ - 1;
   float* planes = lds;                          // [K][NB][PP]
-  float* zt = lds + (size_t)K * NB * PP;        // [K][VP]
-  double* sred = reinterpret_cast<double*>(zt + K * VP);   // [NT][16 ch][2]
+  float* zt = lds + (size_t)K * NB * PP;        // [2][K][VP]: the Z tiles of two plane steps
+  double* sred = reinterpret_cast<double*>(zt + 2 * K * VP);   // [NT][16 ch][2]
   float* taps = reinterpret_cast<float*>(sred + NT * 16 * 2);   // [K][27] (LTAP)
 
   // ---- per-channel setup: taps, InstanceNorm record, first two planes in flight
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
 #pragma unroll
       for (int tp = 0; tp < 27; ++tp) wk[i][tp] = wdw[(wv * CPW + i) * 27 + tp];
   }
-  for (int i = threadIdx.x; i < K * NB * PP + K * VP; i += blockDim.x) planes[i] = 0.f;   // + zt
+  for (int i = threadIdx.x; i < K * NB * PP + 2 * K * VP; i += blockDim.x) planes[i] = 0.f;   // + zt
 
   // ---- GEMM role of this wave: tile tau = wv -> (voxel group g, channel block m, Y or R)
   const bool mm = wv < NT;
@@ -199,6 +199,41 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
 #pragma unroll
   for (int i = 0; i < CPW; ++i) a0[i] = a1[i] = a2[i] = f4{0.f, 0.f, 0.f, 0.f};
 
+  // (c) the channel GEMM on the MFMA of plane step tt's Z tile: Y (or R) tile of 16 channels x
+  // 64 voxels.  It runs one plane step late, between the next step's barrier and its stencil, so
+  // the 4 * NC (* 2) GEMM waves overlap their MFMAs with the other waves' stencils and a step
+  // needs one workgroup barrier instead of two (the Z tiles alternate between two buffers)
+  auto gemm = [&](int tt) {
+    const int zo = z0 - 2 + tt;
+    if (!mm) return;
+    const float* bsrc = (SC && which == 1) ? planes + W + (size_t)((tt - 1) % NB) * PP + v0
+                                           : zt + (tt & 1) * K * VP + v0;
+    const size_t kstr = (SC && which == 1) ? (size_t)NB * PP : (size_t)VP;
+    f4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < K / 4; ++ks) {
+      const f4 b = *reinterpret_cast<const f4*>(bsrc + (size_t)(4 * ks + lk) * kstr);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = mfma4(aw[ks], b[q], acc[q]);
+    }
+    // lane (lrm, lk) holds channels 16m + 4lk + rr of the voxel quad v0 .. v0+3
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int co = 16 * m + 4 * lk + rr;
+      f4 o = f4{acc[0][rr], acc[1][rr], acc[2][rr], acc[3][rr]};
+      T* dst = outp + (long long)co * S + (long long)zo * HW + (long long)(y0 + vrow) * W + vx;
+      if (vok) stv4(dst, o);
+      o = round_to(o, dst);   // statistics of the stored values
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double dv = vok ? (double)o[q] : 0.0;
+        s1[rr] += dv;
+        s2[rr] = fma(dv, dv, s2[rr]);
+      }
+    }
+  };
+  auto fin_at = [&](int tt) { const int zo = z0 - 2 + tt; return zo >= z0 && zo < z1; };
+
   auto step = [&](int t, int slot) {
     const int zi = z0 - 1 + t, zo = zi - 1;
     const int bi = t % NB;
@@ -211,9 +246,14 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
                         rks[i]);
       w_fetch(st[i][slot], xn + (long long)c * cst + zc(zi + PD), wm);
     }
-    __syncthreads();   // B1: planes visible; the previous step's GEMM reads of zt are done
+    // B: planes visible; the previous step's Z tile complete; the GEMM reads of the Z tile this
+    // step overwrites (two steps back) done
+    __syncthreads();
+    if (t >= 1 && fin_at(t - 1)) gemm(t - 1);   // uniform over the workgroup
+    __builtin_amdgcn_sched_barrier(0);   // the GEMM's registers die before the stencil's
     const bool fin = zo >= z0 && zo < z1;
     // (b) the stencil of each own channel (dw3q_fwd's tap order), Z quad -> zt (and global)
+    float* ztc = zt + (t & 1) * K * VP;
 #pragma unroll
     for (int i = 0; i < CPW; ++i) {
       const int c = wv * CPW + i;
@@ -242,7 +282,7 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
       if (fin) {
         const f4 o = round_to(a0[i], (const T*)nullptr);   // Z at its storage precision
         if (lr < RB)
-          *reinterpret_cast<f4*>(zt + c * VP + lr * W + ox) = own ? o : f4{0.f, 0.f, 0.f, 0.f};
+          *reinterpret_cast<f4*>(ztc + c * VP + lr * W + ox) = own ? o : f4{0.f, 0.f, 0.f, 0.f};
         if (z != nullptr && own)
           stv4(z + (long long)n * zns + (long long)c * S + (long long)zo * HW + (long long)(y0 + oy) * W + ox, o);
       }
@@ -250,42 +290,14 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
       a1[i] = a2[i];
       a2[i] = f4{0.f, 0.f, 0.f, 0.f};
     }
-    if (!fin) return;   // uniform over the workgroup
-    __syncthreads();   // B2: the Z tile of plane zo is complete
-    // (c) the channel GEMM on the MFMA: Y (or R) tile of 16 channels x 64 voxels
-    if (mm) {
-      const float* bsrc = (SC && which == 1) ? planes + W + (size_t)((t - 1) % NB) * PP + v0
-                                             : zt + v0;
-      const size_t kstr = (SC && which == 1) ? (size_t)NB * PP : (size_t)VP;
-      f4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-      for (int ks = 0; ks < K / 4; ++ks) {
-        const f4 b = *reinterpret_cast<const f4*>(bsrc + (size_t)(4 * ks + lk) * kstr);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = mfma4(aw[ks], b[q], acc[q]);
-      }
-      // lane (lrm, lk) holds channels 16m + 4lk + rr of the voxel quad v0 .. v0+3
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int co = 16 * m + 4 * lk + rr;
-        f4 o = f4{acc[0][rr], acc[1][rr], acc[2][rr], acc[3][rr]};
-        T* dst = outp + (long long)co * S + (long long)zo * HW + (long long)(y0 + vrow) * W + vx;
-        if (vok) stv4(dst, o);
-        o = round_to(o, dst);   // statistics of the stored values
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const double dv = vok ? (double)o[q] : 0.0;
-          s1[rr] += dv;
-          s2[rr] = fma(dv, dv, s2[rr]);
-        }
-      }
-    }
   };
 #pragma unroll
   for (int t = 0; t < TZC + 2; t += PD) {
 #pragma unroll
     for (int k = 0; k < PD; ++k) step(t + k, k);
   }
+  __syncthreads();   // the last step's Z tile
+  if (fin_at(TZC + 1)) gemm(TZC + 1);
 
   // ---- statistics partials: lanes of a row -> waves of the same (m, which) in g order
   if (mm) {
@@ -330,9 +342,9 @@ struct DPGeom {
   bool ok;
 };
 
-// planes + Z tile + statistics scratch (16 tiles) + taps
+// planes + two Z tiles + statistics scratch (16 tiles) + taps
 size_t dp_lds(int K, int NB, int RB, int W) {
-  return ((size_t)K * NB * (RB + 2) * W + (size_t)K * 256) * sizeof(float) +
+  return ((size_t)K * NB * (RB + 2) * W + (size_t)2 * K * 256) * sizeof(float) +
          (size_t)16 * 16 * 2 * sizeof(double) + (size_t)K * 27 * sizeof(float);
 }
 

@@ -857,20 +857,6 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
   const float* dyn = dy + (long long)n * dyns;
   const T* xn = x + (long long)n * xns;
 
-  if (PRO) {   // per-row InstanceNorm-backward coefficients (rows < J <= 128)
-    if (tid < J) {
-      double t[2];
-      seq_sum<2>(in_part + ((long long)tid * N + n) * npart * 2, npart, t);
-      const float* q = rec + ((long long)n * J + tid) * kRec;
-      float* o = coef + tid * 8;
-      o[0] = q[1] * q[5];
-      o[1] = (float)(t[0] / S);
-      o[2] = q[0];
-      o[3] = q[1];
-      o[4] = (float)(t[1] / S);
-    }
-    __syncthreads();
-  }
   f4 gw[JT];
   float bsum[JT];
 #pragma unroll
@@ -910,6 +896,22 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
     for (int g = 0; g < 4; ++g)
       xb[g] = load_x4<GV, false>(xn, k0 + lr, K, v0 + 16 * g + 4 * lk, S, S, 0, 0);
 
+    if (PRO && tile == t0) {
+      // per-row InstanceNorm-backward coefficients (rows < J <= 128), requested after the first
+      // tile's streamed loads so that both arrive in one memory round trip
+      if (tid < J) {
+        double t[2];
+        seq_sum<2>(in_part + ((long long)tid * N + n) * npart * 2, npart, t);
+        const float* q = rec + ((long long)n * J + tid) * kRec;
+        float* o = coef + tid * 8;
+        o[0] = q[1] * q[5];
+        o[1] = (float)(t[0] / S);
+        o[2] = q[0];
+        o[3] = q[1];
+        o[4] = (float)(t[1] / S);
+      }
+      __syncthreads();
+    }
     if (PRO) {
 #pragma unroll
       for (int jr = 0; jr < JT * 4; ++jr) {
