@@ -1416,8 +1416,10 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
     const QGeom g = qgeom(N, C, D, H, W);
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
     const bool gl = dw_gl(g, W, E);
-    // MODE 1 (IN-fused) only on the LDS-DMA variant: register-staged it measured faster split
-    if (rec == nullptr || gl) {
+    // MODE 1 (IN-fused): the LDS-DMA variant, and the register-staged single pass for bf16
+    // storage (its 12^3 planes have no bf16 DMA layout: -9 us/step against the split passes);
+    // fp32 register-staged measured faster split
+    if (rec == nullptr || gl || E == 2) {
       // single pass: data + weight gradient from one read of dZ and A
       size_t lds = 4 * (size_t)(g.RB + 2) * (W + kLPad) * sizeof(float);
       if (lds < 160 * sizeof(float)) lds = 160 * sizeof(float);   // reduction scratch

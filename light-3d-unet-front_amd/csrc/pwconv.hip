@@ -1257,7 +1257,7 @@ __global__ __launch_bounds__(256) void convt_pair_bwd_kernel(
   }
 }
 
-constexpr int kPwSchMax = 512;
+constexpr int kPwSchMax = 256;   // 4-wave sweeps at >= 64K voxels: config 5 -115 us (the 64^3 J = 32 tails hold 85 KB of LDS as 8-wave sweeps: one workgroup per CU), 48^3 -3 us
 constexpr int kPwNswMax = 1;
 constexpr int kPwSchMid = 256;   // voxel chunk of the mid-size levels (4096 <= S < 65536: 24^3); 512: +10 us/step
 int pw_sch(int S) {
