@@ -806,6 +806,135 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   }
 }
 
+// The pointwise backward with ONE input channel (K = 1: the first block's conv1.pointwise,
+// unet3d.py:163-167 with in_channels = 1) and the InstanceNorm-backward prologue (PRO 1):
+//   dY[j][s]  = f_j (dpre[j][s] - M1_j - (y[j][s] - mu_j) rs_j M2_j)     (l3u_in_bwd_apply)
+//   dX[s]     = sum_j W[j] dY[j][s]                                     (j in order, fp32 fma)
+//   part[j]   = sum_{s in chunk} dY[j][s] X[s]                           (fixed-order tree)
+// On the VALU: at K = 1 the MFMA tile is 15/16 padding and the fused kernel moved 16 dY rows
+// through LDS for one output column.  A thread owns 4 voxels, a workgroup the pw_bwd_fused
+// chunk of SCH voxels (same partial layout part[chunk][J][1]); rows 16 at a time (J <= 32).  A
+// rank-1 y (yns < 0) is one stored channel, row j = rec[j][7] * it (the materialised values).
+template <typename T>
+__global__ __launch_bounds__(128) void pw_bwd_k1_kernel(
+    const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
+    const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
+    const T* __restrict__ x, long long xns, const float* __restrict__ w, float* __restrict__ dx,
+    long long dxns, int accumulate, float* __restrict__ part, int N, int J, int S, int SCH, int nsc) {
+  L3U_STAMP_SCOPE(107);
+  __shared__ float coef[32 * 8];
+  __shared__ double psum[32 * 4 * 2];
+  __shared__ float wred[2][32];
+  const int tid = threadIdx.x, l = tid & 63, wave = tid >> 6, nwv = blockDim.x >> 6;
+  const int sc = blockIdx.x % nsc, n = blockIdx.x / nsc;
+  const int s = sc * SCH + 4 * tid;
+  const bool ok = s < S && 4 * tid < SCH;
+  const bool yk = yns < 0;
+  const float* dyn = dy + (long long)n * dyns;
+  const T* yn = yin + (long long)n * (yk ? -yns : yns);
+  // the first 16 rows' streamed loads, then the coefficients (one memory round trip)
+  f4 g[16], yv[16];
+  const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  auto load_rows = [&](int j0) {
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int j = j0 + jj;
+      g[jj] = (j < J && ok) ? ldv4(dyn + (long long)j * S + s) : z4;
+      if (!yk) yv[jj] = (j < J && ok) ? ldv4(yn + (long long)j * S + s) : z4;
+    }
+    if (yk) yv[0] = ok ? ldv4(yn + s) : z4;
+  };
+  load_rows(0);
+  const f4 xv = ok ? ldv4(x + (long long)n * xns + s) : z4;
+  // 4 lanes per row sum the IN-backward partials (16 loads per lane in flight at once, then added
+  // in index order), combined in lane order
+  for (int jr = tid >> 2; jr < J; jr += blockDim.x >> 2) {
+    const int sub = tid & 3;
+    double t0 = 0.0, t1 = 0.0;
+    const double* pp = in_part + ((long long)jr * N + n) * npart * 2;
+    constexpr int PB = 16;
+    for (int i0 = sub; i0 < npart; i0 += 4 * PB) {
+      double2 v[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int i = i0 + 4 * u;
+        v[u] = i < npart ? *reinterpret_cast<const double2*>(pp + i * 2) : double2{0.0, 0.0};
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) { t0 += v[u].x; t1 += v[u].y; }
+    }
+    psum[(jr * 4 + sub) * 2] = t0;
+    psum[(jr * 4 + sub) * 2 + 1] = t1;
+  }
+  __syncthreads();
+  for (int j = tid; j < J; j += blockDim.x) {
+    double t0 = 0.0, t1 = 0.0;
+    for (int i = 0; i < 4; ++i) { t0 += psum[(j * 4 + i) * 2]; t1 += psum[(j * 4 + i) * 2 + 1]; }
+    const float* q = rec + ((long long)n * J + j) * kRec;
+    float* o = coef + j * 8;
+    o[0] = q[1] * q[5];          // f = rstd * gamma
+    o[1] = (float)(t0 / S);      // M1
+    o[2] = q[0];                 // mu
+    o[3] = q[1];                 // rstd
+    o[4] = (float)(t1 / S);      // M2
+    o[5] = q[7];                 // rank-1 scale
+    o[6] = w[j];                 // W[j][0]
+  }
+  __syncthreads();
+  f4 dxa = z4;
+  float pw[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) pw[j] = 0.f;
+  const f4 y1 = yv[0];
+  auto rows = [&](auto H) {   // rows 16 H .. 16 H + 15 (compile-time indices: registers)
+    constexpr int h = decltype(H)::value;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int j = 16 * h + jj;
+      if (j < J) {   // uniform
+        const float* c = coef + j * 8;
+        const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
+        const f4 yj = yk ? mul_rn(y1, c[5]) : yv[jj];
+        f4 d;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = ok ? f * (g[jj][q] - M1 - (yj[q] - mu) * rs * M2) : 0.f;
+        const float wj = c[6];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          dxa[q] = fmaf(wj, d[q], dxa[q]);
+          pw[j] = fmaf(d[q], xv[q], pw[j]);
+        }
+      }
+    }
+  };
+  rows(std::integral_constant<int, 0>{});
+  if (J > 16) {   // uniform
+    load_rows(16);
+    rows(std::integral_constant<int, 1>{});
+  }
+  if (ok) {
+    float* dst = dx + (long long)n * dxns + s;
+    if (accumulate) dxa += ldv4(dst);
+    *reinterpret_cast<f4*>(dst) = dxa;
+  }
+  // weight-gradient partial of the chunk: xor tree over the wave, then the waves in order
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    if (j < J) {   // uniform
+      float v = pw[j];
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (l == 0) wred[wave][j] = v;
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < J; j += blockDim.x) {
+    float v = wred[0][j];
+    for (int k = 1; k < nwv; ++k) v += wred[k][j];
+    part[(long long)blockIdx.x * J + j] = v;
+  }
+}
+
 // Fused 1x1-conv backward for wide J (J = 16 * JT * NWV: 64 / 128 for the 12^3 / 6^3 levels,
 // and the ConvTranspose3d(k2, s2) backward, J = Co*8 up to 512), latency-bound shapes: one
 // workgroup of NWV waves per (64-voxel tile, 16 columns of K).  Wave w owns the dY rows
@@ -1548,15 +1677,15 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);   // one sweep of the chunk per workgroup
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
   const size_t dlds = (size_t)nwv * 16 * NJ * 68 * sizeof(float);   // dY tiles (DS = 68)
-  // a rank-1 y (the first block's conv1.pointwise, K = 1): its own variant
-  L3U_REQUIRE(y_nstride >= 0 || (NJ == 1 && NK == 1));
-  if (y && y_nstride < 0) {
-    if constexpr (sizeof(T) == 4)
-      hipLaunchKernelGGL((pw_bwd_fused_kernel<T, 1, 1, 1, true>), grid, block, dlds, stream, dy,
-                         dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx,
-                         dx_nstride, accumulate, part, N, J, K, S, SCH, nsc);
+  // one input channel with the IN prologue (the first block's conv1.pointwise, y materialised or
+  // rank-1): the VALU kernel, same chunks and partial layout
+  if (K == 1 && y != nullptr && SCH <= 512 && J <= 32) {
+    hipLaunchKernelGGL((pw_bwd_k1_kernel<T>), dim3(N * nsc), dim3(SCH / 4), 0, stream, dy, dy_nstride,
+                       y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride,
+                       accumulate, part, N, J, S, SCH, nsc);
     L3U_CHECK_LAUNCH();
   }
+  L3U_REQUIRE(y_nstride >= 0);   // a rank-1 y is K = 1 (above)
 #define PWBF(A_, B_) do { if (y) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 1>), grid, block, dlds, \
       stream, dy, dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, N, J, K, S, SCH, nsc); \

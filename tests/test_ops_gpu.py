@@ -235,7 +235,9 @@ def test_pw_bwd_weight(cuda, case):
 
 # fused 1x1-conv backward: (N, J, K, S, with_in_prologue, accumulate)
 PW_BWD_CASES = [
-    (2, 16, 1, 6 * 8 * 10, True, False),       # init block conv1 (K = 1), ragged chunk
+    (2, 16, 1, 6 * 8 * 10, True, False),       # init block conv1 (K = 1, VALU kernel), ragged chunk
+    (1, 16, 1, 48 ** 3, True, False),          # ... at 48^3 (256-voxel chunks)
+    (2, 32, 1, 24 ** 3, True, True),           # ... two 16-row halves (config 5), accumulate
     (2, 16, 16, 12 ** 3, False, False),
     (1, 16, 32, 24 ** 3, True, False),         # up3 conv1 shape class, multi-iteration chunks
     (2, 32, 16, 6 * 6 * 8, False, True),       # shortcut: accumulate into d(input)
