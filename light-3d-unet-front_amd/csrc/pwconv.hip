@@ -605,7 +605,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   constexpr int WS = TK + ((16 - TK) % 64 + 64) % 64;   // >= TK, = 16 mod 64
   constexpr int DS = 68;                                // dY tile row stride (floats)
   constexpr int PS = 8;                                 // lanes per channel for the IN sums
-  static_assert(NK * 256 <= 16 * DS, "weight-gradient reduction must fit in the dY tiles");
+  static_assert(NJ == 2 || NK * 256 <= 16 * DS, "weight-gradient reduction must fit in the dY tiles");
   __shared__ __attribute__((aligned(16))) float w_l[TJ * WS];
   __shared__ __attribute__((aligned(16))) float coef[PRO ? TJ * 8 : 1];
   __shared__ double psum[PRO ? TJ * PS * 2 : 1];
@@ -662,12 +662,20 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       if (j < J && sd < s_hi) yv[jr] = ldv4(yn + (yk ? 0ll : (long long)j * S) + sd);
     }
   }
+  // X (the weight gradient's B operand) is requested here, before the small operands, when the
+  // registers allow (XL); the wide tails (TJ = 32, TK = 64) request it after forming dY, so that
+  // the dY / out / y registers are dead by then (VGPRs: 2 -> 3 waves per SIMD) and its loads
+  // overlap the data-gradient MFMAs and stores
+  constexpr bool XL = !(PRO != 0 && NJ == 2);
   f4 xv[4][NK];
+  auto load_xv = [&] {
 #pragma unroll
-  for (int gg = 0; gg < 4; ++gg)
+    for (int gg = 0; gg < 4; ++gg)
 #pragma unroll
-    for (int b = 0; b < NK; ++b)
-      xv[gg][b] = load_x4<true, false>(xn, k0 + 16 * b + lr, K, sw + 16 * gg + 4 * lk, s_hi, S, 0, 0);
+      for (int b = 0; b < NK; ++b)
+        xv[gg][b] = load_x4<true, false>(xn, k0 + 16 * b + lr, K, sw + 16 * gg + 4 * lk, s_hi, S, 0, 0);
+  };
+  if constexpr (XL) load_xv();
 
   // 2. ... then the small per-workgroup operands: the weight slice and (PRO) the per-channel
   // InstanceNorm-backward coefficients, whose fp64 partial sums are spread over PS lanes per
@@ -727,10 +735,16 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       for (int q = 0; q < 4; ++q) g[jr][q] = ok ? f * (g[jr][q] - M1 - (yv[jr][q] - mu) * rs * M2) : 0.f;
     }
   }
-  float* tile = dyt_lds + (size_t)wave * TJ * DS;
+  // the wave's dY tile: all TJ rows, or (TJ = 32) 16 rows at a time, written again for the second
+  // half after the first half's weight-gradient reads (half the LDS: at 64^3 three -> four
+  // workgroups per CU)
+  constexpr int TR = NJ == 2 ? 16 : TJ;   // rows of the wave's LDS tile
+  float* tile = dyt_lds + (size_t)wave * TR * DS;
 #pragma unroll
-  for (int jr = 0; jr < JR; ++jr)
+  for (int jr = 0; jr < TR / 4; ++jr)
     *reinterpret_cast<f4*>(tile + (4 * jr + lk) * DS + 4 * lr) = g[jr];
+
+  if constexpr (!XL) load_xv();
 
   // 4. data gradient, one 16-row tile of dX at a time, from the registers
 #pragma unroll
@@ -765,44 +779,103 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   for (int a = 0; a < NJ; ++a)
 #pragma unroll
     for (int b = 0; b < NK; ++b) gw[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+  auto wgrad = [&](auto A) {   // rows 16 a .. 16 a + 15 of the dY tile (16 a - TJ + TR in LDS)
+    constexpr int a = decltype(A)::value;
+    constexpr int ar = TR == TJ ? a : 0;
 #pragma unroll
-  for (int gg = 0; gg < 4; ++gg) {
-    f4 av[NJ];
+    for (int gg = 0; gg < 4; ++gg) {
+      const f4 av = *reinterpret_cast<const f4*>(tile + (16 * ar + lr) * DS + 16 * gg + 4 * lk);
 #pragma unroll
-    for (int a = 0; a < NJ; ++a)
-      av[a] = *reinterpret_cast<const f4*>(tile + (16 * a + lr) * DS + 16 * gg + 4 * lk);
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+        for (int b = 0; b < NK; ++b) gw[a][b] = mfma4(av[q], xv[gg][b][q], gw[a][b]);
+    }
+  };
+  if constexpr (TR == TJ) {
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      f4 av[NJ];
 #pragma unroll
       for (int a = 0; a < NJ; ++a)
+        av[a] = *reinterpret_cast<const f4*>(tile + (16 * a + lr) * DS + 16 * gg + 4 * lk);
 #pragma unroll
-        for (int b = 0; b < NK; ++b) gw[a][b] = mfma4(av[a][q], xv[gg][b][q], gw[a][b]);
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int a = 0; a < NJ; ++a)
+#pragma unroll
+          for (int b = 0; b < NK; ++b) gw[a][b] = mfma4(av[a][q], xv[gg][b][q], gw[a][b]);
+    }
+  } else {
+    wgrad(std::integral_constant<int, 0>{});
+    // the second 16 rows into the same tile once this wave's reads of the first are done
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr)
+      *reinterpret_cast<f4*>(tile + (4 * jr + lk) * DS + 4 * lr) = g[4 + jr];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wgrad(std::integral_constant<int, 1>{});
   }
 
-  // 6. fixed-order cross-wave reduction (reuses the dY tiles): every wave parks its partial
-  // tile, wave 0 adds them in wave order
-  __syncthreads();
+  // 6. fixed-order cross-wave reduction (reuses the dY tiles), in wave order: every wave parks
+  // its partial tile and wave 0 adds them; with the half tiles the waves add into one buffer in
+  // turn (the same order and sums)
   float* red = dyt_lds;
-#pragma unroll
-  for (int a = 0; a < NJ; ++a)
-#pragma unroll
-    for (int b = 0; b < NK; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[((wave * NJ + a) * NK + b) * 256 + r * 64 + l] = gw[a][b][r];
-  __syncthreads();
-  if (wave == 0) {
-    float* o = part + (long long)blockIdx.x * J * K;
+  if constexpr (TR == TJ) {
+    __syncthreads();
 #pragma unroll
     for (int a = 0; a < NJ; ++a)
 #pragma unroll
       for (int b = 0; b < NK; ++b)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = red[(a * NK + b) * 256 + r * 64 + l];
-          for (int wv = 1; wv < nwv; ++wv) v += red[((wv * NJ + a) * NK + b) * 256 + r * 64 + l];
-          const int jj = 16 * a + 4 * lk + r, kk = k0 + 16 * b + lr;
-          if (jj < J && kk < K) o[(long long)jj * K + kk] = v;
-        }
+        for (int r = 0; r < 4; ++r) red[((wave * NJ + a) * NK + b) * 256 + r * 64 + l] = gw[a][b][r];
+    __syncthreads();
+    if (wave == 0) {
+      float* o = part + (long long)blockIdx.x * J * K;
+#pragma unroll
+      for (int a = 0; a < NJ; ++a)
+#pragma unroll
+        for (int b = 0; b < NK; ++b)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = red[(a * NK + b) * 256 + r * 64 + l];
+            for (int wv = 1; wv < nwv; ++wv) v += red[((wv * NJ + a) * NK + b) * 256 + r * 64 + l];
+            const int jj = 16 * a + 4 * lk + r, kk = k0 + 16 * b + lr;
+            if (jj < J && kk < K) o[(long long)jj * K + kk] = v;
+          }
+    }
+  } else {
+    static_assert(NJ * NK * 256 <= 4 * 16 * DS, "the reduction buffer fits the tiles of 4 waves");
+    for (int wv = 0; wv < nwv; ++wv) {
+      __syncthreads();
+      if (wave == wv) {
+#pragma unroll
+        for (int a = 0; a < NJ; ++a)
+#pragma unroll
+          for (int b = 0; b < NK; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int i = ((a * NK + b) * 4 + r) * 64 + l;
+              red[i] = wv == 0 ? gw[a][b][r] : red[i] + gw[a][b][r];
+            }
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
+      float* o = part + (long long)blockIdx.x * J * K;
+#pragma unroll
+      for (int a = 0; a < NJ; ++a)
+#pragma unroll
+        for (int b = 0; b < NK; ++b)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int jj = 16 * a + 4 * lk + r, kk = k0 + 16 * b + lr;
+            if (jj < J && kk < K) o[(long long)jj * K + kk] = red[((a * NK + b) * 4 + r) * 64 + l];
+          }
+    }
   }
 }
 
@@ -1576,7 +1649,7 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
-  const size_t dlds = (size_t)nwv * 16 * NJ * 68 * sizeof(float);   // dY tiles (DS = 68)
+  const size_t dlds = (size_t)max(nwv, 4) * 16 * 68 * sizeof(float);   // 16-row dY tiles (DS = 68)
 #define PWBT0(A_, B_, R_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2, R_>), grid, block, dlds, stream, \
       dout, dout_nstride, yr, yr_nstride, rec, tail_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel, dscale, dpool, dpns, pidx, Hf, Wf)
@@ -1622,7 +1695,7 @@ int pw_bwd_tail_pair_impl(const float* dout, long long dout_nstride, const float
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK), 2), block(64 * nwv);
-  const size_t dlds = (size_t)nwv * 16 * NJ * 68 * sizeof(float);   // dY tiles (DS = 68)
+  const size_t dlds = (size_t)max(nwv, 4) * 16 * 68 * sizeof(float);   // 16-row dY tiles (DS = 68)
 #define PWTP0(A_, B_, R_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2, false, R_>), grid, block, dlds, stream, \
       dout, dout_nstride, a.yr, a.yrns, a.rec, tail_part, npart, a.x, a.xns, a.w, a.dx, a.dxns, \
       a.accumulate, a.part, N, J, a.K, S, SCH, nsc, out, out_nstride, a.sel, dscale, dpool, dpns, pidx, \
@@ -1676,7 +1749,7 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);   // one sweep of the chunk per workgroup
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
-  const size_t dlds = (size_t)nwv * 16 * NJ * 68 * sizeof(float);   // dY tiles (DS = 68)
+  const size_t dlds = (size_t)max(nwv, 4) * 16 * 68 * sizeof(float);   // 16-row dY tiles (DS = 68)
   // one input channel with the IN prologue (the first block's conv1.pointwise, y materialised or
   // rank-1): the VALU kernel, same chunks and partial layout
   if (K == 1 && y != nullptr && SCH <= 512 && J <= 32) {
