@@ -662,11 +662,11 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       if (j < J && sd < s_hi) yv[jr] = ldv4(yn + (yk ? 0ll : (long long)j * S) + sd);
     }
   }
-  // X (the weight gradient's B operand) is requested here, before the small operands, when the
-  // registers allow (XL); the wide tails (TJ = 32, TK = 64) request it after forming dY, so that
-  // the dY / out / y registers are dead by then (VGPRs: 2 -> 3 waves per SIMD) and its loads
-  // overlap the data-gradient MFMAs and stores
-  constexpr bool XL = !(PRO != 0 && NJ == 2);
+  // X (the weight gradient's B operand): with a prologue (PRO 1 / 2) it is requested after dY is
+  // formed, so that the dY / out / y registers are dead by then (TJ = 32, TK = 64: 226 -> 166
+  // VGPRs, 2 -> 3 waves per SIMD; TJ = 16: 4 -> 5 for the IN-prologue forms) and its loads
+  // overlap the data-gradient MFMAs and stores (config 5 -175 us, 48^3 -18 us); PRO 0 first
+  constexpr bool XL = PRO == 0;
   f4 xv[4][NK];
   auto load_xv = [&] {
 #pragma unroll
