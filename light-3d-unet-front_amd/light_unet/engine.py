@@ -64,7 +64,7 @@ _FUSE_ADAMW = os.environ.get("L3U_FUSE_ADAMW", "1") != "0"
 # the last block's tail-backward partials out of the out_conv backward's pass over its output
 # (l3u_outconv_bwd_tail: no l3u_norm_act_bwd_reduce launch, no second read of dout / out / y2 /
 # r); L3U_OC_TAIL=0 keeps the separate reduce
-_OC_TAIL = os.environ.get("L3U_OC_TAIL", "0") != "0"
+_OC_TAIL = os.environ.get("L3U_OC_TAIL", "1") != "0"
 
 
 def _items_cover_once(items, numel):
