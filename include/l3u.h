@@ -345,29 +345,6 @@ int l3u_outconv_bwd_ftl_dz(const float* p, const float* t, const float* ftl_part
                            const float* gscale, const float* h, long long h_nstride,
                            const float* w, float* dh, long long dh_nstride, double* part,
                            float* loss, int N, int C, int S, hipStream_t stream);
-/* All four forms above in one entry (dp != NULL: given dL/dp; else t with the global sums, or with
- * the forward's FocalTversky partials when sums == NULL; dz_only: dz instead of dh), and, with
- * tail != NULL, the last block's tail-backward partials from the same pass (h is that block's
- * output; unet3d.py:89-93): with g[c] = w[c] * dz * lrelu'(h[c]),
- *   tail->part[C][N][l3u_outconv_nblocks(S)][3] (fp64) = {sum g, sum g*xhat2, sum g*xhat_r}
- * -- the l3u_norm_act_bwd_reduce[_r1] partials (its xhat from the y2 / r records), in this
- * kernel's workgroups instead of that launch's second read of dout, out, y2 and r.  C <= 16,
- * S % 4 == 0; y2 / r are [N][C][S] tensors of the entry's storage type (fp32 / bf16 twin).     */
-typedef struct l3u_tail_src {
-  const void* y2;
-  long long y2_nstride;
-  const float* rec2;
-  const void* r;
-  long long r_nstride;
-  const float* rec_r;
-  double* part;
-} l3u_tail_src;
-int l3u_outconv_bwd_tail(const float* dp, const float* p, const float* t, const double* sums,
-                         const float* ftl_part, int ftl_nparts, double alpha, double beta,
-                         double gamma, double smooth, const float* gscale, const float* h,
-                         long long h_nstride, const float* w, float* dh, long long dh_nstride,
-                         int dz_only, double* part, float* loss, const l3u_tail_src* tail, int N,
-                         int C, int S, hipStream_t stream);
 
 /* ---- Training patches (light_unet/datasets/patch_dataset.py:114-220) -----------------------
  * One record per patch: the case volume it is cut from (device pointers, [sd][sh][sw] fp32), the
@@ -580,12 +557,6 @@ int l3u_outconv_bwd_ftl_bf16(const float* p, const float* t, const float* ftl_pa
                              const float* gscale, const l3u_bf16* h, long long h_nstride,
                              const float* w, float* dh, long long dh_nstride, double* part,
                              float* loss, int N, int C, int S, hipStream_t stream);
-int l3u_outconv_bwd_tail_bf16(const float* dp, const float* p, const float* t, const double* sums,
-                              const float* ftl_part, int ftl_nparts, double alpha, double beta,
-                              double gamma, double smooth, const float* gscale, const l3u_bf16* h,
-                              long long h_nstride, const float* w, float* dh, long long dh_nstride,
-                              int dz_only, double* part, float* loss, const l3u_tail_src* tail,
-                              int N, int C, int S, hipStream_t stream);
 int l3u_outconv_bwd_dz_bf16(const float* dp, const float* p, const float* t, const double* sums,
                             double alpha, double beta, double gamma, double smooth,
                             const float* gscale, const l3u_bf16* h, long long h_nstride,

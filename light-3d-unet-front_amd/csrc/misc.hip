@@ -181,23 +181,16 @@ L3U_DEV void ftl_lane_sums(const float* __restrict__ part, int nb, double& a, do
   c = wave_sum_d(c);
 }
 
-// TAIL: the last block's tail-backward partials come out of the same pass (l3u_outconv_bwd_tail):
-// with g[c] = w[c] dz lrelu'(h[c]) (h = the block output), tpart[c][n][blk] = {sum g,
-// sum g xhat2, sum g xhat_r} in fp64 (xhat from the y2 / r records) -- what
-// l3u_norm_act_bwd_reduce[_r1] computes from a second read of dout, out, y2 and r
-template <typename T, bool VEC, bool TAIL = false>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     int dz_only, const float* __restrict__ dp, const float* __restrict__ p, const float* __restrict__ t,
     const double* __restrict__ sums, double alpha, double beta, double gamma, double smooth,
     const float* __restrict__ gscale, const T* __restrict__ h, long long hns,
     const float* __restrict__ w, float* __restrict__ dh, long long dhns,
     double* __restrict__ part, float* __restrict__ loss, int C, int S,
-    const float* __restrict__ fpart = nullptr, int fnp = 0, const T* __restrict__ ty2 = nullptr,
-    long long ty2ns = 0, const float* __restrict__ trec2 = nullptr, const T* __restrict__ tr = nullptr,
-    long long trns = 0, const float* __restrict__ trecr = nullptr, double* __restrict__ tpart = nullptr,
-    int N = 0) {
+    const float* __restrict__ fpart = nullptr, int fnp = 0) {
   L3U_STAMP_SCOPE(404);
-  extern __shared__ double redd[];   // [4][C+1] (TAIL: [4][C+1 + 3C])
+  extern __shared__ double redd[];   // [4][C+1]
   const int n = blockIdx.y, nb = gridDim.x;
   const T* hp = h + (long long)n * hns;
   float* dhp = dh + (long long)n * dhns;
@@ -206,37 +199,18 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
   // VEC: the streamed operands (p, t or dp, the C channels of h) are requested first, so their
   // latency overlaps the FocalTversky prologue below
   f4 pv4 = {0.f, 0.f, 0.f, 0.f}, gv4 = {0.f, 0.f, 0.f, 0.f};
-  constexpr int CM = TAIL ? 16 : 32;   // channels held (TAIL: C <= 16, the launcher checks)
-  f4 hv[VEC ? CM : 1];
+  f4 hv[VEC ? 32 : 1];
   if (VEC) {
     if (i0 < S) {
       pv4 = ldv4(p + o + i0);
       gv4 = ldv4((dp ? dp : t) + o + i0);
     }
 #pragma unroll
-    for (int c = 0; c < CM; ++c) {
+    for (int c = 0; c < 32; ++c) {
       hv[c] = f4{0.f, 0.f, 0.f, 0.f};
       if (c < C && i0 < S) hv[c] = ldv4(hp + (long long)c * S + i0);
     }
   }
-  // TAIL: y2 / r of 8 channels at a time (the first 8 requested with the streamed operands; the
-  // next 8 into the same registers once the first are used: two waves per SIMD instead of one)
-  constexpr int TB = TAIL ? 8 : 1;
-  f4 y2v[TB], rv[TB];
-  auto tail_load = [&](int c0) {
-    const T* yp = ty2 + (long long)n * ty2ns;
-    const T* rp = tr + (long long)n * trns;
-#pragma unroll
-    for (int b = 0; b < TB; ++b) {
-      const int c = c0 + b;
-      y2v[b] = rv[b] = f4{0.f, 0.f, 0.f, 0.f};
-      if (c < C && i0 < S) {
-        y2v[b] = ldv4(yp + (long long)c * S + i0);
-        rv[b] = ldv4(rp + (long long)c * S + i0);
-      }
-    }
-  };
-  if (TAIL) tail_load(0);
   float cA = 0.f, cB = 0.f;
   if (dp == nullptr) {
     // every wave forms the coefficients itself (no LDS hand-off, no barrier).  fpart: the
@@ -264,10 +238,10 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
       dz[q] = g * pv * (1.f - pv);
     }
   }
-  float acc[CM + 1];
+  float acc[33];
 #pragma unroll
-  for (int c = 0; c < CM + 1; ++c) acc[c] = 0.f;
-  acc[CM] = (dz[0] + dz[1]) + (dz[2] + dz[3]);
+  for (int c = 0; c < 33; ++c) acc[c] = 0.f;
+  acc[32] = (dz[0] + dz[1]) + (dz[2] + dz[3]);
   if (dz_only) {   // d(pre-sigmoid) only: the consumers form dh[c] = w[c] * dz on the fly
     if (VEC) {
       if (i0 < S) stv4(dhp + i0, dz);
@@ -278,7 +252,7 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     }
   }
 #pragma unroll
-  for (int c = 0; c < CM; ++c) {
+  for (int c = 0; c < 32; ++c) {
     if (c < C) {
       if (VEC) {
         if (i0 < S) {
@@ -297,55 +271,18 @@ __global__ __launch_bounds__(256) void outconv_bwd_kernel(
     }
   }
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int RW = TAIL ? 4 * C + 1 : C + 1;   // doubles per wave in redd
 #pragma unroll
-  for (int c = 0; c < CM + 1; ++c) {
-    if (c < C || c == CM) {
+  for (int c = 0; c < 33; ++c) {
+    if (c < C || c == 32) {
       const double r = wave_sum_d((double)acc[c]);
-      if (l == 0) redd[wv * RW + (c == CM ? C : c)] = r;
-    }
-  }
-  if (TAIL) {
-    // the tail sums of the thread's 4 voxels per channel (fp64 products as the reduce kernel
-    // forms them), then a wave sum per channel and quantity
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const int b = c & 7;
-      if (c == 8 && C > 8) tail_load(8);   // uniform
-      if (c < C) {
-        const float m2 = trec2[((long long)n * C + c) * kRec + 0], rs2 = trec2[((long long)n * C + c) * kRec + 1];
-        const float mr = trecr[((long long)n * C + c) * kRec + 0], rsr = trecr[((long long)n * C + c) * kRec + 1];
-        const float wc = w[c];
-        double t0 = 0.0, t1 = 0.0, t2 = 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (i0 + q < S) {
-            const float g = (wc * dz[q]) * lrelu_d(VEC ? hv[c][q] : 0.f);
-            t0 += g;
-            t1 += (double)g * ((y2v[b][q] - m2) * rs2);
-            t2 += (double)g * ((rv[b][q] - mr) * rsr);
-          }
-        }
-        t0 = wave_sum_d(t0);
-        t1 = wave_sum_d(t1);
-        t2 = wave_sum_d(t2);
-        if (l == 0) {
-          double* o = redd + wv * RW + C + 1 + 3 * c;
-          o[0] = t0; o[1] = t1; o[2] = t2;
-        }
-      }
+      if (l == 0) redd[wv * (C + 1) + (c == 32 ? C : c)] = r;
     }
   }
   __syncthreads();
   if (threadIdx.x <= C) {
     const int tt = threadIdx.x;
-    const double r = (redd[tt] + redd[RW + tt]) + (redd[2 * RW + tt] + redd[3 * RW + tt]);
+    const double r = (redd[tt] + redd[(C + 1) + tt]) + (redd[2 * (C + 1) + tt] + redd[3 * (C + 1) + tt]);
     part[((long long)n * nb + blockIdx.x) * (C + 1) + tt] = r;
-  }
-  if (TAIL && threadIdx.x >= 64 && threadIdx.x < 64 + 3 * C) {
-    const int tt = threadIdx.x - 64, c = tt / 3, k = tt % 3, i = C + 1 + tt;
-    const double r = (redd[i] + redd[RW + i]) + (redd[2 * RW + i] + redd[3 * RW + i]);
-    tpart[(((long long)c * N + n) * nb + blockIdx.x) * 3 + k] = r;
   }
 }
 
@@ -852,23 +789,11 @@ int outconv_bwd_impl(const float* dp, const float* p, const float* t, const doub
                      double alpha, double beta, double gamma, double smooth, const float* gscale,
                      const T* h, long long h_nstride, const float* w, float* dh, long long dh_nstride,
                      double* part, float* loss, int N, int C, int S, hipStream_t stream,
-                     const float* fpart = nullptr, int fnp = 0, int dz_only = 0,
-                     const l3u_tail_src* tail = nullptr) {
+                     const float* fpart = nullptr, int fnp = 0, int dz_only = 0) {
   L3U_REQUIRE(N > 0 && C > 0 && C <= 32 && S > 0);
   L3U_REQUIRE(dp != nullptr || (t != nullptr && (sums != nullptr || (fpart != nullptr && fnp > 0))));
   const bool vec = S % 4 == 0 && h_nstride % 4 == 0 && dh_nstride % 4 == 0;
   dim3 grid((S + 1023) / 1024, N);
-  if (tail != nullptr) {
-    L3U_REQUIRE(vec && C <= 16 && tail->y2 && tail->rec2 && tail->r && tail->rec_r && tail->part &&
-                tail->y2_nstride % 4 == 0 && tail->r_nstride % 4 == 0);
-    const size_t lds = 4 * (4 * C + 1) * sizeof(double);
-    hipLaunchKernelGGL((outconv_bwd_kernel<T, true, true>), grid, dim3(256), lds, stream, dz_only, dp, p,
-                       t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride,
-                       part, loss, C, S, fpart, fnp, static_cast<const T*>(tail->y2), tail->y2_nstride,
-                       tail->rec2, static_cast<const T*>(tail->r), tail->r_nstride, tail->rec_r,
-                       tail->part, N);
-    L3U_CHECK_LAUNCH();
-  }
   const size_t lds = 4 * (C + 1) * sizeof(double);
   if (vec) hipLaunchKernelGGL((outconv_bwd_kernel<T, true>), grid, dim3(256), lds, stream, dz_only, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S, fpart, fnp);
   else hipLaunchKernelGGL((outconv_bwd_kernel<T, false>), grid, dim3(256), lds, stream, dz_only, dp, p, t, sums, alpha, beta, gamma, smooth, gscale, h, h_nstride, w, dh, dh_nstride, part, loss, C, S, fpart, fnp);
@@ -929,14 +854,6 @@ L3U_TWIN(l3u_outconv_bwd_dz, P_OCB, outconv_bwd_impl(dp, p, t, sums, alpha, beta
 L3U_TWIN(l3u_outconv_bwd_ftl_dz, P_OCBF, outconv_bwd_impl((const float*)nullptr, p, t,
          (const double*)nullptr, alpha, beta, gamma, smooth, gscale, bp(h), h_nstride, w, dh, dh_nstride,
          part, loss, N, C, S, stream, ftl_part, ftl_nparts, 1))
-#define P_OCBT(TT) (const float* dp, const float* p, const float* t, const double* sums,            \
-    const float* ftl_part, int ftl_nparts, double alpha, double beta, double gamma, double smooth,   \
-    const float* gscale, const TT* h, long long h_nstride, const float* w, float* dh,               \
-    long long dh_nstride, int dz_only, double* part, float* loss, const l3u_tail_src* tail, int N,   \
-    int C, int S, hipStream_t stream)
-L3U_TWIN(l3u_outconv_bwd_tail, P_OCBT, outconv_bwd_impl(dp, p, t, sums, alpha, beta, gamma, smooth,
-         gscale, bp(h), h_nstride, w, dh, dh_nstride, part, loss, N, C, S, stream, ftl_part, ftl_nparts,
-         dz_only, tail))
 template <typename T>
 int box_copy_impl(const T* src, long long sns, int sd, int sh, int sw, T* dst, long long dns, int dd,
                   int dh, int dw, int oz, int oy, int ox, int N, int C, hipStream_t stream) {

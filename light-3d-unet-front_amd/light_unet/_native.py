@@ -89,7 +89,6 @@ _SIGS = {
     "l3u_cast_bf16_f32": [P, P, L, P],
     "l3u_outconv_bwd_dz": [P, P, P, P, D, D, D, D, P, P, L, P, P, L, P, P, I, I, I, P],
     "l3u_outconv_bwd_ftl_dz": [P, P, P, I, D, D, D, D, P, P, L, P, P, L, P, P, I, I, I, P],
-    "l3u_outconv_bwd_tail": [P, P, P, P, P, I, D, D, D, D, P, P, L, P, P, L, I, P, P, P, I, I, I, P],
     "l3u_norm_act_bwd_reduce_r1": [P, L, P, P, L, P, L, P, P, L, P, P, I, I, I, P],
     "l3u_pw_bwd_tail_r1": [P, L, P, P, L, P, L, P, P, I, I, P, L, P, P, L, I, P, I, I, I, I, P],
     "l3u_norm_act_bwd_reduce_up": [P, L, P, L, P, P, L, P, L, P, P, L, P, P, I, I, I, I, I, P],
@@ -110,7 +109,7 @@ BF16_TWINS = ("l3u_dw3_fwd", "l3u_dw3_bwd", "l3u_pw_fwd", "l3u_pw_fwd2", "l3u_pw
               "l3u_outconv_bwd_ftl", "l3u_box_copy",
               "l3u_front_fwd", "l3u_dwpw_fwd", "l3u_outconv_bwd_dz", "l3u_outconv_bwd_ftl_dz",
               "l3u_norm_act_bwd_reduce_r1", "l3u_pw_bwd_tail_r1", "l3u_norm_act_bwd_reduce_up",
-              "l3u_pw_bwd_tail_up", "l3u_outconv_bwd_tail")
+              "l3u_pw_bwd_tail_up")
 for _n in BF16_TWINS:
     _SIGS[_n + "_bf16"] = _SIGS[_n]
 # query helpers that return a value instead of an error code
@@ -133,13 +132,6 @@ class NormSrc(ctypes.Structure):
     record from.  Pass `norm_src_ptr(s)`; keep the object alive across the call."""
     _fields_ = [("stat_part", P), ("nsb", I), ("layer", I), ("gamma", P), ("beta", P),
                 ("drop_p", F), ("seed", U64), ("step", P), ("rec_out", P), ("rank1", P)]
-
-
-class TailSrc(ctypes.Structure):
-    """struct l3u_tail_src (include/l3u.h): the last block's tail operands for
-    l3u_outconv_bwd_tail.  Pass `ctypes.pointer(s)`; keep the object alive across the call."""
-    _fields_ = [("y2", P), ("y2_nstride", L), ("rec2", P), ("r", P), ("r_nstride", L),
-                ("rec_r", P), ("part", P)]
 
 
 class AugParam(ctypes.Structure):

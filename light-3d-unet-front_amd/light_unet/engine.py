@@ -61,10 +61,6 @@ _FRONT_R1 = os.environ.get("L3U_FRONT_R1", "1") != "0"
 # parameters it produces (l3u_reduce_segments_adamw: no separate l3u_adamw_tick launch);
 # L3U_FUSE_ADAMW=0 keeps the two launches
 _FUSE_ADAMW = os.environ.get("L3U_FUSE_ADAMW", "1") != "0"
-# the last block's tail-backward partials out of the out_conv backward's pass over its output
-# (l3u_outconv_bwd_tail: no l3u_norm_act_bwd_reduce launch, no second read of dout / out / y2 /
-# r); L3U_OC_TAIL=0 keeps the separate reduce
-_OC_TAIL = os.environ.get("L3U_OC_TAIL", "1") != "0"
 
 
 def _items_cover_once(items, numel):
@@ -234,7 +230,6 @@ class UNetEngine:
         # parameters, records and partial sums stay fp32 either way
         self.act_dtype = torch.float32
         self._grad_phase = False   # backward: gradient buffers are fp32 in either storage mode
-        self._tail_pre = {}        # backward: block tails whose partials an earlier launch made
 
     # ------------------------------------------------------------------ helpers
     @property
@@ -722,34 +717,7 @@ class UNetEngine:
         nb = nat.query("l3u_outconv_nblocks", S[0])
         po = A.alloc(2 * N * nb * (c0 + 1))          # fp64 partials
         loss_ptr = None
-        # the last block's tail partials from the same pass (its output is out_conv's input)
-        self._tail_pre = {}
-        tail = None
-        if (_OC_TAIL and self.kinds["up3.res_block."][0][0] == "ds" and c0 <= 16 and S[0] % 4 == 0
-                and self._tail_fusable(up3, up3["x"].C, c0, S[0]) and up3["r"].scale is None
-                and up3["r"].ns % 4 == 0 and h.ns % 4 == 0):
-            pn = A.alloc(2 * c0 * N * nb * 3)            # fp64 partials [C][N][nb][3]
-            self._tail_pre["up3.res_block."] = (pn, nb)
-            tail = nat.TailSrc(up3["y2"].data_ptr(), c0 * S[0], up3["recs"][2].data_ptr(), up3["r"].p,
-                               up3["r"].ns, up3["recs"][0].data_ptr(), A.ptr(pn))
-        if tail is not None:
-            # one entry for the given-dL/dp and the FocalTversky forms
-            if dp is not None:
-                args = (dp.data_ptr(), sv["p"].data_ptr(), None, None, None, 0, 0.0, 0.0, 0.0, 0.0)
-            else:
-                t, sums, (alpha, beta, gamma, smooth) = ftl[:3]
-                if len(ftl) > 3 and ftl[3] is not None:
-                    loss_ptr = ftl[3].data_ptr()
-                if sums is None:
-                    args = (None, sv["p"].data_ptr(), t.data_ptr(), None, ftl[4].data_ptr(), ftl[5],
-                            alpha, beta, gamma, smooth)
-                else:
-                    args = (None, sv["p"].data_ptr(), t.data_ptr(), sums.data_ptr(), None, 0,
-                            alpha, beta, gamma, smooth)
-            self._call("l3u_outconv_bwd_tail", *args, None, h.p, h.ns,
-                       self._w(flat, "out_conv.weight"), dh.data_ptr(), dhns, 1 if r1 else 0,
-                       A.ptr(po), loss_ptr, nat.norm_src_ptr(tail), N, c0, S[0], st)
-        elif dp is not None:
+        if dp is not None:
             g = (dp.data_ptr(), None, None, 0.0, 0.0, 0.0, 0.0, None)
             self._call("l3u_outconv_bwd" + sfx, g[0], sv["p"].data_ptr(), *g[1:], h.p, h.ns,
                        self._w(flat, "out_conv.weight"), dh.data_ptr(), dhns, A.ptr(po),
@@ -866,20 +834,14 @@ class UNetEngine:
         shortcut = sv["shortcut"]
         rv = sv["r"] if shortcut else sv["x"]
         y2 = sv["y2"]
-        pre_done = self._tail_pre.get(pre) if fused else None   # from l3u_outconv_bwd_tail
-        if pre_done is not None:
-            pn, nb = pre_done
-        else:
-            nb = nat.query("l3u_norm_act_nblocks", S)
-            pn = A.alloc(2 * cout * N * nb * 3)        # fp64 partials
+        nb = nat.query("l3u_norm_act_nblocks", S)
+        pn = A.alloc(2 * cout * N * nb * 3)            # fp64 partials
         pnd = pn // 2
         self._seg(pnd + 1, N * nb, 3, N * nb * 3, cout, pre + "norm2.weight", f64=1)
         self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "norm2.bias", f64=1)
         if fused:
             self._seg(pnd + 2, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.weight", f64=1)
             self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.bias", f64=1)
-            if pre_done is not None:
-                return pn, nb
             if dout.scale is not None:   # rank-1 dout (l3u_outconv_bwd_dz)
                 self._call("l3u_norm_act_bwd_reduce_r1", dout.p, dout.ns, dout.scale, out.p, out.ns,
                            y2.data_ptr(), cout * S, rec2, rv.p, rv.sns, rec_r, A.ptr(pn), N, cout, S,
