@@ -284,7 +284,7 @@ def test_pw_bwd_tail_twin(cuda, case):
 
 
 @pytest.mark.parametrize("case", [(4, 128, 64, 6, 6, 6), (4, 64, 32, 12, 12, 12), (4, 32, 16, 24, 24, 24),
-                                  (1, 8, 4, 5, 7, 9)])
+                                  (1, 8, 4, 5, 7, 9), (2, 128, 64, 16, 16, 16)])
 def test_convt_twin(cuda, case):
     N, Ci, Co, D, H, W = case
     Si = D * H * W
