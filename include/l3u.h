@@ -67,8 +67,9 @@ typedef struct l3u_norm_src {
 /* Rank-1 operands (the first block's y1 = w1[c] * z1 and r = wsc[c] * x, unet3d.py:163-167 with
  * one input channel): a NEGATIVE batch stride (-ns) on the normalised operand of
  *   l3u_dwpw_fwd (x, with src/rec), l3u_norm_act_fwd / l3u_norm_act_pool_fwd (r),
- *   l3u_norm_act_bwd_reduce[_r1|_up] (r), l3u_pw_bwd (y), l3u_pw_bwd_tail[_r1|_up] (yr) and
- *   l3u_dw3_bwd (x, with rec)
+ *   l3u_norm_act_bwd_reduce[_r1|_up] (r), l3u_pw_bwd (y), l3u_pw_bwd_tail[_r1|_up] (yr),
+ *   l3u_dw3_bwd (x, with rec) and l3u_dw3_fwd (x, with rec or src; the shapes of
+ *   l3u_dw3_bwd_rank1)
  * means that operand holds ONE channel per sample (batch stride ns) and channel c is
  * record[c][7] * it, the float product the materialised tensor would hold (bit for bit).  The
  * record's slot 7 is set when it is finalized from an l3u_norm_src with rank1 != NULL.  fp32
@@ -80,7 +81,8 @@ typedef struct l3u_norm_src {
  * w: [C][27].  rec != NULL fuses a = lrelu(scale*(x-mean) + shift) into the input load (the
  * InstanceNorm1 + LeakyReLU + Dropout3d that precede conv2.depthwise, unet3d.py:84-89).      */
 int l3u_dw3_nchunk(int N, int C, int D, int H, int W);   /* z/y chunks per (n, c) */
-int l3u_dw3_bwd_rank1(int N, int C, int D, int H, int W); /* 1: l3u_dw3_bwd takes a rank-1 x */
+int l3u_dw3_bwd_rank1(int N, int C, int D, int H, int W); /* 1: l3u_dw3_bwd and l3u_dw3_fwd
+                                                             take a rank-1 x at this shape */
 int l3u_dw3_fwd(const float* x, long long x_nstride, const float* w, const float* rec,
                 const l3u_norm_src* src, float* y, long long y_nstride, int N, int C, int D,
                 int H, int W, hipStream_t stream);   /* src != NULL: finalize rec in-kernel */

@@ -294,6 +294,10 @@ static bool convt_tile_shape(int N, int Ci, int Co, int D, int H, int W, ConvtTi
     return false;
   const long long S = (long long)D * H * W;
   if (W % 2 != 0 || S % 4 != 0 || S > (1ll << 26)) return false;
+  // dY is read through a buffer descriptor over one sample (32-bit num_records, voffset and
+  // soffset): every byte offset of the sample's Co * 8 * S floats must stay below 2^31, otherwise
+  // the loads past the limit return 0 silently (the three-launch path takes such volumes)
+  if ((long long)Co * 32 * S >= (1ll << 31)) return false;
   const int PP = D * H * (W / 2);
   // 16 input channels per block; 2 blocks per workgroup (up to 32 channels) with 32-pair tiles,
   // 4 blocks with 16-pair tiles for the wider layers (same LDS footprint) when the volume has

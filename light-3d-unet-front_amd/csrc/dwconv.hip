@@ -1106,6 +1106,208 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Forward stencil on the single pass's machinery (l3u_dw3_fwd, planes >= 12^2, one-wave tiles):
+// the input planes go global -> LDS by LDS-DMA, a ring of PD + 1 plane buffers (no staging VGPRs,
+// a deeper prefetch than dw3q_fwd's two register-staged planes), and the 27 tap products per voxel
+// issue mostly as v_pk_fma_f32: output planes (zi-1, zi) of a voxel are one accumulator PAIR,
+// multiplied by the tap pair (kd 2, kd 1) from SGPRs with the neighbour broadcast by op_sel, and
+// plane zi+1 (kd 0) pairs voxels (i, i+1) where the neighbour pair is register-aligned -- the data
+// path of dw3p_bwd_kernel with unflipped taps (24 + 12 packed and 12 scalar FMAs per row quad and
+// input plane, against dw3q_fwd's 36 scalar ones).
+//   XF = 1: the input is transformed on load, a = lrelu(scale*(x-mean)+shift) (IN1 + LeakyReLU +
+//           Dropout3d before conv2.depthwise), applied to the rows read from LDS with packed ops;
+//           rows / planes outside the volume get scale = shift = 0 so the zero page stays a zero
+//           in the A domain; the record is finalized in-kernel when has_src.
+// The output quad is written through a buffer descriptor with an out-of-range offset for lanes
+// that own no voxel, so every wave issues exactly one store per output plane and the DMA waits
+// are exact compile-time counts that include the stores.
+// ------------------------------------------------------------------------------------------------
+constexpr int kDwfPd = 2;   // planes in flight ahead of the one being consumed
+#ifndef L3U_DWF_GL
+#define L3U_DWF_GL 1
+#endif
+constexpr bool kDwfGl = L3U_DWF_GL != 0;   // the forward on dw3g_fwd_kernel (0: dw3q_fwd)
+
+template <int TZC, int NS, int PD>
+constexpr int gf_younger(int s) {   // vm ops younger than plane s's DMAs when step s waits
+  int n = 0;
+  for (int t = s + 1; t <= s + PD && t < TZC + 2; ++t) n += NS;   // DMAs of planes s+1 .. s+PD
+  // stores of steps s-PD .. s-1 (issued after plane s's DMAs, which went out at step s-PD)
+  for (int t = s - PD; t < s; ++t) n += (t >= 2 && t <= TZC + 1) ? 1 : 0;
+  return n;
+}
+
+template <typename T, int XF, int TZC, bool XR1 = false>
+__global__ __launch_bounds__(64) void dw3g_fwd_kernel(
+    const T* __restrict__ x, long long xns, const float* __restrict__ w,
+    const float* __restrict__ rec, l3u_norm_src src, int has_src, T* __restrict__ y,
+    long long yns, int N, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
+  L3U_STAMP_SCOPE(206);
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr bool BH = sizeof(T) == 2;
+  constexpr int NS = BH ? 1 : 2;          // DMA slots per plane
+  constexpr int PD = kDwfPd, GNB = PD + 1;
+  using LT = T;                           // LDS element type of the plane image
+  const int WQ = W >> 2, HW = H * W;
+  const QBlock b = q_decode(C, D, H, RB, RPW, ny, TZ, nz, WQ);
+  const long long cofs = (long long)b.c * D * HW;
+  // XR1 (xns < 0, XF, fp32): a rank-1 input, channel c = rec[c][7] * one stored channel
+  // (include/l3u.h "Rank-1 operands"): the first block's y1 = w1[c] * z1, never materialised
+  const T* xp = x + (long long)b.n * (XR1 ? -xns : xns) + (XR1 ? 0ll : cofs);
+  T* yp = y + (long long)b.n * yns + cofs;
+  const int GPS = BH ? 512 : (RB + 2) * W;   // elements per ring buffer
+  LT* const ring = reinterpret_cast<LT*>(lds);
+  const int zlo = max(0, b.z0 - 1), zhi = min(D - 1, b.z1);
+  auto in_rng = [&](int z) { return z >= zlo && z <= zhi; };
+  const QMap qm = q_map(b.y0, b.rows, H, W, WQ);
+  const float* zpage = g_l3u_zero_page + 4 * (threadIdx.x & 63);
+  int goff2 = 0;
+  bool ok2 = false;
+  if (BH) {   // lane l moves quads 2l, 2l+1 (one row: W % 8 == 0)
+    const int qp = 2 * (int)threadIdx.x, lr2 = qp / WQ, y2 = b.y0 - 1 + lr2;
+    ok2 = qp < (RB + 2) * WQ && y2 >= 0 && y2 < H;
+    goff2 = min(max(y2, 0), H - 1) * W + (qp - lr2 * WQ) * 4;
+  }
+  const int nq = (RB + 2) * WQ;
+  const unsigned lbase = (unsigned)(size_t)lds;
+  auto gissue = [&](auto TI) {   // input plane z0-1+t -> ring buffer t % GNB
+    constexpr int t = decltype(TI)::value;
+    const int zi = b.z0 - 1 + t;
+    const bool in = in_rng(zi);
+    const unsigned bz = lbase + (unsigned)((t % GNB) * GPS) * (unsigned)sizeof(T);
+    if constexpr (BH) {
+      const void* s = (ok2 && in) ? (const void*)(xp + (long long)zi * HW + goff2) : (const void*)zpage;
+      glds16(s, bz);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (k == 1 && (int)threadIdx.x >= nq - 64) continue;
+        const void* s = (qm.ok[k] && in) ? (const void*)(xp + (long long)zi * HW + qm.goff[k]) : (const void*)zpage;
+        glds16(s, bz + k * 1024u);
+      }
+    }
+  };
+  run_steps(gissue, std::make_integer_sequence<int, PD>{});
+  // taps: pair (kd 2, kd 1) and kd 0 per in-plane tap t = r * 3 + dx
+  f2 wp[9];
+  float w0[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    wp[t] = f2{w[b.c * 27 + 18 + t], w[b.c * 27 + 9 + t]};
+    w0[t] = w[b.c * 27 + t];
+  }
+  float sc = 1.f, sh = 0.f, mu = 0.f, rks = 1.f;
+  if (XF) {
+    if (has_src) {
+      float* s8 = lds + (BH ? GNB * 256 : GNB * GPS);
+      block_record(src, b.n, b.c, C, b.ck == 0, s8);
+      mu = s8[0]; sc = s8[2]; sh = s8[3]; rks = s8[7];
+    } else {
+      const float* r = rec + (long long)b.nc * kRec;
+      mu = r[0]; sc = r[2]; sh = r[3]; rks = r[7];
+    }
+  }
+  float rv[3];   // XF: row r of the thread's 3-row window lies inside the volume
+#pragma unroll
+  for (int r = 0; r < 3; ++r) rv[r] = (unsigned)(b.y0 + b.oy + r - 1) < (unsigned)H ? 1.f : 0.f;
+  // the output store: quad (oy, ox) of plane zf; lanes owning no voxel get an offset past the
+  // descriptor's range (the store is dropped), so the store always issues
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+      yp, 0, (int)min((long long)D * HW * (long long)sizeof(T), 0x7fffffffll), 0x00020000);
+  const unsigned qoff = b.own ? (unsigned)(((b.y0 + b.oy) * W + b.ox) * (int)sizeof(T)) : 0x80000000u;
+  const f2 zero2 = {0.f, 0.f};
+  f2 P[4];                      // (plane zi-1, plane zi) per voxel of the quad
+  f2 S01 = zero2, S23 = zero2;  // plane zi+1, voxels (0,1), (2,3)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) P[i] = zero2;
+  auto step = [&](auto I) {
+    constexpr int s = decltype(I)::value;
+    constexpr bool doP = s >= 1 && s <= TZC + 1;
+    constexpr bool doS = s <= TZC - 1;
+    constexpr bool fin = s >= 2 && s <= TZC + 1;
+    const int zi = b.z0 - 1 + s;
+    const LT* buf = ring + (s % GNB) * GPS;
+    // issue plane s + PD (its buffer was last read in step s - 1, behind that step's barrier),
+    // then wait for plane s
+    if constexpr (s + PD < TZC + 2) gissue(std::integral_constant<int, s + PD>{});
+    dw_wait_vm<gf_younger<TZC, NS, PD>(s)>();
+    __syncthreads();
+    if constexpr (doP || doS) {
+      f4 row[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) row[r] = ldv4(buf + (b.oy + r) * W + b.ox);
+      if constexpr (XF == 1) {
+        float zm = in_rng(zi) ? 1.f : 0.f;
+        pin(zm);
+        if constexpr (XR1) {   // the channel's value: the materialised product, bit for bit
+#pragma unroll
+          for (int r = 0; r < 3; ++r) row[r] = mul_rn(row[r], rks);
+        }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const float mr = zm * rv[r];
+          const f2 sc2 = {sc * mr, sc * mr}, sh2 = {sh * mr, sh * mr}, mu2 = {mu, mu};
+          f2 lo = f2{row[r][0], row[r][1]} - mu2, hi = f2{row[r][2], row[r][3]} - mu2;
+          lo = pfma(sc2, lo, sh2);
+          hi = pfma(sc2, hi, sh2);
+          const f2 ls = lo * f2{kSlope, kSlope}, hs = hi * f2{kSlope, kSlope};
+          row[r] = f4{fmaxf(lo.x, ls.x), fmaxf(lo.y, ls.y), fmaxf(hi.x, hs.x), fmaxf(hi.y, hs.y)};
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        f2 n2, p2;
+        f4 m;
+        q_nbr3(row[r], buf, b.oy + r, W, b.ox, b.el, b.er, n2, m, p2);
+        const f2 m01 = {m[0], m[1]}, m23 = {m[2], m[3]};
+        if constexpr (doP) {
+          const f2 t0 = wp[r * 3], t1 = wp[r * 3 + 1], t2 = wp[r * 3 + 2];
+          P[0] = pk_bc_s<kNH>(P[0], t0, n2); P[0] = pk_bc_s<0>(P[0], t1, m01); P[0] = pk_bc_s<1>(P[0], t2, m01);
+          P[1] = pk_bc_s<0>(P[1], t0, m01);  P[1] = pk_bc_s<1>(P[1], t1, m01); P[1] = pk_bc_s<0>(P[1], t2, m23);
+          P[2] = pk_bc_s<1>(P[2], t0, m01);  P[2] = pk_bc_s<0>(P[2], t1, m23); P[2] = pk_bc_s<1>(P[2], t2, m23);
+          P[3] = pk_bc_s<0>(P[3], t0, m23);  P[3] = pk_bc_s<1>(P[3], t1, m23); P[3] = pk_bc_s<0>(P[3], t2, p2);
+        }
+        if constexpr (doS) {
+          const float a0 = w0[r * 3], a1 = w0[r * 3 + 1], a2 = w0[r * 3 + 2];
+          S01.x = sfma_s(S01.x, a0, n2.y);
+          S01.y = sfma_s(S01.y, a0, m[0]);
+          S23.x = sfma_s(S23.x, a0, m[1]);
+          S23.y = sfma_s(S23.y, a0, m[2]);
+          S01 = pfma(f2{a1, a1}, m01, S01);
+          S23 = pfma(f2{a1, a1}, m23, S23);
+          S01.x = sfma_s(S01.x, a2, m[1]);
+          S01.y = sfma_s(S01.y, a2, m[2]);
+          S23.x = sfma_s(S23.x, a2, m[3]);
+          S23.y = sfma_s(S23.y, a2, p2.x);
+        }
+      }
+    }
+    if constexpr (fin) {
+      const f4 o = {P[0].x, P[1].x, P[2].x, P[3].x};
+      const int zf = zi - 1;
+      const unsigned off = zf < b.z1 ? qoff + (unsigned)((long long)zf * HW * (long long)sizeof(T)) : 0x80000000u;
+      if constexpr (BH) {
+        const b4_t ob = __builtin_convertvector(o, b4_t);
+        typedef unsigned u2v __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ob), yr, off, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f4, o), yr, off, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pin(P[i]);
+    pin(S01);
+    pin(S23);
+    P[0] = f2{P[0].y, S01.x};
+    P[1] = f2{P[1].y, S01.y};
+    P[2] = f2{P[2].y, S23.x};
+    P[3] = f2{P[3].y, S23.y};
+    S01 = S23 = zero2;
+  };
+  run_steps(step, std::make_integer_sequence<int, TZC + 2>{});
+}
+
+// ------------------------------------------------------------------------------------------------
 // Whole-volume variants for small planes/volumes (the 12^3 and 6^3 levels): one workgroup per
 // (n, c) holds the whole zero-padded volume [(D+2)(H+2)(W+2)] in LDS and each thread computes
 // voxels v = tid, tid + 256, ... with all 27 taps read straight from LDS.  One load phase and
@@ -1356,6 +1558,7 @@ int dw3_fwd_impl(const T* x, long long x_nstride, const float* w, const float* r
   const l3u_norm_src s = src ? *src : z;
   const int has = src ? 1 : 0;
   const bool xf = rec != nullptr || src != nullptr;
+  L3U_REQUIRE(x_nstride >= 0 || (!use_volume(D, H, W) && use_quads(H, W)));
   if (use_volume(D, H, W)) {
     size_t lds = (size_t)(D + 2) * (H + 2) * (W + 2) * sizeof(float);
     if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);
@@ -1365,6 +1568,28 @@ int dw3_fwd_impl(const T* x, long long x_nstride, const float* w, const float* r
   }
   if (use_quads(H, W) && x_nstride % 4 == 0 && y_nstride % 4 == 0) {
     const QGeom g = qgeom(N, C, D, H, W);
+    constexpr int E = (int)sizeof(T);
+    if (x_nstride < 0) {   // rank-1 input: the fp32 LDS-DMA form with a record only (l3u_dw3_bwd_rank1)
+      L3U_REQUIRE(E == 4 && xf && kDwfGl && dw_gl(g, W, E) && (g.RB + 2) * g.WQ > 64);
+      const size_t lds = (kDwfPd + 1) * (size_t)(g.RB + 2) * g.WQ * 16 + 8 * sizeof(float);
+      dim3 grid(N * C * g.nz * g.ny), block(64);
+#define DWGR(T_) hipLaunchKernelGGL((dw3g_fwd_kernel<T, 1, T_, true>), grid, block, lds, stream, x, \
+      x_nstride, w, rec, s, has, y, y_nstride, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
+      if constexpr (E == 4) { if (g.TZ == 16) DWGR(16); else if (g.TZ == 12) DWGR(12); else if (g.TZ == 8) DWGR(8); else if (g.TZ == 4) DWGR(4); else DWGR(2); }
+#undef DWGR
+      L3U_CHECK_LAUNCH();
+    }
+    if (kDwfGl && dw_gl(g, W, E) && (E == 2 || (g.RB + 2) * g.WQ > 64)) {
+      // LDS-DMA ring + packed FMAs (dw3g_fwd_kernel)
+      const size_t lds = (kDwfPd + 1) * (E == 2 ? (size_t)1024 : (size_t)(g.RB + 2) * g.WQ * 16) + 8 * sizeof(float);
+      dim3 grid(N * C * g.nz * g.ny), block(64);
+#define DWGF(M_, T_) hipLaunchKernelGGL((dw3g_fwd_kernel<T, M_, T_>), grid, block, lds, stream, x, \
+      x_nstride, w, rec, s, has, y, y_nstride, N, C, D, H, W, g.RB, g.RPW, g.ny, g.TZ, g.nz)
+      if (xf) { if (g.TZ == 16) DWGF(1, 16); else if (g.TZ == 12) DWGF(1, 12); else if (g.TZ == 8) DWGF(1, 8); else if (g.TZ == 4) DWGF(1, 4); else DWGF(1, 2); }
+      else { if (g.TZ == 16) DWGF(0, 16); else if (g.TZ == 12) DWGF(0, 12); else if (g.TZ == 8) DWGF(0, 8); else if (g.TZ == 4) DWGF(0, 4); else DWGF(0, 2); }
+#undef DWGF
+      L3U_CHECK_LAUNCH();
+    }
     size_t lds = (2 * (size_t)(g.RB + 2) * W + 8) * sizeof(float);
     if (lds < 16 * sizeof(double)) lds = 16 * sizeof(double);   // reduction scratch
     dim3 grid(N * C * g.nz * g.ny), block(g.threads);
@@ -1486,8 +1711,10 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
 // 1 when l3u_dw3_bwd takes a rank-1 input (x_nstride < 0) with rec at this shape (the fp32
 // LDS-DMA single pass, include/l3u.h "Rank-1 operands")
 extern "C" int l3u_dw3_bwd_rank1(int N, int C, int D, int H, int W) {
-  return N > 0 && C > 0 && !use_volume(D, H, W) && use_quads(H, W) &&
-         dw_gl(qgeom(N, C, D, H, W), W, 4);
+  if (!(N > 0 && C > 0 && !use_volume(D, H, W) && use_quads(H, W))) return 0;
+  const QGeom g = qgeom(N, C, D, H, W);
+  // the forward's rank-1 form (dw3g_fwd_kernel) needs two DMA slots per plane as well
+  return dw_gl(g, W, 4) && (!kDwfGl || (g.RB + 2) * g.WQ > 64);
 }
 
 extern "C" int l3u_dw3_nchunk(int N, int C, int D, int H, int W) {

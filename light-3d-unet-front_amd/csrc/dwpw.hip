@@ -108,7 +108,9 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
     const float* __restrict__ wsc, T* __restrict__ r, long long rns, float* __restrict__ rstat,
     T* __restrict__ z, long long zns, int D, int H, int W, int RB, int ny, int nz) {
   L3U_STAMP_SCOPE(501);
-  constexpr int K = 16 * CPW, NB = 2 + SC, NT = 4 * NC * (1 + SC);
+  // plane ring: the stencil reads step t's plane, the shortcut GEMM (one step late) step t-2's;
+  // step t+1 commits while a slower GEMM wave may still read t-2, so SC needs four slots
+  constexpr int K = 16 * CPW, NB = 2 + 2 * SC, NT = 4 * NC * (1 + SC);
   // register budget (1024 threads: <= 128 VGPRs): two channels per wave stage one plane ahead
   // and read their taps from LDS; one channel per wave stages two planes ahead, taps in SGPRs
   constexpr int PD = CPW == 1 ? 2 : 1;
@@ -365,7 +367,7 @@ DPGeom dp_geom(int K, int Nout, int D, int H, int W, int sc) {
   g.ny = (H + g.RB - 1) / g.RB;
   g.TZ = kDwpwTz;
   g.nz = (D + g.TZ - 1) / g.TZ;
-  const int NB = 2 + sc;
+  const int NB = 2 + 2 * sc;
   if (dp_lds(K, NB, g.RB, W) > 160 * 1024) return g;
   g.ok = true;
   return g;
@@ -387,7 +389,7 @@ int dwpw_fwd_impl(const T* x, long long x_nstride, const float* w_dw, const floa
   const l3u_norm_src zs{};
   const l3u_norm_src s = src ? *src : zs;
   const int xf = (rec != nullptr || src != nullptr) ? 1 : 0;
-  const int NB = 2 + sc;
+  const int NB = 2 + 2 * sc;
   const size_t lds = dp_lds(K, NB, g.RB, W);
   dim3 grid(N * g.nz * g.ny), block(1024);
 #define DPF0(XF_, CPW_, NC_, SC_, R_) hipLaunchKernelGGL((dwpw_fwd_kernel<T, XF_, CPW_, NC_, SC_, kDwpwTz, R_>), grid, \

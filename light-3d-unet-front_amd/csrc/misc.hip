@@ -432,6 +432,10 @@ __global__ void counter_add_kernel(int* c, int v) { c[0] += v; }
 
 // ---------------------------------------------------------------- segmented partial reduction
 constexpr int kSegBatch = 8;   // measured: 8 < 16 < 32 us/step
+#ifndef L3U_SEG_VEC
+#define L3U_SEG_VEC 1
+#endif
+constexpr bool kSegVec = L3U_SEG_VEC != 0;   // float4 rows where the item allows (segment_sum)
 // item (8 x int64): src_off, count, istride, tstride, len, dst_off, accumulate, unused
 // dst[dst_off + t] (+)= sum_{i<count} src[src_off + i*istride + t*tstride], t < len (<= 256)
 // Returns, for thread t < len, the segment's sum for output t (red: 256 doubles of LDS).
@@ -439,6 +443,43 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
                                               const long long* __restrict__ it, double* red) {
   const int t = threadIdx.x;
   const int len = (int)it[4];
+  // fp32 partial rows with 16-byte aligned, contiguous outputs (the pointwise / ConvTranspose3d
+  // weight-gradient partials): a thread sums 4 adjacent outputs from float4 loads, so the 864- /
+  // 432-long partial lists of the 48^3 / 24^3 layers take a quarter of the dependent load rounds
+  // of the scalar form below (same fixed order per output: i = k, k + TP, ...; deterministic)
+  if (kSegVec && !it[7] && it[3] == 1 && (len & 3) == 0 && (it[2] & 3) == 0 && (it[0] & 3) == 0) {
+    const int L4 = len >> 2, TP = 256 / L4;
+    const int o4 = t % L4, k = t / L4;
+    const long long cnt = it[1], is4 = it[2] >> 2;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    if (k < TP) {
+      const f4* sf = reinterpret_cast<const f4*>(src + it[0]) + o4;
+      const long long stp = is4 * TP;
+      long long i = k;
+      constexpr int B = kSegBatch;
+      for (; i + (B - 1) * TP < cnt; i += B * TP) {
+        f4 v[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) v[u] = sf[i * is4 + u * stp];
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) s[q] += v[u][q];
+      }
+      for (; i < cnt; i += TP) {
+        const f4 v = sf[i * is4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[q] += v[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[t * 4 + q] = s[q];
+    __syncthreads();
+    double r = 0.0;
+    if (t < len)
+      for (int kk = 0; kk < TP; ++kk) r += red[(kk * L4 + (t >> 2)) * 4 + (t & 3)];
+    return r;
+  }
   // TP threads per output: thread (k, o) sums terms i = k, k+TP, k+2TP, ... of output o
   // (consecutive threads on consecutive outputs: coalesced), then the TP partial sums are added
   // in k order.  TP depends only on len, so the summation order is fixed: deterministic.
@@ -485,7 +526,7 @@ __global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __res
                                                               const long long* __restrict__ items,
                                                               float* __restrict__ dst) {
   L3U_STAMP_SCOPE(410);
-  __shared__ double red[256];
+  __shared__ double red[1024];   // segment_sum: 4 per thread in the float4 form
   const long long* it = items + (long long)blockIdx.x * 8;
   const double r = segment_sum(src, it, red);
   const int t = threadIdx.x;
@@ -505,7 +546,7 @@ __global__ __launch_bounds__(256) void reduce_segments_adamw_kernel(
     const float* __restrict__ lr, float beta1, float beta2, float eps, float wd, int* step,
     float gscale, int* ticket, int* counter2) {
   L3U_STAMP_SCOPE(416);
-  __shared__ double red[256];
+  __shared__ double red[1024];   // segment_sum: 4 per thread in the float4 form
   const long long* it = items + (long long)blockIdx.x * 8;
   const int tc = step[0] + 1;
   const float lrv = lr[0];

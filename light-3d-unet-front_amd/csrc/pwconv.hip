@@ -579,6 +579,16 @@ __global__ __launch_bounds__(256) void pw_bwd_weight_kernel(
 // the second problem of a paired block-tail launch (l3u_pw_bwd_tail_pair, PRO 2): the same
 // block tail (dout, out, tail partials) for the other pointwise backward of the block
 // (conv2.pointwise, sel 1, or the shortcut, sel 2); blockIdx.z == 1
+#ifndef L3U_DYT_SWZ
+#define L3U_DYT_SWZ 1
+#endif
+constexpr bool kDyTileSwz = L3U_DYT_SWZ != 0;
+constexpr int kDyTileDS = kDyTileSwz ? 64 : 68;   // dY tile row stride (floats)
+// float offset of quad q (4 voxels) of row r in a wave's dY tile
+L3U_DEV int dyt_at(int r, int q) {
+  return r * kDyTileDS + 4 * (kDyTileSwz ? (q ^ (r & 15)) : q);
+}
+
 template <typename T>
 struct TailSecond {
   const T* yr; long long yrns; const float* rec; const T* x; long long xns; const float* w;
@@ -603,7 +613,13 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   }
   if ((int)blockIdx.y * TK >= K) return;   // the narrower problem's unused column blocks
   constexpr int WS = TK + ((16 - TK) % 64 + 64) % 64;   // >= TK, = 16 mod 64
-  constexpr int DS = 68;                                // dY tile row stride (floats)
+  // dY tile: row stride DS floats; with kDyTileSwz the 16 quads of a row are XOR-swizzled by the
+  // row (quad q of row r at q ^ (r & 15)): the b128 writes (8 lanes of one row) and the
+  // transposed b128 reads (lane (lr, lk) reads quad 4 gg + lk of row lr; gfx950 serves a
+  // ds_read_b128 in 4 lane groups of 16) are both bank-conflict-free.  The unswizzled stride-68
+  // image had a 2-way conflict in every read group (round-4 SQ pass: 404k conflict cycles per
+  // 553k LDS instructions in the 48^3 tail pair)
+  constexpr int DS = kDyTileDS;
   constexpr int PS = 8;                                 // lanes per channel for the IN sums
   static_assert(NJ == 2 || NK * 256 <= 16 * DS, "weight-gradient reduction must fit in the dY tiles");
   __shared__ __attribute__((aligned(16))) float w_l[TJ * WS];
@@ -742,7 +758,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
   float* tile = dyt_lds + (size_t)wave * TR * DS;
 #pragma unroll
   for (int jr = 0; jr < TR / 4; ++jr)
-    *reinterpret_cast<f4*>(tile + (4 * jr + lk) * DS + 4 * lr) = g[jr];
+    *reinterpret_cast<f4*>(tile + dyt_at(4 * jr + lk, lr)) = g[jr];
 
   if constexpr (!XL) load_xv();
 
@@ -784,7 +800,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     constexpr int ar = TR == TJ ? a : 0;
 #pragma unroll
     for (int gg = 0; gg < 4; ++gg) {
-      const f4 av = *reinterpret_cast<const f4*>(tile + (16 * ar + lr) * DS + 16 * gg + 4 * lk);
+      const f4 av = *reinterpret_cast<const f4*>(tile + dyt_at(16 * ar + lr, 4 * gg + lk));
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -797,7 +813,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       f4 av[NJ];
 #pragma unroll
       for (int a = 0; a < NJ; ++a)
-        av[a] = *reinterpret_cast<const f4*>(tile + (16 * a + lr) * DS + 16 * gg + 4 * lk);
+        av[a] = *reinterpret_cast<const f4*>(tile + dyt_at(16 * a + lr, 4 * gg + lk));
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -813,7 +829,7 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr)
-      *reinterpret_cast<f4*>(tile + (4 * jr + lk) * DS + 4 * lr) = g[4 + jr];
+      *reinterpret_cast<f4*>(tile + dyt_at(4 * jr + lk, lr)) = g[4 + jr];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1649,7 +1665,7 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
-  const size_t dlds = (size_t)max(nwv, 4) * 16 * 68 * sizeof(float);   // 16-row dY tiles (DS = 68)
+  const size_t dlds = (size_t)max(nwv, 4) * 16 * kDyTileDS * sizeof(float);   // 16-row dY tiles
 #define PWBT0(A_, B_, R_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2, R_>), grid, block, dlds, stream, \
       dout, dout_nstride, yr, yr_nstride, rec, tail_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel, dscale, dpool, dpns, pidx, Hf, Wf)
@@ -1695,7 +1711,7 @@ int pw_bwd_tail_pair_impl(const float* dout, long long dout_nstride, const float
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK), 2), block(64 * nwv);
-  const size_t dlds = (size_t)max(nwv, 4) * 16 * 68 * sizeof(float);   // 16-row dY tiles (DS = 68)
+  const size_t dlds = (size_t)max(nwv, 4) * 16 * kDyTileDS * sizeof(float);   // 16-row dY tiles
 #define PWTP0(A_, B_, R_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2, false, R_>), grid, block, dlds, stream, \
       dout, dout_nstride, a.yr, a.yrns, a.rec, tail_part, npart, a.x, a.xns, a.w, a.dx, a.dxns, \
       a.accumulate, a.part, N, J, a.K, S, SCH, nsc, out, out_nstride, a.sel, dscale, dpool, dpns, pidx, \
@@ -1749,7 +1765,7 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
   const int nwv = SCH / 64;
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);   // one sweep of the chunk per workgroup
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
-  const size_t dlds = (size_t)max(nwv, 4) * 16 * 68 * sizeof(float);   // 16-row dY tiles (DS = 68)
+  const size_t dlds = (size_t)max(nwv, 4) * 16 * kDyTileDS * sizeof(float);   // 16-row dY tiles
   // one input channel with the IN prologue (the first block's conv1.pointwise, y materialised or
   // rank-1): the VALU kernel, same chunks and partial layout
   if (K == 1 && y != nullptr && SCH <= 512 && J <= 32) {

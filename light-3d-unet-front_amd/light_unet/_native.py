@@ -5,6 +5,7 @@ library is missing or the tensors are not on a ROCm device, calls raise immediat
 """
 import ctypes
 import os
+import warnings
 
 import torch  # noqa: F401  (loads the HIP runtime the library binds to: one runtime per process)
 
@@ -159,18 +160,24 @@ def load():
             f"HIP library not found at {LIB_PATH}; build it with `make -C light-3d-unet-front_amd` "
             "(or __graft_entry__.build()).  The Light-3D-U-Net MI355X path has no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH)
+    # L3U_SKIP_ABI_CHECK=1: an older variant build on purpose (A/B of an earlier commit's csrc/);
+    # its missing entry points stay unbound (calling one raises) and a version mismatch only warns
+    skip = os.environ.get("L3U_SKIP_ABI_CHECK") == "1"
     for name, args in _SIGS.items():
         fn = getattr(lib, name, None)
-        if fn is None and os.environ.get("L3U_LIB"):
-            continue   # an older variant build (A/B tools): calls of newer entry points raise
+        if fn is None and skip:
+            continue
         if fn is None:
             raise NativeError(f"{LIB_PATH} does not export {name}: rebuild the library")
         fn.argtypes = args
         fn.restype = I
     ver = lib.l3u_abi_version()
-    if ver != ABI_VERSION and not os.environ.get("L3U_LIB"):
-        raise NativeError(f"{LIB_PATH} reports ABI version {ver}, this binding expects "
-                          f"{ABI_VERSION}: rebuild the library")
+    if ver != ABI_VERSION:
+        msg = (f"{LIB_PATH} reports ABI version {ver}, this binding expects {ABI_VERSION}: "
+               "rebuild the library")
+        if not skip:
+            raise NativeError(msg)
+        warnings.warn(msg + " (L3U_SKIP_ABI_CHECK=1: loading it anyway)")
     _lib = lib
     return lib
 

@@ -546,7 +546,7 @@ class UNetEngine:
         y2 = e(N, cout, S)
         # y1 as conv2 reads it: a tensor, or rank-1 (z1 with a negative batch stride)
         y1v = V(z1, 0, S, cout, scale=True) if y1 is None else V(y1, 0, cout * S, cout)
-        if _DWPW and S >= _DWPW_MIN_S and nat.query("l3u_dwpw_supported", cout, cout, d, h, w, 0):
+        if self._use_dwpw(cout, dims):
             # conv2 = depthwise (IN1 + LeakyReLU + Dropout3d on load) + pointwise in one launch
             nsb2 = nat.query("l3u_dwpw_stat_nsb", cout, cout, d, h, w)
             s2 = self.fwd_arena.alloc(N * cout * nsb2 * 3)
@@ -556,8 +556,9 @@ class UNetEngine:
                        self.fwd_arena.ptr(s2), None, None, 0, None, z2.data_ptr(), cout * S, N, cout,
                        cout, d, h, w, st)
         else:
-            assert y1 is not None, "rank-1 y1 needs the fused conv2 (l3u_dwpw_fwd)"
-            self._call("l3u_dw3_fwd", y1.data_ptr(), cout * S,
+            # (a rank-1 y1 goes in with its negative batch stride: l3u_dw3_fwd forms w1[c] * z1
+            # on load, l3u_dw3_bwd_rank1 shapes)
+            self._call("l3u_dw3_fwd", y1v.p, y1v.sns,
                        self._w(flat, pre + "conv2.depthwise.weight"), None, nat.norm_src_ptr(src1),
                        z2.data_ptr(), cout * S, N, cout, d, h, w, st)
             s2 = self.fwd_arena.alloc(N * cout * nsb2 * 3)
@@ -578,14 +579,22 @@ class UNetEngine:
         sv.update(z1=z1, y1=y1, y1v=y1v, z2=z2, y2=y2, dims=dims, shortcut=shortcut)
         return sv
 
+    @staticmethod
+    def _use_dwpw(cout, dims):
+        """conv2 as the one-launch l3u_dwpw_fwd (else l3u_dw3_fwd then l3u_pw_fwd)."""
+        d, h, w = dims
+        return (_DWPW and d * h * w >= _DWPW_MIN_S
+                and nat.query("l3u_dwpw_supported", cout, cout, d, h, w, 0) == 1)
+
     def _front_rank1(self, x, N, cout, dims):
         """The first block's y1 / r stay rank-1 (never materialised) when every consumer takes a
         rank-1 operand at this shape: the fused conv2 (l3u_dwpw_fwd), the LDS-DMA IN-fused
         depthwise backward, the fused pointwise backwards and the fused block tail (fp32)."""
         d, h, w = dims
         S = d * h * w
-        return (_FRONT_R1 and not self.bf16 and self._front_ok(x, dims) and _DWPW and S >= _DWPW_MIN_S
-                and nat.query("l3u_dwpw_supported", cout, cout, d, h, w, 0)
+        return (_FRONT_R1 and not self.bf16 and self._front_ok(x, dims)
+                # conv2's forward takes the rank-1 y1 (the fused l3u_dwpw_fwd, or l3u_dw3_fwd) at
+                # the l3u_dw3_bwd_rank1 shapes, as the IN-fused depthwise backward does
                 and nat.query("l3u_dw3_bwd_rank1", N, cout, d, h, w)
                 and nat.query("l3u_pw_bwd_supported", cout, 1, S)
                 # the rank-1 pointwise backward variants take one 16-column block (J = cout <= 16)

@@ -39,10 +39,12 @@ class TrainStep:
         separate update launch) even in a one-rank process group -- the RCCL path on one GPU.
         capture_collectives: capture() records the collectives into the step's one hipGraph
         instead of enqueuing them eagerly between three graph segments.  None (default): capture
-        them when the group's backend is RCCL ("nccl"; measured on one MI355X: +6.1 us per step
-        over the no-exchange graph, against +33.6 us for the eager segments,
-        profiles/r4a_rccl_probe.json), unless L3U_EAGER_COLLECTIVES=1; gloo collectives run on
-        the host and always stay eager."""
+        them for the forced one-rank RCCL probe (the only captured-collective form measured on
+        hardware: world-1 RCCL, BENCH_r04 `exchange_us`: +12.5 us per step captured, +28.6 us
+        segmented), and at world > 1 only with L3U_CAPTURE_COLLECTIVES=1 (no multi-rank
+        captured replay has been recorded yet, so the eager segments stay the default there);
+        L3U_EAGER_COLLECTIVES=1 forces the segments everywhere.  gloo collectives run on the
+        host and always stay eager."""
         loss_cfg = loss_cfg or {}
         self.alpha = float(loss_cfg.get("alpha", 0.7))
         self.beta = float(loss_cfg.get("beta", 0.3))
@@ -67,7 +69,8 @@ class TrainStep:
         self.exchange = self.world > 1 or self.force
         if capture_collectives is None:
             capture_collectives = self.exchange and _rccl(group) and \
-                os.environ.get("L3U_EAGER_COLLECTIVES", "0") != "1"
+                os.environ.get("L3U_EAGER_COLLECTIVES", "0") != "1" and \
+                (self.world == 1 or os.environ.get("L3U_CAPTURE_COLLECTIVES", "0") == "1")
         self.capture_collectives = bool(capture_collectives)
         self.ftl_mode = ftl_mode
         dev = self.flat.device

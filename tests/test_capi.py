@@ -98,6 +98,12 @@ def test_host_queries_without_gpu():
     assert _native.query("l3u_convt_bwd_fused_nparts", 4, 128, 64, 6, 6, 6) == 0
     assert _native.query("l3u_convt_bwd_fused_nparts", 4, 128, 64, 16, 16, 16) == 4 * 8
     assert _native.query("l3u_convt_bwd_fused_nparts", 4, 256, 128, 6, 6, 6) == 0
+    # the tile kernel reads dY through a buffer descriptor over one sample: Co * 8 * S floats
+    # must stay below 2^31 bytes (Co = 32: S < 2^21), larger volumes take the three-launch path
+    assert _native.query("l3u_convt_bwd_fused_nparts", 1, 64, 32, 127, 128, 128) > 0
+    assert _native.query("l3u_convt_bwd_fused_nparts", 1, 64, 32, 128, 128, 128) == 0
+    assert _native.query("l3u_convt_bwd_fused_nparts", 1, 128, 64, 64, 128, 128) == 0
+    assert _native.query("l3u_convt_bwd_fused_nparts", 1, 128, 64, 62, 128, 128) > 0
     assert _native.query("l3u_dw3_nchunk", 4, 32, 24, 24, 24) == 18   # 6 z-slabs x 3 y-strips
     assert _native.query("l3u_dw3_nchunk", 4, 128, 6, 6, 6) == 1
     assert _native.query("l3u_pw_stat_nsb", 16, 16, 48 ** 3) == 432   # 256-voxel tiles

@@ -12,7 +12,8 @@ pytestmark = pytest.mark.gpu
 
 # (N, K, Nout, D, H, W, shortcut, xf): the model's 48^3 conv2 (16 -> 16, IN on load), the 24^3
 # down1.conv1 (16 -> 32 with the shortcut), a ragged volume (short last strip and slab)
-SHAPES = [(4, 16, 16, 48, 48, 48, 0, 1), (2, 16, 32, 24, 24, 24, 1, 0),
+# (the 48^3 shortcut form exercises the four-slot plane ring of the one-step-late shortcut GEMM)
+SHAPES = [(4, 16, 16, 48, 48, 48, 0, 1), (2, 16, 32, 24, 24, 24, 1, 0), (4, 16, 16, 48, 48, 48, 1, 0),
           (1, 16, 16, 20, 28, 36, 0, 1), (2, 16, 32, 13, 10, 12, 0, 1), (1, 16, 32, 9, 7, 16, 0, 0)]
 
 

@@ -326,13 +326,14 @@ def test_trainstep_data_parallel_two_ranks(cuda, tmp_path):
 
 
 
-@pytest.mark.parametrize("switch,fixture", [("_RANK1", "model_b2_32.npz"),
-                                            ("_POOLFOLD", "model_b2_32.npz"),
-                                            ("_POOLFOLD", "model_b1_48.npz"),
-                                            ("_FRONT_R1", "model_b1_48.npz"),
-                                            ("_PAIR_BWD", "model_b1_48.npz"),
-                                            ("_PAIR_BWD", "model_b2_32.npz")])
-def test_formed_on_load_gradients_bitwise(cuda, golden, switch, fixture):
+@pytest.mark.parametrize("switch,fixture,extra", [("_RANK1", "model_b2_32.npz", {}),
+                                                  ("_POOLFOLD", "model_b2_32.npz", {}),
+                                                  ("_POOLFOLD", "model_b1_48.npz", {}),
+                                                  ("_FRONT_R1", "model_b1_48.npz", {}),
+                                                  ("_FRONT_R1", "model_b1_48.npz", {"_DWPW": False}),
+                                                  ("_PAIR_BWD", "model_b1_48.npz", {}),
+                                                  ("_PAIR_BWD", "model_b2_32.npz", {})])
+def test_formed_on_load_gradients_bitwise(cuda, golden, switch, fixture, extra):
     """Output gradients formed on load give bitwise the gradients of the materialised tensors,
     for the FocalTversky and the given-dL/dp forms of the backward:
     _RANK1: out_conv is rank-1 (unet3d.py:201), the last block gets d(pre-sigmoid) and the
@@ -345,15 +346,30 @@ def test_formed_on_load_gradients_bitwise(cuda, golden, switch, fixture):
     shapes where all of them take the rank-1 form);
     _PAIR_BWD: a block's conv2.pointwise and shortcut backwards in one launch at the 12^3 / 6^3
     levels (l3u_pw_bwd2), the shortcut writing d(input) before the depthwise backward adds to it.
+    extra: engine switches held for both runs (_DWPW False: conv2 as l3u_dw3_fwd + l3u_pw_fwd, the
+    rank-1 y1 formed on load by the depthwise forward).
     The output is compared too."""
     import light_unet.engine as E
-    from light_unet.models.unet3d import Lightweight3DUNet
-    from light_unet.train_step import TrainStep
+    saved = {k: getattr(E, k) for k in extra}
+    for k, v in extra.items():
+        setattr(E, k, v)
     z = golden(fixture)
     sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w/")}
     x = torch.from_numpy(z["x"]).to(cuda)
     t = torch.from_numpy(z["target"]).to(cuda)
     res = []
+    try:
+        _formed_on_load_runs(E, switch, sd, x, t, cuda, res)
+    finally:
+        for k, v in saved.items():
+            setattr(E, k, v)
+    for name, a, b in zip(("ftl grad", "dp grad", "loss", "output"), *res):
+        assert torch.equal(a, b), (name, (a - b).abs().max().item())
+
+
+def _formed_on_load_runs(E, switch, sd, x, t, cuda, res):
+    from light_unet.models.unet3d import Lightweight3DUNet
+    from light_unet.train_step import TrainStep
     for on in (True, False):
         setattr(E, switch, on)
         try:
@@ -373,5 +389,3 @@ def test_formed_on_load_gradients_bitwise(cuda, golden, switch, fixture):
                 assert (sv["blk"]["init_conv."]["y1"] is None) == on
         finally:
             setattr(E, switch, True)
-    for name, a, b in zip(("ftl grad", "dp grad", "loss", "output"), *res):
-        assert torch.equal(a, b), (name, (a - b).abs().max().item())

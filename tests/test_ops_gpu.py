@@ -122,6 +122,55 @@ def test_dw3_fwd_inkernel_finalize(cuda, shape):
     assert torch.equal(ya, yb)
 
 
+@pytest.mark.parametrize("shape", [(4, 16, 48, 48, 48), (2, 16, 24, 24, 24), (1, 4, 9, 20, 24)])
+@pytest.mark.parametrize("finalize", [False, True])
+def test_dw3_fwd_rank1_input(cuda, shape, finalize):
+    """A rank-1 IN-fused input (negative batch stride: one stored channel z, channel c =
+    rec[c][7] * z, include/l3u.h "Rank-1 operands"; the first block's y1 = w1[c] * z1) gives the
+    bits of the materialised tensor's forward, with the record given or finalized in-kernel."""
+    N, C, D, H, W = shape
+    if not nat().query("l3u_dw3_bwd_rank1", N, C, D, H, W):
+        pytest.skip("no rank-1 form at this shape")
+    S = D * H * W
+    gen = torch.Generator().manual_seed(14)
+    z = torch.randn(N, 1, S, generator=gen).to(cuda)
+    rk = (1 + 0.3 * torch.randn(C, generator=gen)).to(cuda)
+    ymat = rk[None, :, None] * z                 # the materialised y1 (same float products)
+    w = torch.randn(C, 27, generator=gen).to(cuda)
+    rec = make_rec(N, C, gen, drop=True).float()
+    rec[..., 7] = rk.cpu()[None, :]
+    rec = rec.to(cuda).contiguous()
+    ya, yb = torch.empty(N, C, S, device=cuda), torch.empty(N, C, S, device=cuda)
+    keep = []
+    if finalize:
+        # the record from (count, mean, M2) partials of the materialised tensor, rank1 = rk
+        nsb = 3
+        ch = torch.tensor_split(ymat.double().cpu(), nsb, dim=2)
+        part = torch.stack([torch.stack([torch.full((N, C), float(c.shape[2]), dtype=torch.float64),
+                                         c.mean(2), ((c - c.mean(2, keepdim=True)) ** 2).sum(2)], -1)
+                            for c in ch], 2).float().contiguous().to(cuda)
+        g = (1 + 0.1 * torch.randn(C, generator=gen)).to(cuda)
+        b = (0.1 * torch.randn(C, generator=gen)).to(cuda)
+        step = torch.tensor([2], dtype=torch.int32, device=cuda)
+        ra, rb = torch.empty(N * C * 8, device=cuda), torch.empty(N * C * 8, device=cuda)
+        sa = nat().NormSrc(part.data_ptr(), nsb, 3, g.data_ptr(), b.data_ptr(), 0.2, 5,
+                           step.data_ptr(), ra.data_ptr(), None)
+        sb = nat().NormSrc(part.data_ptr(), nsb, 3, g.data_ptr(), b.data_ptr(), 0.2, 5,
+                           step.data_ptr(), rb.data_ptr(), rk.data_ptr())
+        keep += [sa, sb]
+        nat().call("l3u_dw3_fwd", ymat.data_ptr(), C * S, w.data_ptr(), None, nat().norm_src_ptr(sa),
+                   ya.data_ptr(), C * S, N, C, D, H, W, st())
+        nat().call("l3u_dw3_fwd", z.data_ptr(), -S, w.data_ptr(), None, nat().norm_src_ptr(sb),
+                   yb.data_ptr(), C * S, N, C, D, H, W, st())
+    else:
+        nat().call("l3u_dw3_fwd", ymat.data_ptr(), C * S, w.data_ptr(), rec.data_ptr(), None,
+                   ya.data_ptr(), C * S, N, C, D, H, W, st())
+        nat().call("l3u_dw3_fwd", z.data_ptr(), -S, w.data_ptr(), rec.data_ptr(), None,
+                   yb.data_ptr(), C * S, N, C, D, H, W, st())
+    torch.cuda.synchronize()
+    assert torch.equal(ya, yb), (ya - yb).abs().max().item()
+
+
 @pytest.mark.parametrize("shape", DW_SHAPES)
 @pytest.mark.parametrize("mode", [0, 1])
 def test_dw3_bwd(cuda, shape, mode):

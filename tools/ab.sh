@@ -1,7 +1,7 @@
 # GPU A/B of two library builds on one box: the model / op GPU tests on the in-tree library, then
 # REPS interleaved headline-step timings of lib/var_<A>.so and lib/var_<B>.so.
 #   bash tools/ab.sh A B [REPS] [TAG]      (builds: tools/mkvar.sh; A_ENV / B_ENV: extra
-#   environment of each side, e.g. A_ENV="L3U_X=0" for a build without a newer entry point;
+#   environment of each side, e.g. A_ENV="L3U_SKIP_ABI_CHECK=1" for a build of an older commit;
 #   AB_ARGS: extra bench arguments, e.g. "--enc 32,64,128,256 --size 64 --steps 20" for config 5;
 #   AB_TESTS=0 skips the tests)
 cd ${GRAFT_REPO_ROOT:-.}

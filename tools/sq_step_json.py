@@ -1,8 +1,13 @@
 """Per-launch SQ counters of one eager training step from tools/pmc_sq_step.sh's passes (the last
 complete step: steps end at each AdamW launch), with the derived figures used in DESIGN §8:
 
-  waves_per_simd  SQ_WAVE_CYCLES / SQ_BUSY_CYCLES / 1024 SIMDs (mean resident waves; the SQ
-                  cycle counters count quad-cycles, the ratio cancels the unit)
+  waves_per_simd  mean resident waves per SIMD over the launch: SQ_WAVE_CYCLES counts quad-cycles
+                  summed over every wave, SQ_BUSY_CYCLES counts cycles summed over the 32 shader
+                  engines (busy / 32 = the launch's duration in cycles: 28-33 x the rocprof
+                  duration in us at the ~2.1-2.4 GHz clock, r4g records), so
+                  waves/SIMD = 4 * WAVE_CYCLES / (BUSY_CYCLES / 32) / 1024 SIMDs
+                  = WAVE_CYCLES / BUSY_CYCLES / 8  (round 4's field omitted the 4 * 32 and read
+                  ~128x low)
   valu_busy       SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (per wave: the share of its life issuing VALU)
   wait_frac       SQ_WAIT_ANY / SQ_WAVE_CYCLES (parked on s_waitcnt / barrier)
   salu_per_valu   SQ_INSTS_SALU / SQ_INSTS_VALU
@@ -58,7 +63,7 @@ def main():
         it = {"kernel": name, "grid": passes[0][i][1],
               "pmc_dur_us": round(sum(q[i][2] for q in passes) / len(passes), 2), "counters": c}
         if wc > 0 and c.get("SQ_BUSY_CYCLES", 0) > 0:
-            it["waves_per_simd"] = round(wc / c["SQ_BUSY_CYCLES"] / 1024, 2)
+            it["waves_per_simd"] = round(4.0 * wc / (c["SQ_BUSY_CYCLES"] / 32.0) / 1024, 2)
             it["valu_busy"] = round(c.get("SQ_ACTIVE_INST_VALU", 0) / wc, 3)
             it["wait_frac"] = round(c.get("SQ_WAIT_ANY", 0) / wc, 3)
         if c.get("SQ_INSTS_VALU", 0) > 0:
