@@ -180,17 +180,6 @@ L3U_DEV void seq_sum(const double* __restrict__ p, int n, double t[NV]) {
   }
 }
 
-// Chan et al. parallel merge of (count, mean, M2) — deterministic when merged in fixed order.
-L3U_DEV void chan_merge(float& n_a, float& mean_a, float& m2_a, float n_b, float mean_b, float m2_b) {
-  const float n = n_a + n_b;
-  if (n <= 0.f) return;
-  const float d = mean_b - mean_a;
-  const float fb = n_b / n;
-  mean_a = mean_a + d * fb;
-  m2_a = m2_a + m2_b + d * d * n_a * fb;
-  n_a = n;
-}
-
 L3U_DEV unsigned long long splitmix64(unsigned long long z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -212,41 +201,55 @@ L3U_DEV RecIn record_inputs(const l3u_norm_src& s, int c) {
 L3U_DEV void record_from(const l3u_norm_src& s, const RecIn& q, int n, int c, int C, float cn,
                          float mu, float m2, float r[kRec]);
 
-// Merge the (count, mean, M2) partials of one (n, c) with the 64 lanes of the calling wave
-// (lane-strided Chan merges, then a fixed xor tree) and build the 8-float record.  Every caller
-// for the same (n, c) gets bit-identical values.  Must be called by a full wave; returns the
-// record in `r` on every lane.
+// Merge the (count, mean, M2) partials of one (n, c) with the 64 lanes of the calling wave and
+// build the 8-float record.  Two passes of plain wave sums (DPP, no LDS): the total count and
+// sum of count * mean give the mean; then every partial's M2 plus count * (mean_i - mean)^2 --
+// all non-negative terms -- sum to the M2 of the whole (n, c).  The lane-strided loads of 8
+// partials per lane are issued together (one memory latency for up to 512 partials; longer lists
+// re-read them in the second pass).  Fixed order: every caller for the same (n, c) gets
+// bit-identical values.  (Round 4 merged pairs with Chan's formula along a 6-round shuffle tree:
+// ~3.5 us on the critical path of every IN-consuming small-level launch, wave stamps r5d.)
+// Must be called by a full wave; returns the record in `r` on every lane.
 L3U_DEV void finalize_record(const l3u_norm_src& s, int n, int c, int C, float r[kRec]) {
   const int l = threadIdx.x & 63;
   const RecIn q = record_inputs(s, c);
   const float* p = s.stat_part + ((long long)n * C + c) * s.nsb * 3;
-  float cn = 0.f, mu = 0.f, m2 = 0.f;
-  // lane-strided sequential merges; the loads of 8 steps are issued together (one memory
-  // latency per 8 partials instead of one per partial), the merge order is unchanged
-  for (int i0 = l; i0 < s.nsb; i0 += 64 * 8) {
-    float v[8][3];
+  float v[8][3];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u][0] = v[u][1] = v[u][2] = 0.f;
+  auto fetch = [&](int i0) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int i = i0 + 64 * u;
       v[u][0] = v[u][1] = v[u][2] = 0.f;
       if (i < s.nsb) { v[u][0] = p[i * 3]; v[u][1] = p[i * 3 + 1]; v[u][2] = p[i * 3 + 2]; }
     }
+  };
+  float cs = 0.f, ms = 0.f;
+  for (int i0 = l; i0 < s.nsb; i0 += 512) {
+    fetch(i0);
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (i0 + 64 * u < s.nsb) chan_merge(cn, mu, m2, v[u][0], v[u][1], v[u][2]);
+    for (int u = 0; u < 8; ++u) { cs += v[u][0]; ms = fmaf(v[u][0], v[u][1], ms); }
   }
+  const float cn = wave_sum(cs);
+  const float mu = cn > 0.f ? wave_sum(ms) / cn : 0.f;
+  float m2 = 0.f;
+  auto add_m2 = [&] {
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float cb = __shfl_xor(cn, o, 64), mb = __shfl_xor(mu, o, 64), vb = __shfl_xor(m2, o, 64);
-    if (l & o) {   // merge in lane order so both partners compute the same value
-      float c2 = cb, mu2 = mb, v2 = vb;
-      chan_merge(c2, mu2, v2, cn, mu, m2);
-      cn = c2; mu = mu2; m2 = v2;
-    } else {
-      chan_merge(cn, mu, m2, cb, mb, vb);
+    for (int u = 0; u < 8; ++u) {
+      const float d = v[u][1] - mu;
+      m2 += fmaf(v[u][0] * d, d, v[u][2]);
+    }
+  };
+  if (s.nsb <= 512) {
+    add_m2();   // the lane's partials are still in registers (zeros where it holds none)
+  } else {
+    for (int i0 = l; i0 < s.nsb; i0 += 512) {
+      fetch(i0);
+      add_m2();
     }
   }
-  record_from(s, q, n, c, C, cn, mu, m2, r);
+  record_from(s, q, n, c, C, cn, mu, wave_sum(m2), r);
 }
 
 // The record of (n, c) from its merged (count, mean, M2): rstd, the affine parameters and the

@@ -1142,7 +1142,7 @@ __global__ __launch_bounds__(64) void dw3g_fwd_kernel(
     const T* __restrict__ x, long long xns, const float* __restrict__ w,
     const float* __restrict__ rec, l3u_norm_src src, int has_src, T* __restrict__ y,
     long long yns, int N, int C, int D, int H, int W, int RB, int RPW, int ny, int TZ, int nz) {
-  L3U_STAMP_SCOPE(206);
+  L3U_STAMP_SCOPE(209);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr bool BH = sizeof(T) == 2;
   constexpr int NS = BH ? 1 : 2;          // DMA slots per plane

@@ -457,19 +457,15 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
       const long long stp = is4 * TP;
       long long i = k;
       constexpr int B = kSegBatch;
-      for (; i + (B - 1) * TP < cnt; i += B * TP) {
+      for (; i < cnt; i += B * TP) {   // every batch's loads in flight at once (no serial tail)
         f4 v[B];
 #pragma unroll
-        for (int u = 0; u < B; ++u) v[u] = sf[i * is4 + u * stp];
+        for (int u = 0; u < B; ++u)
+          v[u] = i + u * TP < cnt ? sf[i * is4 + u * stp] : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < B; ++u)
 #pragma unroll
           for (int q = 0; q < 4; ++q) s[q] += v[u][q];
-      }
-      for (; i < cnt; i += TP) {
-        const f4 v = sf[i * is4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s[q] += v[q];
       }
     }
 #pragma unroll
@@ -494,24 +490,22 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
     constexpr int B = kSegBatch;   // loads in flight per thread
     if (it[7]) {
       const double* sd = reinterpret_cast<const double*>(src) + base;
-      for (; i + (B - 1) * TP < cnt; i += B * TP) {
+      for (; i < cnt; i += B * TP) {   // predicated batches: no serial one-load-per-round tail
         double v[B];
 #pragma unroll
-        for (int u = 0; u < B; ++u) v[u] = sd[i * is + u * stp];
+        for (int u = 0; u < B; ++u) v[u] = i + u * TP < cnt ? sd[i * is + u * stp] : 0.0;
 #pragma unroll
         for (int u = 0; u < B; ++u) s += v[u];
       }
-      for (; i < cnt; i += TP) s += sd[i * is];
     } else {
       const float* sf = src + base;
-      for (; i + (B - 1) * TP < cnt; i += B * TP) {
+      for (; i < cnt; i += B * TP) {
         float v[B];
 #pragma unroll
-        for (int u = 0; u < B; ++u) v[u] = sf[i * is + u * stp];
+        for (int u = 0; u < B; ++u) v[u] = i + u * TP < cnt ? sf[i * is + u * stp] : 0.f;
 #pragma unroll
         for (int u = 0; u < B; ++u) s += v[u];
       }
-      for (; i < cnt; i += TP) s += sf[i * is];
     }
   }
   red[t] = s;

@@ -1449,7 +1449,7 @@ __global__ __launch_bounds__(256) void convt_dw_pair_kernel(
     const T* __restrict__ x, long long xns, const float* __restrict__ dy, long long dyns,
     float* __restrict__ part, float* __restrict__ bsum, int Ci, int Co, int D, int H, int W,
     int SCH, int nsc) {
-  L3U_STAMP_SCOPE(107);
+  L3U_STAMP_SCOPE(109);
   convt_dw_pair_body<T, NJ, NG>(blockIdx.x, blockIdx.y, x, xns, dy, dyns, part, bsum, Ci, Co, D, H, W,
                                 SCH, nsc);
 }

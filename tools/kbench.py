@@ -18,7 +18,23 @@ SHAPES = [tuple(int(v) for v in t.split(",")) for t in os.environ.get(
     "KB_SHAPES", "4,32,48 4,16,48 4,64,24 4,32,24 4,16,24 4,128,12 4,64,12").split()]
 
 
+FLUSH = None
+
+
 def timeit(fn, iters):
+    if FLUSH is not None:   # cold: a 512 MiB write evicts the 256 MiB MALL before every call
+        for _ in range(2):
+            fn()
+        tot = 0.0
+        for _ in range(iters):
+            FLUSH.add_(1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            tot += e0.elapsed_time(e1)
+        return tot / iters * 1e3
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
@@ -35,7 +51,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--which", default="bwd,bwd1,bwdacc,fwd,fwd1")
+    ap.add_argument("--cold", action="store_true", help="evict the caches before every call")
     a = ap.parse_args()
+    global FLUSH
+    if a.cold:
+        FLUSH = torch.zeros(128 << 20, device="cuda:0")
     dev = torch.device("cuda:0")
     st = nat.stream()
     tag = os.path.basename(os.environ.get("L3U_LIB", "default"))

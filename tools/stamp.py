@@ -32,7 +32,7 @@ TICK_US = 0.01   # wall_clock64: 100 MHz
 
 def kernel_names():
     names = {}
-    for f in ("pwconv", "dwconv", "norm", "misc", "dwpw"):
+    for f in ("pwconv", "dwconv", "norm", "misc", "dwpw", "convt"):
         src = open(os.path.join(ROOT, "light-3d-unet-front_amd", "csrc", f + ".hip")).read()
         for m in re.finditer(r"L3U_STAMP_SCOPE\((\d+)\)", src):
             head = src[:m.start()]
