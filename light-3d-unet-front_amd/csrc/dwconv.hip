@@ -1122,7 +1122,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GL ? (MODE 
 // that own no voxel, so every wave issues exactly one store per output plane and the DMA waits
 // are exact compile-time counts that include the stores.
 // ------------------------------------------------------------------------------------------------
-constexpr int kDwfPd = 2;   // planes in flight ahead of the one being consumed
+#ifndef L3U_DWF_PD
+#define L3U_DWF_PD 2
+#endif
+constexpr int kDwfPd = L3U_DWF_PD;   // planes in flight ahead of the one being consumed
 #ifndef L3U_DWF_GL
 #define L3U_DWF_GL 1
 #endif

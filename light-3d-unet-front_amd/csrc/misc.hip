@@ -457,15 +457,19 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
       const long long stp = is4 * TP;
       long long i = k;
       constexpr int B = kSegBatch;
-      for (; i < cnt; i += B * TP) {   // every batch's loads in flight at once (no serial tail)
+      // every batch's loads in flight at once, the tail too: clamped (always valid) addresses and
+      // unconditional loads, the out-of-range terms dropped by a select AFTER the load (a
+      // predicated load made the compiler branch around each load with a vmcnt(0) inside)
+      for (; i < cnt; i += B * TP) {
         f4 v[B];
 #pragma unroll
-        for (int u = 0; u < B; ++u)
-          v[u] = i + u * TP < cnt ? sf[i * is4 + u * stp] : f4{0.f, 0.f, 0.f, 0.f};
+        for (int u = 0; u < B; ++u) v[u] = sf[min(i + u * TP, cnt - 1) * is4];
 #pragma unroll
-        for (int u = 0; u < B; ++u)
+        for (int u = 0; u < B; ++u) {
+          const bool ok = i + u * TP < cnt;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) s[q] += v[u][q];
+          for (int q = 0; q < 4; ++q) s[q] += ok ? (double)v[u][q] : 0.0;
+        }
       }
     }
 #pragma unroll
@@ -490,21 +494,21 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
     constexpr int B = kSegBatch;   // loads in flight per thread
     if (it[7]) {
       const double* sd = reinterpret_cast<const double*>(src) + base;
-      for (; i < cnt; i += B * TP) {   // predicated batches: no serial one-load-per-round tail
+      for (; i < cnt; i += B * TP) {   // clamped unconditional loads, select after (no serial tail)
         double v[B];
 #pragma unroll
-        for (int u = 0; u < B; ++u) v[u] = i + u * TP < cnt ? sd[i * is + u * stp] : 0.0;
+        for (int u = 0; u < B; ++u) v[u] = sd[min(i + u * TP, cnt - 1) * is];
 #pragma unroll
-        for (int u = 0; u < B; ++u) s += v[u];
+        for (int u = 0; u < B; ++u) s += i + u * TP < cnt ? v[u] : 0.0;
       }
     } else {
       const float* sf = src + base;
       for (; i < cnt; i += B * TP) {
         float v[B];
 #pragma unroll
-        for (int u = 0; u < B; ++u) v[u] = i + u * TP < cnt ? sf[i * is + u * stp] : 0.f;
+        for (int u = 0; u < B; ++u) v[u] = sf[min(i + u * TP, cnt - 1) * is];
 #pragma unroll
-        for (int u = 0; u < B; ++u) s += v[u];
+        for (int u = 0; u < B; ++u) s += i + u * TP < cnt ? (double)v[u] : 0.0;
       }
     }
   }

@@ -447,6 +447,93 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
   }
 }
 
+// One-wave form for the mid-size levels (4096 <= S < 32768: 24^3) with K <= 64: a 64-thread
+// workgroup owns one 64-voxel tile x 16 NC output channels and runs the WHOLE reduction in
+// registers (K / 4 float4 loads of X in flight, then K / 4 * 4 * NC MFMAs in one chain per
+// accumulator, the pw_fwd k order), so there is no cross-wave LDS combine and no 32 KB LDS
+// tile per workgroup (pw_fwd_ks at 24^3: four waves of one k-step each, five workgroups per CU,
+// two rounds of waves).  Same epilogue and (count, mean, M2) partials per 64-voxel tile as
+// pw_fwd_ks (l3u_pw_stat_nsb is unchanged).
+template <typename T, int NC, int KS>
+__global__ __launch_bounds__(64) void pw_fwd_w1_kernel(
+    const T* __restrict__ x, long long xns, const float* __restrict__ w, int wl,
+    const float* __restrict__ bias, T* __restrict__ y, long long yns, int accumulate,
+    float* __restrict__ stat_part, int K, int Nout, int S, int nsb,
+    const T* __restrict__ x2, long long xns2, const float* __restrict__ w2, T* __restrict__ y2,
+    long long yns2, float* __restrict__ stat2, int N1) {
+  L3U_STAMP_SCOPE(110);
+  const int l = threadIdx.x, lr = l & 15, lk = l >> 4;
+  const int sb = blockIdx.x, co0 = blockIdx.y * 16 * NC;
+  int n = blockIdx.z;
+  if (x2 != nullptr && n >= N1) {   // the second problem of a paired launch (l3u_pw_fwd2)
+    n -= N1; x = x2; xns = xns2; w = w2; y = y2; yns = yns2; stat_part = stat2;
+  }
+  const T* xn = x + (long long)n * xns;
+  const int sv = sb * 64 + 4 * lr;
+  f4 a[KS];
+  float b[KS][NC];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int kk = 4 * ks + lk;
+    a[ks] = load_x4<true, false>(xn, kk, K, sv, S, S, 0, 0);
+#pragma unroll
+    for (int m = 0; m < NC; ++m) {
+      const int co = co0 + 16 * m + lr;
+      b[ks][m] = (kk < K && co < Nout) ? (wl == 0 ? w[(long long)co * K + kk] : w[(long long)kk * Nout + co]) : 0.f;
+    }
+  }
+  f4 acc[NC][4];
+#pragma unroll
+  for (int m = 0; m < NC; ++m)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[m][q] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int m = 0; m < NC; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[m][q] = mfma4(b[ks][m], a[ks][q], acc[m][q]);
+  // epilogue: lane (lr, lk) holds Y[co0 + 16m + 4lk + r][sb*64 + 4lr + q]
+  T* yn = y + (long long)n * yns;
+  const int cnt = min(64, S - sb * 64);
+#pragma unroll
+  for (int m = 0; m < NC; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + 16 * m + 4 * lk + r;
+      const bool cok = co < Nout;
+      const float bv = (bias && cok) ? bias[co] : 0.f;
+      f4 v = f4{acc[m][0][r], acc[m][1][r], acc[m][2][r], acc[m][3][r]} + bv;
+      T* dst = yn + (long long)co * S + sv;
+      if (cok && sv < S) {
+        if (accumulate) v += ldv4(dst);
+        stv4(dst, v);
+      }
+      v = round_to(v, dst);   // statistics of the stored values
+      if (stat_part != nullptr) {
+        float ls = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (sv + q < S) ls += v[q];
+        const float mean = row_sum16(ls) / (float)cnt;
+        float m2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (sv + q < S) {
+            const float d = v[q] - mean;
+            m2 = fmaf(d, d, m2);
+          }
+        m2 = row_sum16(m2);
+        if (lr == 0 && cok) {
+          float* o = stat_part + (((long long)n * Nout + co) * nsb + sb) * 3;
+          o[0] = (float)cnt;
+          o[1] = mean;
+          o[2] = m2;
+        }
+      }
+    }
+}
+
 // dW[j][k] partial over one voxel chunk of one sample.  A = dY (rows j), B = X^T (cols k),
 // the MFMA k-dimension is the voxel: lane l loads float4 dY[j0+16mo+(l&15)][s+4(l>>4)..+3] and
 // X[k0+16mi+(l&15)][s+4(l>>4)..+3]; component q feeds MFMA q.
@@ -1493,6 +1580,12 @@ constexpr int kPwks8MaxWg = 1024;   // grids up to this many workgroups take all
 // K split across the 4 waves (pw_fwd_ks_kernel) for small volumes with a deep enough reduction
 constexpr int kPwKsMaxS = 32768;
 bool pw_use_ks(int S, int K) { return S < kPwKsMaxS && K >= kPwKsMinK; }
+// the one-wave form (pw_fwd_w1_kernel) of the K-split range from this volume on
+#ifndef L3U_PW_W1
+#define L3U_PW_W1 1
+#endif
+constexpr bool kPwW1 = L3U_PW_W1 != 0;
+constexpr int kPwW1MinS = 4096;
 
 }  // namespace
 
@@ -1516,6 +1609,21 @@ int pw_launch(const T* x, long long x_nstride, const float* w, int w_layout, con
   L3U_REQUIRE(N > 0 && K > 0 && Nout > 0 && S > 0);
   const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (y_nstride % 4 == 0) &&
                    (xm == 0 || Wq % 4 == 0);
+  if (kPwW1 && pw_use_ks(S, K) && xm == 0 && vec && S >= kPwW1MinS && K <= 64) {
+    // one-wave tiles with the whole reduction in registers (pw_fwd_w1_kernel)
+    const int nsb = (S + 63) / 64;
+    const int NC = Nout <= 16 ? 1 : 2;
+    dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), NZ), block(64);
+    const int KSn = K <= 16 ? 4 : (K <= 32 ? 8 : 16);
+#define PW1(NC_, KS_) hipLaunchKernelGGL((pw_fwd_w1_kernel<T, NC_, KS_>), grid, block, 0, stream, x, \
+      x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, p2.x, p2.xns, \
+      p2.w, p2.y, p2.yns, p2.stat, N)
+#define PW1_K(NC_) do { if (KSn == 4) PW1(NC_, 4); else if (KSn == 8) PW1(NC_, 8); else PW1(NC_, 16); } while (0)
+    if (NC == 1) PW1_K(1); else PW1_K(2);
+#undef PW1_K
+#undef PW1
+    L3U_CHECK_LAUNCH();
+  }
   if (pw_use_ks(S, K) && !(xm == 1 && K < kConvtKsMinK)) {
     // co tile: as wide as possible while keeping >= 256 workgroups
     const int nsb = (S + 63) / 64;
