@@ -698,8 +698,11 @@ __global__ __launch_bounds__(256) void dw3q_dw_kernel(
 // ------------------------------------------------------------------------------------------------
 // the single-pass backward: occupancy target and register prefetch depth of the register-staged
 // form; the LDS-DMA form's DMA ring depth and occupancy (the IN-fused MODE 1: 3 waves, 4 spill)
+#ifndef L3U_DWG_PD
+#define L3U_DWG_PD 1
+#endif
 constexpr int kDwpWaves = 3, kDwpPd = 2;
-constexpr int kDwgPd = 1, kDwgWaves = 4, kDwgWaves1 = 3;
+constexpr int kDwgPd = L3U_DWG_PD, kDwgWaves = 4, kDwgWaves1 = 3;
 
 template <class F, int... I>
 L3U_DEV void run_steps(F& f, std::integer_sequence<int, I...>) {
@@ -1130,6 +1133,10 @@ constexpr int kDwfPd = L3U_DWF_PD;   // planes in flight ahead of the one being 
 #define L3U_DWF_GL 1
 #endif
 constexpr bool kDwfGl = L3U_DWF_GL != 0;   // the forward on dw3g_fwd_kernel (0: dw3q_fwd)
+#ifndef L3U_DWF_AUX
+#define L3U_DWF_AUX 0
+#endif
+constexpr int kDwfAux = L3U_DWF_AUX;   // cache bits of the output stores (16: sc1 write-through, 2: nt)
 
 template <int TZC, int NS, int PD>
 constexpr int gf_younger(int s) {   // vm ops younger than plane s's DMAs when step s waits
@@ -1292,9 +1299,9 @@ __global__ __launch_bounds__(64) void dw3g_fwd_kernel(
       if constexpr (BH) {
         const b4_t ob = __builtin_convertvector(o, b4_t);
         typedef unsigned u2v __attribute__((ext_vector_type(2)));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ob), yr, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, ob), yr, off, 0, kDwfAux);
       } else {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f4, o), yr, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f4, o), yr, off, 0, kDwfAux);
       }
     }
 #pragma unroll

@@ -1586,6 +1586,7 @@ bool pw_use_ks(int S, int K) { return S < kPwKsMaxS && K >= kPwKsMinK; }
 #endif
 constexpr bool kPwW1 = L3U_PW_W1 != 0;
 constexpr int kPwW1MinS = 4096;
+constexpr int kPwW1MaxK = 32;   // K = 64 (the 24^3 decoder pair 64 -> 32): 16.2 -> 18.0 us, kept on pw_fwd_ks
 
 }  // namespace
 
@@ -1609,16 +1610,16 @@ int pw_launch(const T* x, long long x_nstride, const float* w, int w_layout, con
   L3U_REQUIRE(N > 0 && K > 0 && Nout > 0 && S > 0);
   const bool vec = (S % 4 == 0) && (x_nstride % 4 == 0) && (y_nstride % 4 == 0) &&
                    (xm == 0 || Wq % 4 == 0);
-  if (kPwW1 && pw_use_ks(S, K) && xm == 0 && vec && S >= kPwW1MinS && K <= 64) {
+  if (kPwW1 && pw_use_ks(S, K) && xm == 0 && vec && S >= kPwW1MinS && K <= kPwW1MaxK) {
     // one-wave tiles with the whole reduction in registers (pw_fwd_w1_kernel)
     const int nsb = (S + 63) / 64;
     const int NC = Nout <= 16 ? 1 : 2;
     dim3 grid(nsb, (Nout + 16 * NC - 1) / (16 * NC), NZ), block(64);
-    const int KSn = K <= 16 ? 4 : (K <= 32 ? 8 : 16);
+    const int KSn = K <= 16 ? 4 : 8;
 #define PW1(NC_, KS_) hipLaunchKernelGGL((pw_fwd_w1_kernel<T, NC_, KS_>), grid, block, 0, stream, x, \
       x_nstride, w, w_layout, bias, y, y_nstride, accumulate, stat_part, K, Nout, S, nsb, p2.x, p2.xns, \
       p2.w, p2.y, p2.yns, p2.stat, N)
-#define PW1_K(NC_) do { if (KSn == 4) PW1(NC_, 4); else if (KSn == 8) PW1(NC_, 8); else PW1(NC_, 16); } while (0)
+#define PW1_K(NC_) do { if (KSn == 4) PW1(NC_, 4); else PW1(NC_, 8); } while (0)
     if (NC == 1) PW1_K(1); else PW1_K(2);
 #undef PW1_K
 #undef PW1
@@ -1726,7 +1727,10 @@ constexpr int kConvtPairMaxS = 8192;
 constexpr int kCtwMinBlocks = 512;
 constexpr int kConvtOnepassAnyw = 0;   // 1: W % 4 != 0 (6^3) by scalar gathers (measured 8 us slower)
 constexpr int kConvtOnepassMaxS = 8192;
-constexpr int kPwbfMinBlocks = 256;   // A/B r3: 256 -4 us/step (3 of 3), 128 +17 us, vs 512
+#ifndef L3U_PWBF_MINBLK
+#define L3U_PWBF_MINBLK 256
+#endif
+constexpr int kPwbfMinBlocks = L3U_PWBF_MINBLK;   // A/B r3: 256 -4 us/step (3 of 3), 128 +17 us, vs 512
 
 // wide form: J a multiple of 64 (<= 128), any K; narrow form: J <= 32, K <= 64
 constexpr int kPwBwdWide = 1;

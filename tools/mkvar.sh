@@ -22,5 +22,5 @@ for f in $SRCD/*.hip; do
     -I$SRCD -I${INCD:-$R/include} $2 -c $f -o $B/$b.o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $P/lib/var_$1.so $B/*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/var.so $B/*.o && mv -f $B/var.so $P/lib/var_$1.so
 echo built $P/lib/var_$1.so

@@ -3,7 +3,9 @@ for every launch of at most 65536 waves, when each wave began and ended (wall cl
 so that a launch's time splits into dispatch spread, wave bodies and the boundary to the next.
 
     bash tools/mkvar.sh stamp -DL3U_STAMP
-    L3U_LIB=$PWD/light-3d-unet-front_amd/lib/var_stamp.so python tools/stamp.py [out.json]
+    L3U_LIB=$PWD/light-3d-unet-front_amd/lib/var_stamp.so python tools/stamp.py [out.json [dump.json]]
+    (STAMP_DUMP_ID=<kernel id>: every wave of that kernel in the last replay, with the engine's
+    reduction items, into dump.json)
 
 Per launch (in step order): kernel, waves, gap = its first wave begin - the previous stamped
 launch's last wave end (the kernel boundary when both are stamped; larger when an unstamped big
@@ -93,6 +95,13 @@ def main():
         rec = np.frombuffer(buf.cpu().numpy().tobytes(), dtype=dt)
         rec = rec[rec["pad"] == 1]   # written slots
         runs.append(launches(rec))
+    dump_id = int(os.environ.get("STAMP_DUMP_ID", "0"))
+    if dump_id and len(sys.argv) > 2:   # every wave of that kernel in the last replay + the items
+        r = rec[rec["id"] == dump_id]
+        items = {str(k): v.cpu().tolist() for k, v in m.engine._items.items()}
+        with open(sys.argv[2], "w") as f:
+            json.dump({"id": dump_id, "blk": r["blk"].tolist(), "t0": r["t0"].tolist(),
+                       "t1": r["t1"].tolist(), "items": items}, f)
     nl = min(len(r) for r in runs)
     rows = []
     for i in range(nl):
