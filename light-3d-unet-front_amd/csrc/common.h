@@ -204,32 +204,60 @@ L3U_DEV void record_from(const l3u_norm_src& s, const RecIn& q, int n, int c, in
 // Merge the (count, mean, M2) partials of one (n, c) with the 64 lanes of the calling wave and
 // build the 8-float record.  Two passes of plain wave sums (DPP, no LDS): the total count and
 // sum of count * mean give the mean; then every partial's M2 plus count * (mean_i - mean)^2 --
-// all non-negative terms -- sum to the M2 of the whole (n, c).  The lane-strided loads of 8
-// partials per lane are issued together (one memory latency for up to 512 partials; longer lists
-// re-read them in the second pass).  Fixed order: every caller for the same (n, c) gets
-// bit-identical values.  (Round 4 merged pairs with Chan's formula along a 6-round shuffle tree:
-// ~3.5 us on the critical path of every IN-consuming small-level launch, wave stamps r5d.)
-// Must be called by a full wave; returns the record in `r` on every lane.
-L3U_DEV void finalize_record(const l3u_norm_src& s, int n, int c, int C, float r[kRec]) {
-  const int l = threadIdx.x & 63;
-  const RecIn q = record_inputs(s, c);
-  const float* p = s.stat_part + ((long long)n * C + c) * s.nsb * 3;
+// all non-negative terms -- sum to the M2 of the whole (n, c).  Fixed order: every caller for
+// the same (n, c) gets bit-identical values.  (Round 4 merged pairs with Chan's formula along a
+// 6-round shuffle tree: ~3.5 us on the critical path of every IN-consuming small-level launch,
+// wave stamps r5d.)  Must be called by a full wave; returns the record in `r` on every lane.
+//
+// Split in two so that a consumer can request the partials FIRST, before its data loads, and
+// finish the record after issuing them (record_pre / record_finish): up to 512 partials are 8
+// clamped unconditional loads per lane in straight-line code (a loop, or a branch around each
+// load, makes hipcc wait for every outstanding load -- vmcnt(0) -- before requesting them).
+struct RecPre {
   float v[8][3];
+  RecIn q;
+};
+// raw loads only (the masking happens at the first use, in record_finish: a select right here
+// would make hipcc wait for the loads before the caller's next requests)
+L3U_DEV void rec_fetch8(const float* p, int nsb, int i0, float (&v)[8][3]) {
 #pragma unroll
-  for (int u = 0; u < 8; ++u) v[u][0] = v[u][1] = v[u][2] = 0.f;
-  auto fetch = [&](int i0) {
+  for (int u = 0; u < 8; ++u) {
+    const int ic = min(i0 + 64 * u, nsb - 1);
+    v[u][0] = p[ic * 3];
+    v[u][1] = p[ic * 3 + 1];
+    v[u][2] = p[ic * 3 + 2];
+  }
+}
+L3U_DEV void rec_mask8(int nsb, int i0, float (&v)[8][3]) {   // zero the entries past the list
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + 64 * u;
-      v[u][0] = v[u][1] = v[u][2] = 0.f;
-      if (i < s.nsb) { v[u][0] = p[i * 3]; v[u][1] = p[i * 3 + 1]; v[u][2] = p[i * 3 + 2]; }
-    }
-  };
+  for (int u = 0; u < 8; ++u) {
+    const bool ok = i0 + 64 * u < nsb;
+    v[u][0] = ok ? v[u][0] : 0.f;
+    v[u][1] = ok ? v[u][1] : 0.f;
+    v[u][2] = ok ? v[u][2] : 0.f;
+  }
+}
+L3U_DEV void record_pre(const l3u_norm_src& s, int n, int c, int C, RecPre& rp) {
+  rp.q = record_inputs(s, c);
+  const float* p = s.stat_part + ((long long)n * C + c) * s.nsb * 3;
+  if (s.nsb <= 512) rec_fetch8(p, s.nsb, threadIdx.x & 63, rp.v);
+}
+L3U_DEV void record_finish(const l3u_norm_src& s, RecPre& rp, int n, int c, int C, float r[kRec]) {
+  const int l = threadIdx.x & 63;
+  const float* p = s.stat_part + ((long long)n * C + c) * s.nsb * 3;
+  float (&v)[8][3] = rp.v;
   float cs = 0.f, ms = 0.f;
-  for (int i0 = l; i0 < s.nsb; i0 += 512) {
-    fetch(i0);
+  if (s.nsb <= 512) {
+    rec_mask8(s.nsb, l, v);
 #pragma unroll
     for (int u = 0; u < 8; ++u) { cs += v[u][0]; ms = fmaf(v[u][0], v[u][1], ms); }
+  } else {   // long lists (config 5's 64^3 GEMMs: 1024 partials): re-read in the second pass
+    for (int i0 = l; i0 < s.nsb; i0 += 512) {
+      rec_fetch8(p, s.nsb, i0, v);
+      rec_mask8(s.nsb, i0, v);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { cs += v[u][0]; ms = fmaf(v[u][0], v[u][1], ms); }
+    }
   }
   const float cn = wave_sum(cs);
   const float mu = cn > 0.f ? wave_sum(ms) / cn : 0.f;
@@ -245,11 +273,17 @@ L3U_DEV void finalize_record(const l3u_norm_src& s, int n, int c, int C, float r
     add_m2();   // the lane's partials are still in registers (zeros where it holds none)
   } else {
     for (int i0 = l; i0 < s.nsb; i0 += 512) {
-      fetch(i0);
+      rec_fetch8(p, s.nsb, i0, v);
+      rec_mask8(s.nsb, i0, v);
       add_m2();
     }
   }
-  record_from(s, q, n, c, C, cn, mu, wave_sum(m2), r);
+  record_from(s, rp.q, n, c, C, cn, mu, wave_sum(m2), r);
+}
+L3U_DEV void finalize_record(const l3u_norm_src& s, int n, int c, int C, float r[kRec]) {
+  RecPre rp;
+  record_pre(s, n, c, C, rp);
+  record_finish(s, rp, n, c, C, r);
 }
 
 // The record of (n, c) from its merged (count, mean, M2): rstd, the affine parameters and the
@@ -287,41 +321,6 @@ L3U_DEV void block_record(const l3u_norm_src& s, int n, int c, int C, bool store
     if (threadIdx.x == 0) {
 #pragma unroll
       for (int i = 0; i < kRec; ++i) sh8[i] = r[i];
-      if (store && s.rec_out) {
-        float* o = s.rec_out + ((long long)n * C + c) * kRec;
-#pragma unroll
-        for (int i = 0; i < kRec; ++i) o[i] = r[i];
-      }
-    }
-  }
-  __syncthreads();
-}
-
-// Two records at once (waves 0 and 1 merge in parallel), one barrier; sh8: 16 floats of LDS.
-L3U_DEV void block_record2(const l3u_norm_src& a, const l3u_norm_src& b, bool has_b, int n, int c,
-                           int C, bool store, float* sh8) {
-  const int wv = threadIdx.x >> 6;
-  if (wv == 0 || (wv == 1 && has_b)) {
-    // field-wise selects: a reference picked at run time between the two by-value kernel
-    // arguments made the compiler copy both to scratch in every thread (120 B of private
-    // memory per thread, ~25 MB of HBM writes per 48^3 launch, profiles/r1i_pmc_step.json)
-    const bool q = wv == 0;
-    l3u_norm_src s;
-    s.stat_part = q ? a.stat_part : b.stat_part;
-    s.nsb = q ? a.nsb : b.nsb;
-    s.layer = q ? a.layer : b.layer;
-    s.gamma = q ? a.gamma : b.gamma;
-    s.beta = q ? a.beta : b.beta;
-    s.drop_p = q ? a.drop_p : b.drop_p;
-    s.seed = q ? a.seed : b.seed;
-    s.step = q ? a.step : b.step;
-    s.rec_out = q ? a.rec_out : b.rec_out;
-    s.rank1 = q ? a.rank1 : b.rank1;
-    float r[kRec];
-    finalize_record(s, n, c, C, r);
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-      for (int i = 0; i < kRec; ++i) sh8[wv * 8 + i] = r[i];
       if (store && s.rec_out) {
         float* o = s.rec_out + ((long long)n * C + c) * kRec;
 #pragma unroll

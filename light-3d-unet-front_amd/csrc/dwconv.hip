@@ -1134,9 +1134,11 @@ constexpr int kDwfPd = L3U_DWF_PD;   // planes in flight ahead of the one being 
 #endif
 constexpr bool kDwfGl = L3U_DWF_GL != 0;   // the forward on dw3g_fwd_kernel (0: dw3q_fwd)
 #ifndef L3U_DWF_AUX
-#define L3U_DWF_AUX 0
+#define L3U_DWF_AUX 2
 #endif
-constexpr int kDwfAux = L3U_DWF_AUX;   // cache bits of the output stores (16: sc1 write-through, 2: nt)
+// cache bits of the output stores: 2 = nt (r5 A/B vs 0: -2..-3.5 us/step; 16 = sc1
+// write-through -1..-2 us)
+constexpr int kDwfAux = L3U_DWF_AUX;
 
 template <int TZC, int NS, int PD>
 constexpr int gf_younger(int s) {   // vm ops younger than plane s's DMAs when step s waits
@@ -1197,6 +1199,8 @@ __global__ __launch_bounds__(64) void dw3g_fwd_kernel(
       }
     }
   };
+  RecPre rp;
+  if (XF && has_src) record_pre(src, b.n, b.c, C, rp);   // the partials, beside the first DMAs
   run_steps(gissue, std::make_integer_sequence<int, PD>{});
   // taps: pair (kd 2, kd 1) and kd 0 per in-plane tap t = r * 3 + dx
   f2 wp[9];
@@ -1208,10 +1212,15 @@ __global__ __launch_bounds__(64) void dw3g_fwd_kernel(
   }
   float sc = 1.f, sh = 0.f, mu = 0.f, rks = 1.f;
   if (XF) {
-    if (has_src) {
-      float* s8 = lds + (BH ? GNB * 256 : GNB * GPS);
-      block_record(src, b.n, b.c, C, b.ck == 0, s8);
-      mu = s8[0]; sc = s8[2]; sh = s8[3]; rks = s8[7];
+    if (has_src) {   // one-wave tiles: the wave merges the record itself
+      float r8[kRec];
+      record_finish(src, rp, b.n, b.c, C, r8);
+      mu = r8[0]; sc = r8[2]; sh = r8[3]; rks = r8[7];
+      if (b.ck == 0 && threadIdx.x == 0 && src.rec_out) {
+        float* o = src.rec_out + (long long)b.nc * kRec;
+#pragma unroll
+        for (int i = 0; i < kRec; ++i) o[i] = r8[i];
+      }
     } else {
       const float* r = rec + (long long)b.nc * kRec;
       mu = r[0]; sc = r[2]; sh = r[3]; rks = r[7];
@@ -1376,6 +1385,10 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int nc = blockIdx.x, c = nc % C, n = nc / C;
   const long long HW = (long long)H * W, S = D * HW, cofs = (long long)c * S;
+  // the record's partials are requested first, the volume right behind them; every wave merges
+  // the record itself (no divergent merge, no LDS broadcast, no barrier)
+  RecPre rp;
+  if ((XF || EPI == 1) && has_src) record_pre(src, n, c, C, rp);
   float raw[kVR];
   v_fetch(raw, x + (long long)n * xns + cofs, D, H, W);
   float wk[27];
@@ -1384,10 +1397,14 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
   float sc = 1.f, sh = 0.f, mu = 0.f, rstd = 1.f, kk = 1.f;
   if (XF || EPI == 1) {
     if (has_src) {
-      float* s8 = lds;
-      block_record(src, n, c, C, true, s8);
-      mu = s8[0]; rstd = s8[1]; sc = s8[2]; sh = s8[3]; kk = s8[4];
-      __syncthreads();
+      float r8[kRec];
+      record_finish(src, rp, n, c, C, r8);
+      mu = r8[0]; rstd = r8[1]; sc = r8[2]; sh = r8[3]; kk = r8[4];
+      if (threadIdx.x == 0 && src.rec_out) {
+        float* o = src.rec_out + (long long)nc * kRec;
+#pragma unroll
+        for (int i = 0; i < kRec; ++i) o[i] = r8[i];
+      }
     } else {
       const float* r = rec + (long long)nc * kRec;
       mu = r[0]; rstd = r[1]; sc = r[2]; sh = r[3]; kk = r[4];

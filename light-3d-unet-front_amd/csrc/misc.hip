@@ -454,7 +454,6 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
     double s[4] = {0.0, 0.0, 0.0, 0.0};
     if (k < TP) {
       const f4* sf = reinterpret_cast<const f4*>(src + it[0]) + o4;
-      const long long stp = is4 * TP;
       long long i = k;
       constexpr int B = kSegBatch;
       // every batch's loads in flight at once, the tail too: clamped (always valid) addresses and
@@ -489,7 +488,6 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
   double s = 0.0;
   if (k < TP) {
     const long long base = it[0] + o * it[3];
-    const long long stp = is * TP;
     long long i = k;
     constexpr int B = kSegBatch;   // loads in flight per thread
     if (it[7]) {

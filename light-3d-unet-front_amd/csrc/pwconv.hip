@@ -791,12 +791,26 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
     const int j = tid / PS, sub = tid % PS;
     double t0 = 0.0, t1 = 0.0;
     if (j < J) {
-      if (PRO == 2) {   // block-tail partials [J][N][npart][3]: {sum g, sum g*xhat2, sum g*xhat_r}
-        const double* pp = in_part + ((long long)j * N + n) * npart * 3;
-        for (int i = sub; i < npart; i += PS) { t0 += pp[i * 3]; t1 += pp[i * 3 + sel]; }
-      } else {
-        const double* pp = in_part + ((long long)j * N + n) * npart * 2;
-        for (int i = sub; i < npart; i += PS) { t0 += pp[i * 2]; t1 += pp[i * 2 + 1]; }
+      // block-tail partials [J][N][npart][3]: {sum g, sum g*xhat2, sum g*xhat_r} (PRO 2), or the
+      // depthwise backward's IN partials [J][N][npart][2] (PRO 1); a lane's share (i = sub,
+      // sub + PS, ..., up to 40 partials at 48^3) in batches of 8 clamped unconditional loads: one
+      // memory round trip per batch instead of one per partial (same order of the adds)
+      const int st = PRO == 2 ? 3 : 2, o1 = PRO == 2 ? sel : 1;
+      const double* pp = in_part + ((long long)j * N + n) * npart * st;
+      for (int i0 = sub; i0 < npart; i0 += 8 * PS) {
+        double a0[8], a1[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = min(i0 + u * PS, npart - 1);
+          a0[u] = pp[i * st];
+          a1[u] = pp[i * st + o1];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const bool ok = i0 + u * PS < npart;
+          t0 += ok ? a0[u] : 0.0;
+          t1 += ok ? a1[u] : 0.0;
+        }
       }
     }
     psum[tid * 2] = t0;
@@ -1728,9 +1742,12 @@ constexpr int kCtwMinBlocks = 512;
 constexpr int kConvtOnepassAnyw = 0;   // 1: W % 4 != 0 (6^3) by scalar gathers (measured 8 us slower)
 constexpr int kConvtOnepassMaxS = 8192;
 #ifndef L3U_PWBF_MINBLK
-#define L3U_PWBF_MINBLK 256
+#define L3U_PWBF_MINBLK 512
 #endif
-constexpr int kPwbfMinBlocks = L3U_PWBF_MINBLK;   // A/B r3: 256 -4 us/step (3 of 3), 128 +17 us, vs 512
+// fewest workgroups of a fused pointwise backward (K split in 16-column blocks until reached):
+// r5 A/B 512 vs 256 -11.5 us/step (the 24^3 pair goes from 432 to 864 workgroups, dY re-read
+// from L2); round 3 measured the opposite on the kernel of then (256 -4 us vs 512)
+constexpr int kPwbfMinBlocks = L3U_PWBF_MINBLK;
 
 // wide form: J a multiple of 64 (<= 128), any K; narrow form: J <= 32, K <= 64
 constexpr int kPwBwdWide = 1;

@@ -30,7 +30,9 @@ _PAIR_PW = os.environ.get("L3U_PAIR_PW", "1") != "0"
 # 32..256 on the 48^3 step (tools/seg_caps.sh); L3U_SEG_CAPS overrides
 # block-tail backward inside the pointwise backwards (l3u_pw_bwd_tail); L3U_TAIL_FUSE=0 disables
 _TAIL_FUSE = os.environ.get("L3U_TAIL_FUSE", "1") != "0"
-_SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32").split(","))
+# (round 5: a fourth class, lists longer than 1024 -- the 48^3 pointwise partials, 1728 per
+# layer -- with 8 outputs per item: 32 threads per output quad, 2 load rounds instead of 7)
+_SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32,8").split(","))
 # conv2 (depthwise + pointwise, InstanceNorm1 on load) as one l3u_dwpw_fwd launch for volumes of
 # at least this many voxels (the 48^3 level; at 24^3 its 1024-thread slabs are too few to fill
 # the chip, tools/dwpw_bench.py); L3U_DWPW=0 disables
@@ -289,7 +291,8 @@ class UNetEngine:
         base = self.offsets[dst_name][0] + dst_elem
         # outputs per item (one 256-thread workgroup each): fewer for long partial lists so that
         # every thread's serial share stays short (256 / cap threads share each output's terms)
-        cap = _SEG_CAPS[0] if count <= 128 else (_SEG_CAPS[1] if count <= 384 else _SEG_CAPS[2])
+        cap = _SEG_CAPS[0] if count <= 128 else (_SEG_CAPS[1] if count <= 384 else (
+            _SEG_CAPS[2] if count <= 1024 or len(_SEG_CAPS) < 4 else _SEG_CAPS[3]))
         t0 = 0
         while t0 < length:
             ln = min(cap, length - t0)
