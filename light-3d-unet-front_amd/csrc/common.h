@@ -331,6 +331,41 @@ L3U_DEV void block_record(const l3u_norm_src& s, int n, int c, int C, bool store
   __syncthreads();
 }
 
+// Two records at once (waves 0 and 1 merge in parallel), one barrier; sh8: 16 floats of LDS.
+L3U_DEV void block_record2(const l3u_norm_src& a, const l3u_norm_src& b, bool has_b, int n, int c,
+                           int C, bool store, float* sh8) {
+  const int wv = threadIdx.x >> 6;
+  if (wv == 0 || (wv == 1 && has_b)) {
+    // field-wise selects: a reference picked at run time between the two by-value kernel
+    // arguments made the compiler copy both to scratch in every thread (120 B of private
+    // memory per thread, ~25 MB of HBM writes per 48^3 launch, profiles/r1i_pmc_step.json)
+    const bool q = wv == 0;
+    l3u_norm_src s;
+    s.stat_part = q ? a.stat_part : b.stat_part;
+    s.nsb = q ? a.nsb : b.nsb;
+    s.layer = q ? a.layer : b.layer;
+    s.gamma = q ? a.gamma : b.gamma;
+    s.beta = q ? a.beta : b.beta;
+    s.drop_p = q ? a.drop_p : b.drop_p;
+    s.seed = q ? a.seed : b.seed;
+    s.step = q ? a.step : b.step;
+    s.rec_out = q ? a.rec_out : b.rec_out;
+    s.rank1 = q ? a.rank1 : b.rank1;
+    float r[kRec];
+    finalize_record(s, n, c, C, r);
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int i = 0; i < kRec; ++i) sh8[wv * 8 + i] = r[i];
+      if (store && s.rec_out) {
+        float* o = s.rec_out + ((long long)n * C + c) * kRec;
+#pragma unroll
+        for (int i = 0; i < kRec; ++i) o[i] = r[i];
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // a / b for 0 <= a < 2^24, b > 0, with inv = 1.f / b: one float multiply and a correction step
 // (the float quotient is within 1 of the exact one) instead of an integer division
 L3U_DEV int fdiv(int a, int b, float inv) {

@@ -27,20 +27,6 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(l3u_norm_src src, int 
   }
 }
 
-// the merged records, stored for the backward by thread 0 of the (n, c)'s first workgroup
-L3U_DEV void store_records(const l3u_norm_src& a, const float (&ra)[kRec], const l3u_norm_src& b,
-                           const float (&rb)[kRec], bool has_b, int nc, bool first) {
-  if (!first || threadIdx.x != 0) return;
-  if (a.rec_out) {
-#pragma unroll
-    for (int i = 0; i < kRec; ++i) a.rec_out[(long long)nc * kRec + i] = ra[i];
-  }
-  if (has_b && b.rec_out) {
-#pragma unroll
-    for (int i = 0; i < kRec; ++i) b.rec_out[(long long)nc * kRec + i] = rb[i];
-  }
-}
-
 // out = lrelu(scale2*(y2-mean2) + shift2 + R),  R = r (identity) or scale_r*(r-mean_r) + shift_r.
 // With HAS_SRC the records are finalized here from the GEMM partials (no in_finalize launch);
 // workgroup x == 0 of each (n, c) stores them for the backward.
@@ -50,6 +36,7 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
     const T* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
     int shortcut, T* __restrict__ out, long long ons, int C, int S) {
   L3U_STAMP_SCOPE(302);
+  __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   // RK (rns < 0): rank-1 residual, record_r[7] * one stored channel (include/l3u.h)
   constexpr bool rk = RK;
@@ -59,20 +46,13 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
   // the first tile is requested before the records are finalized (their partial-sum loads
   // overlap it); every later tile one iteration ahead
   const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4, istep = gridDim.x * 1024;
-  RecPre p2, pr;   // every wave merges the records itself: partials first, then the first tile
-  if (HAS_SRC) {
-    record_pre(src2, n, c, C, p2);
-    if (shortcut) record_pre(srcr, n, c, C, pr);
-  }
   f4 yv = {0.f, 0.f, 0.f, 0.f}, rv = yv;
   if (VEC && i0 < S) { yv = ldv4(yp + i0); rv = ldv4(rp + i0); }
   float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f, rks = 1.f;
   if (HAS_SRC) {
-    float ra[kRec], rb[kRec];
-    record_finish(src2, p2, n, c, C, ra);
-    m2 = ra[0]; a2 = ra[2]; b2 = ra[3];
-    if (shortcut) { record_finish(srcr, pr, n, c, C, rb); mr = rb[0]; ar = rb[2]; br = rb[3]; rks = rb[7]; }
-    store_records(src2, ra, srcr, rb, shortcut != 0, nc, blockIdx.x == 0);
+    block_record2(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh);
+    m2 = sh[0]; a2 = sh[2]; b2 = sh[3];
+    if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; rks = sh[15]; }
   } else {
     m2 = rec2[(long long)nc * kRec + 0];
     a2 = rec2[(long long)nc * kRec + 2];
@@ -115,6 +95,7 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
     int shortcut, T* __restrict__ out, long long ons, T* __restrict__ pooled,
     long long pns, unsigned char* __restrict__ idx, int C, int D, int H, int W) {
   L3U_STAMP_SCOPE(303);
+  __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   const long long S = (long long)D * H * W;
   const int Ho = H / 2, W4 = W / 4;
@@ -142,19 +123,12 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
       rv[j] = ldv4(rp + off);
     }
   };
-  RecPre p2, pr;   // every wave merges the records itself: partials first, then the first block
-  if (HAS_SRC) {
-    record_pre(src2, n, c, C, p2);
-    if (shortcut) record_pre(srcr, n, c, C, pr);
-  }
   if (o0 < Sp) fetch(o0);
   float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f, rks = 1.f;
   if (HAS_SRC) {
-    float ra[kRec], rb[kRec];
-    record_finish(src2, p2, n, c, C, ra);
-    m2 = ra[0]; a2 = ra[2]; b2 = ra[3];
-    if (shortcut) { record_finish(srcr, pr, n, c, C, rb); mr = rb[0]; ar = rb[2]; br = rb[3]; rks = rb[7]; }
-    store_records(src2, ra, srcr, rb, shortcut != 0, nc, blockIdx.x == 0);
+    block_record2(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh);
+    m2 = sh[0]; a2 = sh[2]; b2 = sh[3];
+    if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; rks = sh[15]; }
   } else {
     m2 = rec2[(long long)nc * kRec + 0];
     a2 = rec2[(long long)nc * kRec + 2];

@@ -30,9 +30,9 @@ _PAIR_PW = os.environ.get("L3U_PAIR_PW", "1") != "0"
 # 32..256 on the 48^3 step (tools/seg_caps.sh); L3U_SEG_CAPS overrides
 # block-tail backward inside the pointwise backwards (l3u_pw_bwd_tail); L3U_TAIL_FUSE=0 disables
 _TAIL_FUSE = os.environ.get("L3U_TAIL_FUSE", "1") != "0"
-# (round 5: a fourth class, lists longer than 1024 -- the 48^3 pointwise partials, 1728 per
-# layer -- with 8 outputs per item: 32 threads per output quad, 2 load rounds instead of 7)
-_SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32,8").split(","))
+# (an optional fourth value applies to lists longer than 1024 -- the 48^3 pointwise partials,
+# 1728 per layer: round 5 measured 8 outputs per item there +2.6 us on the reduction launch)
+_SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32").split(","))
 # conv2 (depthwise + pointwise, InstanceNorm1 on load) as one l3u_dwpw_fwd launch for volumes of
 # at least this many voxels (the 48^3 level; at 24^3 its 1024-thread slabs are too few to fill
 # the chip, tools/dwpw_bench.py); L3U_DWPW=0 disables
