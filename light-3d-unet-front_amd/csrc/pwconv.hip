@@ -365,6 +365,9 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
   // consecutive banks, conflict-free).  Every wave parks its partials; wave w then owns output
   // tile m = w (16 channels x 64 voxels) and adds the four waves' partials of that tile in wave
   // order (fixed: deterministic), so the epilogue stores are spread over min(NC, 4) waves.
+#ifdef L3U_STAMP_KS
+  L3U_STAMP_MARK(0);   // stamp variant: the k-loop (loads + MFMAs) done
+#endif
   {
     float* dst = lds + wave * NT * 64 + l;
 #pragma unroll
@@ -375,7 +378,9 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
         for (int r = 0; r < 4; ++r) dst[((m * 4 + q) * 4 + r) * 64] = acc[m][q][r];
   }
   __syncthreads();
+#ifndef L3U_STAMP_KS
   L3U_STAMP_MARK(0);
+#endif
   const int m = wave;
   if (m >= NC) return;
   f4 t4[4];
