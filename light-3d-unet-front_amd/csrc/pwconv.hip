@@ -687,8 +687,18 @@ struct TailSecond {
   float* dx; long long dxns; int accumulate; float* part; int K; int sel;
 };
 
+#ifndef L3U_PWBF_WAVES1
+#define L3U_PWBF_WAVES1 0
+#endif
+// minimum waves per SIMD asked of the 16-row forms with up to 32 columns (0: the compiler's
+// choice, 4 for the block-tail forms at 106-108 VGPRs)
+constexpr int kPwbfWaves1 = L3U_PWBF_WAVES1;
+#ifndef L3U_PWBF_PB
+#define L3U_PWBF_PB 8
+#endif
+constexpr int kPwbfPB = L3U_PWBF_PB;
 template <typename T, int NJ, int NK, int PRO, bool R1 = false, bool R1B = false>
-__global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NJ == 1 && NK <= 2 && kPwbfWaves1 > 0 ? kPwbfWaves1 : 1))) void pw_bwd_fused_kernel(
     const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
     const T* __restrict__ x, long long xns, const float* __restrict__ w,
@@ -802,16 +812,16 @@ __global__ __launch_bounds__(512) void pw_bwd_fused_kernel(
       // memory round trip per batch instead of one per partial (same order of the adds)
       const int st = PRO == 2 ? 3 : 2, o1 = PRO == 2 ? sel : 1;
       const double* pp = in_part + ((long long)j * N + n) * npart * st;
-      for (int i0 = sub; i0 < npart; i0 += 8 * PS) {
-        double a0[8], a1[8];
+      for (int i0 = sub; i0 < npart; i0 += kPwbfPB * PS) {
+        double a0[kPwbfPB], a1[kPwbfPB];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < kPwbfPB; ++u) {
           const int i = min(i0 + u * PS, npart - 1);
           a0[u] = pp[i * st];
           a1[u] = pp[i * st + o1];
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < kPwbfPB; ++u) {
           const bool ok = i0 + u * PS < npart;
           t0 += ok ? a0[u] : 0.0;
           t1 += ok ? a1[u] : 0.0;
