@@ -210,11 +210,32 @@ def _e(name):
     return 2 if name.endswith("_bf16") else 4
 
 
+# reduction items of the recorded step by device pointer (engine._items), for the byte model of
+# the weight-gradient reduction launch
+SEG_ITEMS = {}
+
+
+def seg_items_from(engine):
+    SEG_ITEMS.clear()
+    for t in engine._items.values():
+        SEG_ITEMS[t.data_ptr()] = t.cpu().tolist()
+
+
 def call_bytes(name, a):
     """Algorithmic HBM bytes of one C-ABI call from its arguments (activations e = 4
     (fp32) or 2 (the _bf16 twins), gradients fp32), with a shape label; None when the call is not
-    in the depthwise or GEMM families."""
+    in the depthwise, GEMM or reduction families."""
     e, base = _e(name), name[:-5] if name.endswith("_bf16") else name
+    if base in ("l3u_reduce_segments", "l3u_reduce_segments_adamw") and a[1] in SEG_ITEMS:
+        # (src, items, nitems, ...): every partial read once (fp32, or fp64 for the IN affine
+        # partials), the 64-byte item table, and per output the gradient write plus (adamw) the
+        # parameter and both moments read and written
+        rows = SEG_ITEMS[a[1]]
+        part = sum(r[1] * r[4] * (8 if r[7] else 4) for r in rows)
+        nout = sum(r[4] for r in rows)
+        per = 28 if base.endswith("adamw") else 4
+        return ("reduce", f"{base[4:]} {len(rows)} items, {part / 1e6:.1f} MB partials",
+                part + 64 * len(rows) + per * nout + 4 * sum(r[4] for r in rows if r[6]))
     if base == "l3u_dw3_fwd":     # (x, xns, w, rec, src, y, yns, N, C, D, H, W)
         N, C, D, H, W = a[7:12]
         S = D * H * W
@@ -305,7 +326,7 @@ def family_rooflines(nat_call, calls):
     sel = []
     for name, args in calls:
         r = call_bytes(name, args)
-        if r is not None:
+        if r is not None and r[0] != "reduce":   # (re-running it would apply AdamW again)
             sel.append((name, args, r))
     ms = StepRecorder.time_calls(nat_call, [(n, a) for n, a, _ in sel])
     fam = {"dw": [], "gemm": []}
@@ -366,8 +387,11 @@ def instep_evidence(workload, launches):
            "tree_matches": same_tree,
            "step_kernel_us": rec["step_kernel_us"], "launches": rec["launches"],
            "under_10us": rec.get("under_10us")}
-    for fam in ("dw", "gemm"):
-        out[fam] = {k: rec[fam][k] for k in ("launches", "bytes", "us", "achieved", "frac")}
+    for fam in ("dw", "gemm", "reduce"):
+        if fam in rec:
+            out[fam] = {k: rec[fam][k] for k in ("launches", "bytes", "us", "achieved", "frac")}
+    if "reduce" in rec and rec["reduce"]["calls"]:
+        out["reduce"]["call"] = rec["reduce"]["calls"][0]["call"]
     out["dominant"] = max(rec["dw"]["calls"] + rec["gemm"]["calls"], key=lambda r: r["us"])
     out["family_calls"] = ncalls
     out["matches_this_step"] = (same_tree and (launches is None or rec.get("calls") == launches))
@@ -921,6 +945,7 @@ def main():
     step(xs[2], ts[2])
     torch.cuda.synchronize()
     restore()
+    seg_items_from(model.engine)
     orig = rec.orig
     dom_calls = [(n, a) for n, a in rec.calls if n == dom_name and a[-5] == cdom and a[-4] == args.size]
     dom_ms = StepRecorder.time_calls(orig, dom_calls[:1], reps=50)[0] if dom_calls else None

@@ -39,23 +39,33 @@ typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
 
 L3U_DEV f4_t ldv4(const float* p) { return *reinterpret_cast<const f4_t*>(p); }
 L3U_DEV f4_t ldv4(const bf16* p) { return __builtin_convertvector(*reinterpret_cast<const b4_t*>(p), f4_t); }
-L3U_DEV void stv4(float* p, f4_t v) { *reinterpret_cast<f4_t*>(p) = v; }
-L3U_DEV void stv4(bf16* p, f4_t v) { *reinterpret_cast<b4_t*>(p) = __builtin_convertvector(v, b4_t); }
+// L3U_ST_NT=1: the generic tensor stores below non-temporal (streamed past the XCD's L2, which the
+// next launch cannot hit anyway: the kernel-boundary release writes it back, the acquire
+// invalidates it)
+#ifndef L3U_ST_NT
+#define L3U_ST_NT 0
+#endif
+template <typename V>
+L3U_DEV void st_pol(V* p, V v) {
+  if constexpr (L3U_ST_NT != 0) __builtin_nontemporal_store(v, p); else *p = v;
+}
+L3U_DEV void stv4(float* p, f4_t v) { st_pol(reinterpret_cast<f4_t*>(p), v); }
+L3U_DEV void stv4(bf16* p, f4_t v) { st_pol(reinterpret_cast<b4_t*>(p), __builtin_convertvector(v, b4_t)); }
 L3U_DEV void stv4_nt(float* p, f4_t v) { __builtin_nontemporal_store(v, reinterpret_cast<f4_t*>(p)); }
 L3U_DEV void stv4_nt(bf16* p, f4_t v) {
   __builtin_nontemporal_store(__builtin_convertvector(v, b4_t), reinterpret_cast<b4_t*>(p));
 }
 L3U_DEV f2_t ldv2(const float* p) { return *reinterpret_cast<const f2_t*>(p); }
 L3U_DEV f2_t ldv2(const bf16* p) { return __builtin_convertvector(*reinterpret_cast<const b2_t*>(p), f2_t); }
-L3U_DEV void stv2(float* p, f2_t v) { *reinterpret_cast<f2_t*>(p) = v; }
-L3U_DEV void stv2(bf16* p, f2_t v) { *reinterpret_cast<b2_t*>(p) = __builtin_convertvector(v, b2_t); }
+L3U_DEV void stv2(float* p, f2_t v) { st_pol(reinterpret_cast<f2_t*>(p), v); }
+L3U_DEV void stv2(bf16* p, f2_t v) { st_pol(reinterpret_cast<b2_t*>(p), __builtin_convertvector(v, b2_t)); }
 // v rounded to the storage precision of T (the value a store + reload would give)
 L3U_DEV f4_t round_to(f4_t v, const float*) { return v; }
 L3U_DEV f4_t round_to(f4_t v, const bf16*) { return __builtin_convertvector(__builtin_convertvector(v, b4_t), f4_t); }
 L3U_DEV float ld1(const float* p) { return *p; }
 L3U_DEV float ld1(const bf16* p) { return (float)*p; }
-L3U_DEV void st1(float* p, float v) { *p = v; }
-L3U_DEV void st1(bf16* p, float v) { *p = (bf16)v; }
+L3U_DEV void st1(float* p, float v) { st_pol(p, v); }
+L3U_DEV void st1(bf16* p, float v) { st_pol(p, (bf16)v); }
 
 // a * b rounded on its own, never contracted into a following add (an FMA would round once and
 // differ from the product that was stored: the rank-1 operands must equal the materialised tensor)

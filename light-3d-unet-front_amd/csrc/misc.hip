@@ -436,6 +436,10 @@ constexpr int kSegBatch = 8;   // measured: 8 < 16 < 32 us/step
 #define L3U_SEG_VEC 1
 #endif
 constexpr bool kSegVec = L3U_SEG_VEC != 0;   // float4 rows where the item allows (segment_sum)
+#ifndef L3U_SEG_LONG
+#define L3U_SEG_LONG 32
+#endif
+constexpr int kSegLong = L3U_SEG_LONG;   // terms per thread above which the scalar form doubles B
 // item (8 x int64): src_off, count, istride, tstride, len, dst_off, accumulate, unused
 // dst[dst_off + t] (+)= sum_{i<count} src[src_off + i*istride + t*tstride], t < len (<= 256)
 // Returns, for thread t < len, the segment's sum for output t (red: 256 doubles of LDS).
@@ -447,22 +451,25 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
   // weight-gradient partials): a thread sums 4 adjacent outputs from float4 loads, so the 864- /
   // 432-long partial lists of the 48^3 / 24^3 layers take a quarter of the dependent load rounds
   // of the scalar form below (same fixed order per output: i = k, k + TP, ...; deterministic)
+  // The item's base address is workgroup-uniform (scalar registers) and every per-lane offset
+  // within it fits 32 bits: one offset VGPR per load in flight instead of a 64-bit address
+  const float* __restrict__ sb = src + it[0];
+  const int cnt = (int)it[1];
   if (kSegVec && !it[7] && it[3] == 1 && (len & 3) == 0 && (it[2] & 3) == 0 && (it[0] & 3) == 0) {
     const int L4 = len >> 2, TP = 256 / L4;
     const int o4 = t % L4, k = t / L4;
-    const long long cnt = it[1], is4 = it[2] >> 2;
+    const int is4 = (int)(it[2] >> 2);
     double s[4] = {0.0, 0.0, 0.0, 0.0};
     if (k < TP) {
-      const f4* sf = reinterpret_cast<const f4*>(src + it[0]) + o4;
-      long long i = k;
+      const f4* __restrict__ sf = reinterpret_cast<const f4*>(sb);
       constexpr int B = kSegBatch;
       // every batch's loads in flight at once, the tail too: clamped (always valid) addresses and
       // unconditional loads, the out-of-range terms dropped by a select AFTER the load (a
       // predicated load made the compiler branch around each load with a vmcnt(0) inside)
-      for (; i < cnt; i += B * TP) {
+      for (int i = k; i < cnt; i += B * TP) {
         f4 v[B];
 #pragma unroll
-        for (int u = 0; u < B; ++u) v[u] = sf[min(i + u * TP, cnt - 1) * is4];
+        for (int u = 0; u < B; ++u) v[u] = sf[o4 + min(i + u * TP, cnt - 1) * is4];
 #pragma unroll
         for (int u = 0; u < B; ++u) {
           const bool ok = i + u * TP < cnt;
@@ -481,33 +488,38 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
   }
   // TP threads per output: thread (k, o) sums terms i = k, k+TP, k+2TP, ... of output o
   // (consecutive threads on consecutive outputs: coalesced), then the TP partial sums are added
-  // in k order.  TP depends only on len, so the summation order is fixed: deterministic.
+  // in k order.  TP depends only on len, so the summation order is fixed: deterministic.  Lists
+  // longer than kSegLong terms per thread (the one-channel 48^3 depthwise partials: 107 per
+  // thread) keep twice the loads in flight (half the dependent rounds; same order of the adds)
   const int TP = 256 / len;
   const int o = t % len, k = t / len;
-  const long long cnt = it[1], is = it[2];
+  const int is = (int)it[2], base = o * (int)it[3];
   double s = 0.0;
+  auto sum = [&](auto BB) {
+    constexpr int B = decltype(BB)::value;   // loads in flight per thread
+    for (int i = k; i < cnt; i += B * TP) {
+      float v[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) v[u] = sb[base + min(i + u * TP, cnt - 1) * is];
+#pragma unroll
+      for (int u = 0; u < B; ++u) s += i + u * TP < cnt ? (double)v[u] : 0.0;
+    }
+  };
   if (k < TP) {
-    const long long base = it[0] + o * it[3];
-    long long i = k;
-    constexpr int B = kSegBatch;   // loads in flight per thread
-    if (it[7]) {
-      const double* sd = reinterpret_cast<const double*>(src) + base;
-      for (; i < cnt; i += B * TP) {   // clamped unconditional loads, select after (no serial tail)
+    if (it[7]) {   // fp64 partials (src_off and strides count doubles; the lists are short)
+      constexpr int B = kSegBatch;
+      const double* __restrict__ sd = reinterpret_cast<const double*>(src) + it[0];
+      for (int i = k; i < cnt; i += B * TP) {
         double v[B];
 #pragma unroll
-        for (int u = 0; u < B; ++u) v[u] = sd[min(i + u * TP, cnt - 1) * is];
+        for (int u = 0; u < B; ++u) v[u] = sd[base + min(i + u * TP, cnt - 1) * is];
 #pragma unroll
         for (int u = 0; u < B; ++u) s += i + u * TP < cnt ? v[u] : 0.0;
       }
+    } else if (cnt > kSegLong * TP) {
+      sum(std::integral_constant<int, 2 * kSegBatch>{});
     } else {
-      const float* sf = src + base;
-      for (; i < cnt; i += B * TP) {
-        float v[B];
-#pragma unroll
-        for (int u = 0; u < B; ++u) v[u] = sf[min(i + u * TP, cnt - 1) * is];
-#pragma unroll
-        for (int u = 0; u < B; ++u) s += i + u * TP < cnt ? (double)v[u] : 0.0;
-      }
+      sum(std::integral_constant<int, kSegBatch>{});
     }
   }
   red[t] = s;
@@ -518,7 +530,7 @@ __device__ __forceinline__ double segment_sum(const float* __restrict__ src,
   return r;
 }
 
-__global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __restrict__ src,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void reduce_segments_kernel(const float* __restrict__ src,
                                                               const long long* __restrict__ items,
                                                               float* __restrict__ dst) {
   L3U_STAMP_SCOPE(410);
@@ -536,7 +548,7 @@ __global__ __launch_bounds__(256) void reduce_segments_kernel(const float* __res
 // reduced gradient goes straight into the AdamW update of its parameters (the gradient is still
 // stored).  The step counter(s) advance as in adamw_tick_kernel (ticket order).  The parameter /
 // moment loads are issued before the reduction so their round trip overlaps it.
-__global__ __launch_bounds__(256) void reduce_segments_adamw_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void reduce_segments_adamw_kernel(
     const float* __restrict__ src, const long long* __restrict__ items, float* __restrict__ g,
     float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
     const float* __restrict__ lr, float beta1, float beta2, float eps, float wd, int* step,

@@ -688,13 +688,13 @@ struct TailSecond {
 };
 
 #ifndef L3U_PWBF_WAVES1
-#define L3U_PWBF_WAVES1 0
+#define L3U_PWBF_WAVES1 5
 #endif
 // minimum waves per SIMD asked of the 16-row forms with up to 32 columns (0: the compiler's
 // choice, 4 for the block-tail forms at 106-108 VGPRs)
 constexpr int kPwbfWaves1 = L3U_PWBF_WAVES1;
 #ifndef L3U_PWBF_PB
-#define L3U_PWBF_PB 8
+#define L3U_PWBF_PB 4
 #endif
 constexpr int kPwbfPB = L3U_PWBF_PB;
 template <typename T, int NJ, int NK, int PRO, bool R1 = false, bool R1B = false>

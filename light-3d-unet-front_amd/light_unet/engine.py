@@ -65,6 +65,20 @@ _FRONT_R1 = os.environ.get("L3U_FRONT_R1", "1") != "0"
 _FUSE_ADAMW = os.environ.get("L3U_FUSE_ADAMW", "1") != "0"
 
 
+# reduction items launched longest first (their workgroups start before the short items fill
+# the chip, instead of starting last); L3U_SEG_SORT=0 keeps the recording order
+_SEG_SORT = os.environ.get("L3U_SEG_SORT", "1") != "0"
+
+
+def _seg_rounds(it):
+    """Dependent load rounds of one reduction item's threads (misc.hip segment_sum: float4 rows
+    when the item allows, 256 // outputs threads per output, 8 loads in flight per thread)."""
+    src, cnt, ist, tst, ln, _, _, f64 = it
+    vec = not f64 and tst == 1 and ln % 4 == 0 and ist % 4 == 0 and src % 4 == 0
+    tp = 256 // (ln // 4) if vec else 256 // ln
+    return -(-(-(-cnt // tp)) // 8)
+
+
 def _items_cover_once(items, numel):
     """True when every one of numel gradient elements is the output of exactly one
     non-accumulating reduction item (the condition of l3u_reduce_segments_adamw)."""
@@ -691,7 +705,11 @@ class UNetEngine:
                 dev = sv["p"].device
                 self._arenas[key] = torch.empty(max(self.bwd_arena.top, 64), dtype=torch.float32,
                                                 device=dev)
-                self._items[key] = torch.tensor(self._items_rec, dtype=torch.int64, device=dev)
+                # items are independent (each output is written by one item), so their order
+                # changes no result
+                rec = sorted(self._items_rec, key=lambda it: -_seg_rounds(it)) if _SEG_SORT \
+                    else self._items_rec
+                self._items[key] = torch.tensor(rec, dtype=torch.int64, device=dev)
                 self._cover_once[key] = _items_cover_once(self._items_rec, gflat.numel())
             self.bwd_arena.reset(self._arenas[key])
             self._items_rec = []

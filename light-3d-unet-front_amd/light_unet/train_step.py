@@ -159,18 +159,22 @@ class TrainStep:
                 t.copy_(c)
         torch.cuda.synchronize()
         pool = torch.cuda.graph_pool_handle()
+        # thread-local capture: with a process group, the RCCL watchdog thread keeps querying
+        # its work events while this thread captures, which a global-mode capture turns into
+        # "operation not permitted when stream is capturing" in that thread (an abort)
+        mode = "thread_local"
         if not self.exchange or self.capture_collectives:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
                 self(self.xs, self.ts)
             self._graphs = [g]
         else:
             g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1, pool=pool):
+            with torch.cuda.graph(g1, pool=pool, capture_error_mode=mode):
                 self._cap_p, self._cap_sv, self._cap_sums = self._fwd(self.xs, self.ts)
-            with torch.cuda.graph(g2, pool=pool):
+            with torch.cuda.graph(g2, pool=pool, capture_error_mode=mode):
                 self._bwd(self._cap_p, self._cap_sv, self.ts, self._cap_sums)
-            with torch.cuda.graph(g3, pool=pool):
+            with torch.cuda.graph(g3, pool=pool, capture_error_mode=mode):
                 self.opt.step()
             self._graphs = [g1, g2, g3]
         torch.cuda.synchronize()

@@ -78,3 +78,18 @@ def test_paired_call_bytes_are_the_two_calls():
             p, J * S, p, p, Kb * S, p, p, Kb * S, 0, p, Kb, 2, N, J, S, p)
     tp = bench.call_bytes("l3u_pw_bwd_tail_pair", args)
     assert tp[0] == "gemm" and tp[2] == tail(p, 1, Ka, 0) + tail(p, 2, Kb, 0)
+
+
+def test_reduce_call_bytes(monkeypatch):
+    """CPU: the byte model of the weight-gradient reduction launch reads every partial once (fp32,
+    fp64 for the InstanceNorm affine partials) and the item table, and per output writes the
+    gradient and (the fused AdamW form) reads and writes the parameter and both moments."""
+    sys.path.insert(0, ROOT)
+    import bench
+    items = [[0, 1728, 512, 1, 32, 0, 0, 0], [64, 4, 3, 12, 16, 32, 0, 1]]
+    monkeypatch.setattr(bench, "SEG_ITEMS", {99: items})
+    f, label, b = bench.call_bytes("l3u_reduce_segments_adamw", (1, 99, 2))
+    assert f == "reduce" and "2 items" in label
+    assert b == 1728 * 32 * 4 + 4 * 16 * 8 + 2 * 64 + 28 * 48
+    assert bench.call_bytes("l3u_reduce_segments", (1, 99, 2))[2] == 1728 * 32 * 4 + 4 * 16 * 8 + 2 * 64 + 4 * 48
+    assert bench.call_bytes("l3u_reduce_segments", (1, 98, 2)) is None   # items not recorded

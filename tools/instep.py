@@ -1,4 +1,4 @@
-"""In-step rooflines of the depthwise and GEMM families: the rocprofv3 kernel trace of the
+"""In-step rooflines of the depthwise, GEMM and gradient-reduction families: the rocprofv3 kernel trace of the
 graph-replayed training step (tools/profile.sh) aligned launch by launch with the C-ABI calls
 of the same step (bench.py --dump-calls: name, family, label, algorithmic bytes).
 
@@ -95,7 +95,7 @@ def main():
     for j, kname, us in align(ks, calls):
         k0, u0 = per_call.get(j, ("", 0.0))
         per_call[j] = (k0 + (" + " if k0 else "") + kname, u0 + us)
-    fam = {"dw": [], "gemm": []}
+    fam = {"dw": [], "gemm": [], "reduce": []}
     for j, c in enumerate(calls):
         if c["family"] is None:
             continue
@@ -112,6 +112,8 @@ def main():
     for f, rows in fam.items():
         tb = sum(r["bytes"] for r in rows)
         tt = sum(r["us"] for r in rows) * 1e-6
+        if not rows:
+            continue
         rec[f] = {"launches": len(rows), "bytes": tb, "us": round(tt * 1e6, 1),
                   "achieved": round(tb / tt / 1e9, 1), "frac": round(tb / tt / 1e9 / PEAK, 4),
                   "calls": rows}
