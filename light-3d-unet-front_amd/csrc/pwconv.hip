@@ -697,8 +697,19 @@ constexpr int kPwbfWaves1 = L3U_PWBF_WAVES1;
 #define L3U_PWBF_PB 4
 #endif
 constexpr int kPwbfPB = L3U_PWBF_PB;
+#ifndef L3U_PWBF_WAVES2
+#define L3U_PWBF_WAVES2 4
+#endif
+// ... and of the 32-row forms without a prologue and with up to 32 columns (184 -> 88 / 112
+// VGPRs, no spill; the prologue forms spill 11-38 VGPRs at 4 waves)
+constexpr int kPwbfWaves2 = L3U_PWBF_WAVES2;
+template <int NJ, int NK, int PRO>
+constexpr int pwbf_waves() {
+  return NJ == 1 ? (NK <= 2 && kPwbfWaves1 > 0 ? kPwbfWaves1 : 1)
+                 : (PRO == 0 && NK <= 2 && kPwbfWaves2 > 0 ? kPwbfWaves2 : 1);
+}
 template <typename T, int NJ, int NK, int PRO, bool R1 = false, bool R1B = false>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NJ == 1 && NK <= 2 && kPwbfWaves1 > 0 ? kPwbfWaves1 : 1))) void pw_bwd_fused_kernel(
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(pwbf_waves<NJ, NK, PRO>()))) void pw_bwd_fused_kernel(
     const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
     const T* __restrict__ x, long long xns, const float* __restrict__ w,

@@ -31,8 +31,11 @@ _PAIR_PW = os.environ.get("L3U_PAIR_PW", "1") != "0"
 # block-tail backward inside the pointwise backwards (l3u_pw_bwd_tail); L3U_TAIL_FUSE=0 disables
 _TAIL_FUSE = os.environ.get("L3U_TAIL_FUSE", "1") != "0"
 # (an optional fourth value applies to lists longer than 1024 -- the 48^3 pointwise partials,
-# 1728 per layer: round 5 measured 8 outputs per item there +2.6 us on the reduction launch)
+# 1728 per layer: round 5 measured 8 outputs per item there +2.6 us on the reduction launch);
+# lists of <= 32 partials take 256 outputs per item (fewer workgroups: -3 us, r5p); L3U_SEG_SHORT
+# = <max count>:<outputs> overrides
 _SEG_CAPS = tuple(int(v) for v in os.environ.get("L3U_SEG_CAPS", "128,64,32").split(","))
+_SEG_SHORT = tuple(int(v) for v in os.environ.get("L3U_SEG_SHORT", "32:256").split(":"))
 # conv2 (depthwise + pointwise, InstanceNorm1 on load) as one l3u_dwpw_fwd launch for volumes of
 # at least this many voxels (the 48^3 level; at 24^3 its 1024-thread slabs are too few to fill
 # the chip, tools/dwpw_bench.py); L3U_DWPW=0 disables
@@ -307,6 +310,8 @@ class UNetEngine:
         # every thread's serial share stays short (256 / cap threads share each output's terms)
         cap = _SEG_CAPS[0] if count <= 128 else (_SEG_CAPS[1] if count <= 384 else (
             _SEG_CAPS[2] if count <= 1024 or len(_SEG_CAPS) < 4 else _SEG_CAPS[3]))
+        if count <= _SEG_SHORT[0]:
+            cap = _SEG_SHORT[1]
         t0 = 0
         while t0 < length:
             ln = min(cap, length - t0)
