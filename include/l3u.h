@@ -41,7 +41,7 @@ typedef unsigned short l3u_bf16;   /* bfloat16 bit pattern (torch.bfloat16 stora
 /* ABI version of this header (L3U_ABI_VERSION); the ctypes binding refuses a library that reports
  * another.  3: l3u_norm_src.rank1, L3U_ADAMW_TICKET_INTS tickets, the l3u_sblock_* entry points
  * removed (round 3); the round-4 entry points. */
-#define L3U_ABI_VERSION 3
+#define L3U_ABI_VERSION 4
 int l3u_abi_version(void);
 
 /* Where an InstanceNorm record comes from when a consumer kernel finalizes it itself (no separate
@@ -271,6 +271,17 @@ int l3u_norm_act_bwd(const float* dout, long long dout_nstride, const float* out
                      const float* rec2, const float* r, long long r_nstride, const float* rec_r,
                      double* part, float* dy2, long long dy2_nstride, float* dr,
                      long long dr_nstride, int N, int C, int S, hipStream_t stream);
+/* the same with dout = dskip + the next level's MaxPool3d backward of dpool (l3u_maxpool2_bwd
+ * folded in: no level-output gradient tensor, one launch fewer; unet3d.py:104,109), for planes of
+ * <= 2048 voxels with even D / H and W % 4 == 0; bit-identical to l3u_maxpool2_bwd followed by
+ * l3u_norm_act_bwd                                                                              */
+int l3u_norm_act_bwd_up(const float* dskip, long long dskip_nstride, const float* dpool,
+                        long long dpool_nstride, const unsigned char* idx, const float* out,
+                        long long out_nstride, const float* y2, long long y2_nstride,
+                        const float* rec2, const float* r, long long r_nstride,
+                        const float* rec_r, double* part, float* dy2, long long dy2_nstride,
+                        float* dr, long long dr_nstride, int N, int C, int D, int H, int W,
+                        hipStream_t stream);
 /* inner InstanceNorm backward: dy = rstd*gamma*(dpre - mean(dpre) - xhat*mean(dpre*xhat))     */
 int l3u_in_bwd_apply(const float* dpre, long long dpre_nstride, const float* y, long long y_nstride,
                      const float* rec, const double* in_part, int npart, float* dy,
@@ -615,6 +626,13 @@ int l3u_norm_act_bwd_bf16(const float* dout, long long dout_nstride, const l3u_b
                           const float* rec2, const l3u_bf16* r, long long r_nstride,
                           const float* rec_r, double* part, float* dy2, long long dy2_nstride,
                           float* dr, long long dr_nstride, int N, int C, int S, hipStream_t stream);
+int l3u_norm_act_bwd_up_bf16(const float* dskip, long long dskip_nstride, const float* dpool,
+                             long long dpool_nstride, const unsigned char* idx,
+                             const l3u_bf16* out, long long out_nstride, const l3u_bf16* y2,
+                             long long y2_nstride, const float* rec2, const l3u_bf16* r,
+                             long long r_nstride, const float* rec_r, double* part, float* dy2,
+                             long long dy2_nstride, float* dr, long long dr_nstride, int N, int C,
+                             int D, int H, int W, hipStream_t stream);
 int l3u_in_bwd_apply_bf16(const float* dpre, long long dpre_nstride, const l3u_bf16* y,
                           long long y_nstride, const float* rec, const double* in_part, int npart,
                           float* dy, long long dy_nstride, int N, int C, int S, hipStream_t stream);

@@ -318,7 +318,8 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
     const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
     const T* __restrict__ r, long long rns, const float* __restrict__ recr,
     double* __restrict__ part, float* __restrict__ dy2, long long dy2ns, float* __restrict__ dr,
-    long long drns, int N, int C, int S) {
+    long long drns, int N, int C, int S, const float* __restrict__ dpool = nullptr,
+    long long dpns = 0, const unsigned char* __restrict__ pidx = nullptr, int H = 0, int W = 0) {
   L3U_STAMP_SCOPE(306);
   __shared__ double red[4];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
@@ -345,6 +346,11 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
       dv[k] = ov[k] = yv[k] = rv[k] = f4{0.f, 0.f, 0.f, 0.f};
       if (i < S) {
         dv[k] = ldv4(dp + i);
+        if (dpool) {   // + the next level's MaxPool3d backward (l3u_maxpool2_bwd folded in)
+          const int HW = H * W, z = fdiv(i, HW, 1.f / HW), rm = i - z * HW, y = fdiv(rm, W, 1.f / W);
+          dv[k] = unpool_add(dv[k], dpool + (long long)n * dpns + (long long)c * (S / 8),
+                             pidx + (long long)nc * (S / 8), z, y, rm - y * W, H, W);
+        }
         ov[k] = ldv4(op + i);
         yv[k] = ldv4(yp + i);
         if (recr) rv[k] = ldv4(rp + i);
@@ -612,14 +618,20 @@ int norm_act_bwd_impl(const float* dout, long long dout_nstride, const T* out,
                       long long out_nstride, const T* y2, long long y2_nstride,
                       const float* rec2, const T* r, long long r_nstride, const float* rec_r,
                       double* part, float* dy2, long long dy2_nstride, float* dr,
-                      long long dr_nstride, int N, int C, int S, hipStream_t stream) {
+                      long long dr_nstride, int N, int C, int S, hipStream_t stream,
+                      const float* dpool = nullptr, long long dpns = 0,
+                      const unsigned char* pidx = nullptr, int D = 0, int H = 0, int W = 0) {
   L3U_REQUIRE(N > 0 && C > 0 && S > 0 && elem_blocks(S) == 1);
   L3U_REQUIRE(r_nstride >= 0);   // no rank-1 residual on the split tail
   const bool vec = S % 4 == 0 && dout_nstride % 4 == 0 && out_nstride % 4 == 0 &&
                    y2_nstride % 4 == 0 && r_nstride % 4 == 0 && dy2_nstride % 4 == 0 &&
                    dr_nstride % 4 == 0;
+  // the folded MaxPool3d backward: the register-held form (S <= 2048), even D / H, W % 4 == 0
+  L3U_REQUIRE(dpool == nullptr || (vec && pidx && S <= 2048 && D * H * W == S && D % 2 == 0 &&
+                                   H % 2 == 0 && W % 4 == 0 && dpns % 2 == 0 &&
+                                   ((uintptr_t)dpool & 7) == 0));
   dim3 grid(1, N * C);
-  if (vec) hipLaunchKernelGGL((norm_act_bwd_one_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
+  if (vec) hipLaunchKernelGGL((norm_act_bwd_one_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S, dpool, dpns, pidx, H, W);
   else hipLaunchKernelGGL((norm_act_bwd_one_kernel<T, false>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
   L3U_CHECK_LAUNCH();
 }
@@ -687,6 +699,17 @@ L3U_TWIN(l3u_norm_act_bwd_apply, P_NBA, norm_act_bwd_apply_impl(dout, dout_nstri
 L3U_TWIN(l3u_norm_act_bwd, P_NB1, norm_act_bwd_impl(dout, dout_nstride, bp(out), out_nstride,
          bp(y2), y2_nstride, rec2, bp(r), r_nstride, rec_r, part, dy2, dy2_nstride, dr,
          dr_nstride, N, C, S, stream))
+// the same with the block-output gradient = skip gradient + the next level's MaxPool3d backward
+// (l3u_maxpool2_bwd folded in, the one-launch planes of l3u_norm_act_bwd)
+#define P_NB1U(TT) (const float* dskip, long long dskip_nstride, const float* dpool,                 \
+    long long dpool_nstride, const unsigned char* idx, const TT* out, long long out_nstride,         \
+    const TT* y2, long long y2_nstride, const float* rec2, const TT* r, long long r_nstride,        \
+    const float* rec_r, double* part, float* dy2, long long dy2_nstride, float* dr,                 \
+    long long dr_nstride, int N, int C, int D, int H, int W, hipStream_t stream)
+L3U_TWIN(l3u_norm_act_bwd_up, P_NB1U, dpool == nullptr ? (int)hipErrorInvalidValue :
+         norm_act_bwd_impl(dskip, dskip_nstride, bp(out), out_nstride, bp(y2), y2_nstride, rec2,
+         bp(r), r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, D * H * W, stream,
+         dpool, dpool_nstride, idx, D, H, W))
 #define P_IBA(TT) (const float* dpre, long long dpre_nstride, const TT* y, long long y_nstride,    \
     const float* rec, const double* in_part, int npart, float* dy, long long dy_nstride, int N,      \
     int C,                                                                                           \

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get(
     "L3U_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libl3u_hip.so"))
 
 # include/l3u.h L3U_ABI_VERSION: the library must report exactly this
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -72,6 +72,7 @@ _SIGS = {
     "l3u_front_fwd": [P, L, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "l3u_pw_bwd_tail": [P, L, P, L, P, L, P, P, I, I, P, L, P, P, L, I, P, I, I, I, I, P],
     "l3u_norm_act_bwd": [P, L, P, L, P, L, P, P, L, P, P, P, L, P, L, I, I, I, P],
+    "l3u_norm_act_bwd_up": [P, L, P, L, P, P, L, P, L, P, P, L, P, P, P, L, P, L, I, I, I, I, I, P],
     "l3u_gconv3_nblocks": [I],
     "l3u_gconv3_wgrad_nparts": [I, I],
     "l3u_gconv3_fwd": [P, L, P, P, P, L, P, I, I, I, I, I, I, I, P],
@@ -110,7 +111,7 @@ BF16_TWINS = ("l3u_dw3_fwd", "l3u_dw3_bwd", "l3u_pw_fwd", "l3u_pw_fwd2", "l3u_pw
               "l3u_outconv_bwd_ftl", "l3u_box_copy",
               "l3u_front_fwd", "l3u_dwpw_fwd", "l3u_outconv_bwd_dz", "l3u_outconv_bwd_ftl_dz",
               "l3u_norm_act_bwd_reduce_r1", "l3u_pw_bwd_tail_r1", "l3u_norm_act_bwd_reduce_up",
-              "l3u_pw_bwd_tail_up")
+              "l3u_pw_bwd_tail_up", "l3u_norm_act_bwd_up")
 for _n in BF16_TWINS:
     _SIGS[_n + "_bf16"] = _SIGS[_n]
 # query helpers that return a value instead of an error code

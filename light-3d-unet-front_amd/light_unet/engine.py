@@ -833,7 +833,8 @@ class UNetEngine:
             cons = ("init_conv.", "down1.res_block.", "down2.res_block.")[lvl]
             csv = sv["blk"][cons]
             if (_POOLFOLD and self.kinds[cons][0][0] == "ds" and d % 2 == 0 and hh % 2 == 0
-                    and w % 4 == 0 and self._tail_fusable(csv, csv["x"].C, cprev, S[lvl])):
+                    and w % 4 == 0 and (self._tail_fusable(csv, csv["x"].C, cprev, S[lvl])
+                                        or self._tail_one_up(csv, S[lvl]))):
                 # the consuming block tail forms it on load (l3u_*_up): no tensor, no launch
                 dout = V(dcat, cprev * S[lvl], 2 * cprev * S[lvl], cprev, pool=(dpool, idx, dims[lvl]))
                 continue
@@ -857,6 +858,14 @@ class UNetEngine:
         return (_TAIL_FUSE and sv["shortcut"] and nat.query("l3u_norm_act_nblocks", S) > 1
                 and cout <= 32 and nat.query("l3u_pw_bwd_supported", cout, cout, S)
                 and nat.query("l3u_pw_bwd_supported", cout, cin, S))
+
+    @staticmethod
+    def _tail_one_up(sv, S):
+        """An unfused block tail whose planes take the one-launch l3u_norm_act_bwd can form its
+        output gradient on load as well (l3u_norm_act_bwd_up, the register-held planes <= 2048
+        voxels: the 12^3 level), without a rank-1 residual."""
+        return (nat.query("l3u_norm_act_nblocks", S) == 1 and S <= 2048
+                and (sv["r"] if sv["shortcut"] else sv["x"]).scale is None)
 
     def _tail_bwd(self, pre, sv, dout, dxv, N, cout, S, st, dev, fused=False):
         """Backward of the block tail out = lrelu(IN2(y2) + residual): d y2 and d residual (the
@@ -890,8 +899,8 @@ class UNetEngine:
                 self._call("l3u_norm_act_bwd_reduce", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(),
                            cout * S, rec2, rv.p, rv.sns, rec_r, A.ptr(pn), N, cout, S, st)
             return pn, nb
-        assert dout.scale is None and dout.pool is None, "a formed-on-load output gradient " \
-            "needs the fused block tail"
+        assert dout.scale is None and (dout.pool is None or nb == 1), "a formed-on-load output " \
+            "gradient needs the fused block tail or a one-launch plane"
         assert rv.scale is None, "a rank-1 residual needs the fused block tail"
         dy2 = self._empty(N, cout, S, device=dev)
         if shortcut:
@@ -901,6 +910,13 @@ class UNetEngine:
             self._seg(pnd + 0, N * nb, 3, N * nb * 3, cout, pre + "shortcut.1.bias", f64=1)
         else:
             drv = dxv   # identity shortcut: d(input) starts as g
+        if nb == 1 and dout.pool is not None:   # + the folded MaxPool3d backward
+            dpool, idx, (d, h, w) = dout.pool
+            self._call("l3u_norm_act_bwd_up", dout.p, dout.ns, dpool.data_ptr(), cout * (S // 8),
+                       idx.data_ptr(), out.p, out.ns, y2.data_ptr(), cout * S, rec2, rv.p, rv.ns,
+                       rec_r if shortcut else None, A.ptr(pn), dy2.data_ptr(), cout * S, drv.p,
+                       drv.ns, N, cout, d, h, w, st)
+            return dy2, drv
         if nb == 1:   # one workgroup per plane: reduce and apply in one launch
             self._call("l3u_norm_act_bwd", dout.p, dout.ns, out.p, out.ns, y2.data_ptr(), cout * S,
                        rec2, rv.p, rv.ns, rec_r if shortcut else None, A.ptr(pn), dy2.data_ptr(),

@@ -77,7 +77,7 @@ def test_bf16_twins_mirror_fp32_entry_points():
 
 def test_host_queries_without_gpu():
     from light_unet import _native
-    assert _native.query("l3u_abi_version") == _native.ABI_VERSION == 3
+    assert _native.query("l3u_abi_version") == _native.ABI_VERSION == 4
     assert _native.query("l3u_dw3_nchunk", 4, 32, 48, 48, 48) == 30   # 3 z-slabs x 10 y-strips
     assert _native.query("l3u_dw3_nchunk", 4, 16, 48, 48, 48) == 40   # 12-plane slabs: 4 x 10
     assert _native.query("l3u_pw_bwd_supported", 16, 32, 48 ** 3) == 1

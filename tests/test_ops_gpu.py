@@ -891,6 +891,46 @@ def test_norm_act_bwd_one_launch_equals_pair(cuda, shape, shortcut):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("dims", [(4, 64, 12, 12, 12), (2, 8, 8, 8, 8), (1, 4, 4, 6, 8)])
+@pytest.mark.parametrize("shortcut", [False, True])
+def test_norm_act_bwd_up_equals_maxpool_bwd_then_one_launch(cuda, dims, shortcut):
+    """l3u_norm_act_bwd_up (dout = dskip + the next level's MaxPool3d backward, formed on load) ==
+    l3u_maxpool2_bwd (with dskip as its addend) followed by l3u_norm_act_bwd, bitwise."""
+    N, C, D, H, W = dims
+    S = D * H * W
+    gen = torch.Generator().manual_seed(43)
+    t = lambda *s: torch.randn(*s, generator=gen).to(cuda)  # noqa: E731
+    x = t(N, C, D, H, W)
+    pooled = torch.empty(N, C, S // 8, device=cuda)
+    idx = torch.empty(N, C, S // 8, dtype=torch.uint8, device=cuda)
+    nat().call("l3u_maxpool2_fwd", x.data_ptr(), C * S, pooled.data_ptr(), C * S // 8, idx.data_ptr(),
+               N, C, D, H, W, st())
+    dpool, dskip, out, y2, r = t(N, C, S // 8), t(N, C, S), t(N, C, S), t(N, C, S), t(N, C, S)
+    rec2 = make_rec(N, C, gen).float().to(cuda)
+    recr = make_rec(N, C, gen).float().to(cuda) if shortcut else None
+    rp = recr.data_ptr() if shortcut else None
+
+    def run(up):
+        part = torch.full((C * N * 3,), float("nan"), dtype=torch.float64, device=cuda)
+        dy2 = torch.full((N, C, S), float("nan"), device=cuda)
+        dr = torch.full((N, C, S), float("nan"), device=cuda)
+        tail = (out.data_ptr(), C * S, y2.data_ptr(), C * S, rec2.data_ptr(), r.data_ptr(), C * S, rp,
+                part.data_ptr(), dy2.data_ptr(), C * S, dr.data_ptr(), C * S, N, C)
+        if up:
+            nat().call("l3u_norm_act_bwd_up", dskip.data_ptr(), C * S, dpool.data_ptr(), C * S // 8,
+                       idx.data_ptr(), *tail, D, H, W, st())
+        else:
+            dlev = torch.full((N, C, S), float("nan"), device=cuda)
+            nat().call("l3u_maxpool2_bwd", dpool.data_ptr(), C * S // 8, idx.data_ptr(), dskip.data_ptr(),
+                       C * S, dlev.data_ptr(), C * S, N, C, D, H, W, st())
+            nat().call("l3u_norm_act_bwd", dlev.data_ptr(), C * S, *tail, S, st())
+        torch.cuda.synchronize()
+        return part, dy2, dr
+
+    for a, b in zip(run(True), run(False)):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("shape", [(4, 16, 32, 48 ** 3), (4, 32, 16, 24 ** 3), (2, 16, 8, 1000),
                                    (1, 8, 3, 7 * 9 * 12)])
 def test_pw_bwd_tail_equals_apply_then_pw_bwd(cuda, shape):
