@@ -703,9 +703,16 @@ constexpr int kPwbfPB = L3U_PWBF_PB;
 // ... and of the 32-row forms without a prologue and with up to 32 columns (184 -> 88 / 112
 // VGPRs, no spill; the prologue forms spill 11-38 VGPRs at 4 waves)
 constexpr int kPwbfWaves2 = L3U_PWBF_WAVES2;
+#ifndef L3U_PWBF_WAVES1K1
+#define L3U_PWBF_WAVES1K1 6
+#endif
+// ... and of the 16-row, 16-column forms (80 VGPRs at 6 waves without a spill; the 32-column ones
+// spill 11-20 there)
+constexpr int kPwbfWaves1k1 = L3U_PWBF_WAVES1K1;
 template <int NJ, int NK, int PRO>
 constexpr int pwbf_waves() {
-  return NJ == 1 ? (NK <= 2 && kPwbfWaves1 > 0 ? kPwbfWaves1 : 1)
+  return NJ == 1 ? (NK == 1 && kPwbfWaves1k1 > 0 ? kPwbfWaves1k1
+                                                 : (NK <= 2 && kPwbfWaves1 > 0 ? kPwbfWaves1 : 1))
                  : (PRO == 0 && NK <= 2 && kPwbfWaves2 > 0 ? kPwbfWaves2 : 1);
 }
 template <typename T, int NJ, int NK, int PRO, bool R1 = false, bool R1B = false>
@@ -823,16 +830,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(pwbf_waves<
       // memory round trip per batch instead of one per partial (same order of the adds)
       const int st = PRO == 2 ? 3 : 2, o1 = PRO == 2 ? sel : 1;
       const double* pp = in_part + ((long long)j * N + n) * npart * st;
-      for (int i0 = sub; i0 < npart; i0 += kPwbfPB * PS) {
-        double a0[kPwbfPB], a1[kPwbfPB];
+      // (batches of 2 for the 16-column forms at 6 waves per SIMD: their 80-VGPR budget)
+      constexpr int PB = NJ == 1 && NK == 1 && kPwbfWaves1k1 >= 6 ? 2 : kPwbfPB;
+      for (int i0 = sub; i0 < npart; i0 += PB * PS) {
+        double a0[PB], a1[PB];
 #pragma unroll
-        for (int u = 0; u < kPwbfPB; ++u) {
+        for (int u = 0; u < PB; ++u) {
           const int i = min(i0 + u * PS, npart - 1);
           a0[u] = pp[i * st];
           a1[u] = pp[i * st + o1];
         }
 #pragma unroll
-        for (int u = 0; u < kPwbfPB; ++u) {
+        for (int u = 0; u < PB; ++u) {
           const bool ok = i0 + u * PS < npart;
           t0 += ok ? a0[u] : 0.0;
           t1 += ok ? a1[u] : 0.0;
