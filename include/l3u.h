@@ -40,8 +40,8 @@ typedef unsigned short l3u_bf16;   /* bfloat16 bit pattern (torch.bfloat16 stora
 
 /* ABI version of this header (L3U_ABI_VERSION); the ctypes binding refuses a library that reports
  * another.  3: l3u_norm_src.rank1, L3U_ADAMW_TICKET_INTS tickets, the l3u_sblock_* entry points
- * removed (round 3); the round-4 entry points. */
-#define L3U_ABI_VERSION 4
+ * removed (round 3); the round-4 entry points.  5: l3u_pw_bwd_chunk (round 6). */
+#define L3U_ABI_VERSION 5
 int l3u_abi_version(void);
 
 /* Where an InstanceNorm record comes from when a consumer kernel finalizes it itself (no separate
@@ -132,6 +132,9 @@ int l3u_dwpw_fwd(const float* x, long long x_nstride, const float* w_dw, const f
                  hipStream_t stream);
 /* weight gradient partials: part[N*nsc][J][K] = sum_s dY[n][j][s] X[n][k][s] per voxel chunk   */
 int l3u_pw_bwd_weight_nparts(int N, int S);
+/* the voxel chunk of those partials (nsc = ceil(S / chunk)); a multiple of 256, at most 512: each
+ * chunk is one workgroup sweep of the kernels that write them (csrc/pwconv.hip pw_chunk_ok)     */
+int l3u_pw_bwd_chunk(int S);
 int l3u_pw_bwd_weight(const float* dy, long long dy_nstride, const float* x, long long x_nstride,
                       float* part, int N, int J, int K, int S, hipStream_t stream);
 
@@ -497,7 +500,9 @@ int l3u_adamw_tick(float* p, const float* g, float* m, float* v, long long numel
 /* ---- deterministic second-stage reduction --------------------------------------------------
  * items[nitems][8] int64 = {src_off, count, istride, tstride, len<=256, dst_off, accumulate, f64}:
  * dst[dst_off+t] (+)= sum_{i<count} src[src_off + i*istride + t*tstride], summed in fp64;
- * f64 != 0: the source is fp64 and offsets/strides count doubles from the same base.         */
+ * f64 != 0: the source is fp64 and offsets/strides count doubles from the same base.
+ * src is 16-byte aligned (checked), and every item's per-lane offsets fit 32 bits:
+ * (count-1)*istride + (len-1)*tstride < 2^31 (the engine checks it when it records an item). */
 int l3u_reduce_segments(const float* src, const long long* items, int nitems, float* dst,
                         hipStream_t stream);
 /* the same reduction fused with the AdamW update (l3u_adamw_tick's arithmetic and step /

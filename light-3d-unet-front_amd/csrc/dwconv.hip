@@ -1732,8 +1732,9 @@ int dw3_bwd_impl(const float* dz, long long dz_nstride, const T* x, long long x_
 extern "C" int l3u_dw3_bwd_rank1(int N, int C, int D, int H, int W) {
   if (!(N > 0 && C > 0 && !use_volume(D, H, W) && use_quads(H, W))) return 0;
   const QGeom g = qgeom(N, C, D, H, W);
-  // the forward's rank-1 form (dw3g_fwd_kernel) needs two DMA slots per plane as well
-  return dw_gl(g, W, 4) && (!kDwfGl || (g.RB + 2) * g.WQ > 64);
+  // the forward's rank-1 form is dw3g_fwd_kernel only (dw3_fwd_impl REQUIREs kDwfGl), with two
+  // DMA slots per plane, so a build without it (L3U_DWF_GL=0) offers no rank-1 shape at all
+  return dw_gl(g, W, 4) && kDwfGl && (g.RB + 2) * g.WQ > 64;
 }
 
 extern "C" int l3u_dw3_nchunk(int N, int C, int D, int H, int W) {

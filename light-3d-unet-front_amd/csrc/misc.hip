@@ -995,7 +995,8 @@ int l3u_adamw_tick(float* p, const float* g, float* m, float* v, long long numel
 
 int l3u_reduce_segments(const float* src, const long long* items, int nitems, float* dst,
                         hipStream_t stream) {
-  L3U_REQUIRE(nitems > 0);
+  // src 16-byte aligned: segment_sum's float4 rows check only the item's own offset (it[0] % 4)
+  L3U_REQUIRE(nitems > 0 && src && ((uintptr_t)src & 15) == 0);
   hipLaunchKernelGGL(reduce_segments_kernel, dim3(nitems), dim3(256), 0, stream, src, items, dst);
   L3U_CHECK_LAUNCH();
 }
@@ -1004,7 +1005,7 @@ int l3u_reduce_segments_adamw(const float* src, const long long* items, int nite
                               float* p, float* m, float* v, const float* lr, float beta1,
                               float beta2, float eps, float weight_decay, int* step,
                               float grad_scale, int* ticket, int* counter2, hipStream_t stream) {
-  L3U_REQUIRE(nitems > 0 && step && ticket);
+  L3U_REQUIRE(nitems > 0 && step && ticket && src && ((uintptr_t)src & 15) == 0);
   hipLaunchKernelGGL(reduce_segments_adamw_kernel, dim3(nitems), dim3(256), 0, stream, src, items,
                      g, p, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale, ticket,
                      counter2);

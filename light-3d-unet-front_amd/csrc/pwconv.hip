@@ -1614,9 +1614,23 @@ __global__ __launch_bounds__(256) void convt_pair_bwd_kernel(
 constexpr int kPwSchMax = 256;   // 4-wave sweeps at >= 64K voxels: config 5 -115 us (the 64^3 J = 32 tails hold 85 KB of LDS as 8-wave sweeps: one workgroup per CU), 48^3 -3 us
 constexpr int kPwNswMax = 1;
 constexpr int kPwSchMid = 256;   // voxel chunk of the mid-size levels (4096 <= S < 65536: 24^3); 512: +10 us/step
-int pw_sch(int S) {
+constexpr int pw_sch(int S) {
   return S >= 65536 ? kPwSchMax : (S >= 4096 ? kPwSchMid : (S >= 1024 ? 512 : 256));
 }
+// The chunk invariant.  A chunk is ONE workgroup sweep of every kernel that writes chunk partials
+// (part[N * nsc][J][K], nsc = ceil(S / SCH)): pw_bwd_fused_kernel runs SCH / 64 waves (1..8),
+// pw_bwd_k1_kernel SCH / 4 threads, which must be whole waves (its xor-tree reduction reads all 64
+// lanes) and at most its 128-thread launch bound (pw_bwd_weight_kernel and the ConvTranspose3d
+// weight kernels bound their loops by the chunk and take any size).  A chunk size breaking this
+// left lanes of the K = 1 kernel's reduction unwritten (round 5: 192-voxel chunks, 48-thread
+// workgroups, gave NaN weight gradients at the 64^3 first block).  Every chunk size pw_sch can
+// return is checked here, l3u_pw_bwd_chunk reports it to the host (tests/test_capi.py), and the
+// launches re-check their own form.
+constexpr bool pw_chunk_ok(int SCH) {
+  return SCH % 256 == 0 && SCH / 64 >= 1 && SCH / 64 <= 8 && SCH / 4 <= 128;
+}
+static_assert(pw_chunk_ok(pw_sch(1)) && pw_chunk_ok(pw_sch(1024)) && pw_chunk_ok(pw_sch(4096)) &&
+              pw_chunk_ok(pw_sch(65536)), "every pointwise-backward chunk size keeps the invariant");
 
 // voxel sub-tiles per wave of pw_fwd_kernel: fewer for narrow outputs so that big volumes
 // still launch enough workgroups (>= 4 per CU at one sample)
@@ -1933,6 +1947,7 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
   // one input channel with the IN prologue (the first block's conv1.pointwise, y materialised or
   // rank-1): the VALU kernel, same chunks and partial layout
   if (K == 1 && y != nullptr && SCH <= 512 && J <= 32) {
+    L3U_REQUIRE(pw_chunk_ok(SCH));   // SCH / 4 threads: whole waves, <= the 128-thread bound
     hipLaunchKernelGGL((pw_bwd_k1_kernel<T>), dim3(N * nsc), dim3(SCH / 4), 0, stream, dy, dy_nstride,
                        y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride,
                        accumulate, part, N, J, S, SCH, nsc);
@@ -2122,6 +2137,8 @@ int l3u_pw_bwd_weight_nparts(int N, int S) {
   const int SCH = pw_sch(S);
   return N * ((S + SCH - 1) / SCH);
 }
+
+int l3u_pw_bwd_chunk(int S) { return S > 0 ? pw_sch(S) : 0; }
 
 int l3u_pw_bwd_supported(int J, int K, int S) {
   if (!(J > 0 && K > 0 && S > 0 && S % 4 == 0)) return 0;

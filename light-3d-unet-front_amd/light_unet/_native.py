@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get(
     "L3U_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libl3u_hip.so"))
 
 # include/l3u.h L3U_ABI_VERSION: the library must report exactly this
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -32,6 +32,7 @@ _SIGS = {
     "l3u_pw_stat_nsb": [I, I, I],
     "l3u_pw_fwd": [P, L, P, I, P, P, L, I, P, I, I, I, I, P],
     "l3u_pw_bwd_weight_nparts": [I, I],
+    "l3u_pw_bwd_chunk": [I],
     "l3u_pw_bwd_weight": [P, L, P, L, P, I, I, I, I, P],
     "l3u_pw_bwd_supported": [I, I, I],
     "l3u_pw_bwd_nparts": [I, I, I, I],
@@ -120,7 +121,7 @@ _QUERIES = {"l3u_abi_version", "l3u_dw3_nchunk", "l3u_pw_stat_nsb", "l3u_pw_bwd_
             "l3u_norm_act_nblocks", "l3u_outconv_nblocks", "l3u_ftl_nblocks",
             "l3u_gconv3_nblocks", "l3u_gconv3_wgrad_nparts", "l3u_front_nblocks",
             "l3u_ccl_nchunks", "l3u_dwpw_supported", "l3u_dwpw_stat_nsb",
-            "l3u_dw3_bwd_rank1", "l3u_pw_bwd2_supported"}
+            "l3u_dw3_bwd_rank1", "l3u_pw_bwd2_supported", "l3u_pw_bwd_chunk"}
 
 _lib = None
 

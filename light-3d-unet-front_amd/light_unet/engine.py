@@ -315,6 +315,10 @@ class UNetEngine:
         t0 = 0
         while t0 < length:
             ln = min(cap, length - t0)
+            # misc.hip segment_sum: per-lane offsets from the item's base are 32-bit
+            if (count - 1) * istride + (ln - 1) * tstride >= 2 ** 31:
+                raise NotImplementedError(f"reduction item for {dst_name} spans more than 2^31 "
+                                          "partials from its base (32-bit offsets in segment_sum)")
             self._items_rec.append((src_off + t0 * tstride, count, istride, tstride, ln,
                                     base + t0, accumulate, f64))
             t0 += ln

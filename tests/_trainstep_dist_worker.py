@@ -7,7 +7,9 @@ Every rank runs the product TrainStep (light_unet/train_step.py) on its half of 
   B  local mode, dropout 0: one eager step (the averaged flat gradient);
   C  dropout 0.1: the Dropout3d keep scales the forward drew for every (block, n, c).
 Rank r saves its arrays to <out>/rank<r>.npz.  Launched by torch.distributed.run (gloo, all
-ranks on cuda:0; RCCL on a node)."""
+ranks on cuda:0; RCCL on a node).  argv: <out> [encoder channels, e.g. 16,32,64,128] [f32 | bf16]
+[volume edge]: the network (BASELINE config 5: 32,64,128,256), the activation storage (config 3:
+bf16) and the patch size of the run."""
 import os
 import sys
 
@@ -33,14 +35,23 @@ def batches(n_steps, size=SIZE):
     return out
 
 
-def fresh_model(dev, dropout_p):
+def fresh_model(dev, dropout_p, enc=(16, 32, 64, 128)):
     from light_unet.models.unet3d import Lightweight3DUNet
     torch.manual_seed(42)
-    return Lightweight3DUNet(dropout_p=dropout_p).to(dev).train()
+    return Lightweight3DUNet(encoder_channels=list(enc), dropout_p=dropout_p).to(dev).train()
+
+
+def parse(argv):
+    """(encoder channels, activation dtype, volume edge) from the worker's argv[2:]"""
+    enc = tuple(int(c) for c in argv[0].split(",")) if len(argv) > 0 else (16, 32, 64, 128)
+    dt = torch.bfloat16 if len(argv) > 1 and argv[1] == "bf16" else torch.float32
+    size = int(argv[2]) if len(argv) > 2 else SIZE
+    return enc, dt, size
 
 
 def main():
     out = sys.argv[1]
+    enc, adt, size = parse(sys.argv[2:])
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = torch.device("cuda:0")
@@ -48,13 +59,13 @@ def main():
     from light_unet.train_step import TrainStep
     per = 4 // world
     sl = slice(rank * per, (rank + 1) * per)
-    bt = batches(2)
+    bt = batches(2, size)
     dx = [torch.from_numpy(x[sl].copy()).to(dev) for x, _ in bt]
     dt = [torch.from_numpy(t[sl].copy()).to(dev) for _, t in bt]
     res = {}
     # A: exact mode, eager step then graph replay
-    m = fresh_model(dev, 0.0)
-    ts = TrainStep(m, ftl_mode="exact")
+    m = fresh_model(dev, 0.0, enc)
+    ts = TrainStep(m, ftl_mode="exact", dtype=adt)
     loss = ts(dx[0], dt[0])
     torch.cuda.synchronize()
     res["A_loss1"] = np.float64(loss.item())
@@ -67,13 +78,14 @@ def main():
     res["A_loss2"] = np.float64(loss.item())
     res["A_p2"] = ts.flat.cpu().numpy().copy()
     # B: local mode (plain DDP averaging)
-    m = fresh_model(dev, 0.0)
-    ts = TrainStep(m, ftl_mode="local")
+    m = fresh_model(dev, 0.0, enc)
+    ts = TrainStep(m, ftl_mode="local", dtype=adt)
     ts(dx[0], dt[0])
     torch.cuda.synchronize()
     res["B_g1"] = ts.gflat.cpu().numpy().copy()
     # C: Dropout3d keep scales drawn by this rank's forward
-    m = fresh_model(dev, 0.1)
+    m = fresh_model(dev, 0.1, enc)
+    m.engine.set_act_dtype(adt)
     _, sv = m.engine.forward(m.flat_parameters(), dx[0], training=True, dropout_p=0.1,
                              counter=m._rng_counter, save=True)
     torch.cuda.synchronize()

@@ -560,7 +560,11 @@ def _stored(model, x):
     eng.set_act_dtype(BF)
     _, sv = eng.forward(model.flat_parameters(), x, training=True, dropout_p=0.0, save=True)
     torch.cuda.synchronize()
-    N = x.shape[0]
+    return _stored_sv(sv, x.shape[0])
+
+
+def _stored_sv(sv, N):
+    """_stored from a forward's saved state (the engine's own, or a TrainStep's)."""
     out = {}
     for pre, b in sv["blk"].items():
         d, h, w = b["dims"]
@@ -622,6 +626,75 @@ def test_bf16_model_vs_bf16_storage_oracle(cuda, golden, fname):
     print(f"bf16 {fname} vs bf16-storage oracle (forced): {len(st.pairs)} storage points, worst "
           f"mismatch fraction {worst:.1e}; out {oerr:.1e}, loss {l16:.7f} vs {lb.item():.7f}, "
           f"grad rel L2 {gerr:.1e}")
+    assert oerr <= 1e-5, oerr
+    assert abs(l16 - lb.item()) <= 1e-6 * abs(lb.item())
+    assert gerr <= 1e-3, gerr
+
+
+@pytest.mark.timeout(300)
+def test_bf16_trainstep_bs4_48_vs_bf16_storage_oracle(cuda):
+    """BASELINE config 3's step at the benchmarked shape: the product TrainStep(dtype=bf16) at
+    bs 4 x 48^3 (bench.py's `bf16` leg), eager and hipGraph-replayed, against the bf16-storage
+    oracle driven by the step's own stored tensors (the bounds of
+    test_bf16_model_vs_bf16_storage_oracle: every stored tensor within 1 bf16 ulp of the op on the
+    engine's inputs on >= 99.9% of its elements, output 1e-5, loss 1e-6 relative, whole-gradient
+    relative L2 1e-3); the replayed step equals the eager one bitwise."""
+    from oracle import bf16_oracle as B16
+    from oracle import unet_oracle as U
+    from light_unet.models.unet3d import Lightweight3DUNet
+    from light_unet.train_step import TrainStep
+    torch.manual_seed(42)
+    model = Lightweight3DUNet(dropout_p=0.0)
+    sd0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    rng = np.random.default_rng(42)
+    xh = torch.from_numpy(rng.random((4, 1, 48, 48, 48), dtype=np.float32))
+    th = torch.from_numpy((rng.random((4, 1, 48, 48, 48)) > 0.97).astype(np.float32))
+    x, t = xh.to(cuda), th.to(cuda)
+    m = model.to(cuda).train()
+    ts = TrainStep(m, dtype=BF)
+    p, sv, sums = ts._fwd(x, t)
+    torch.cuda.synchronize()
+    stored = _stored_sv(sv, 4)
+    ts._bwd(p, sv, t, sums)
+    torch.cuda.synchronize()
+    o16 = p.detach().cpu().numpy()
+    l16 = float(ts.loss.item())
+    gflat = ts.gflat.clone()
+    del p, sv, sums
+    # the replayed step
+    m2 = Lightweight3DUNet(dropout_p=0.0)
+    m2.load_state_dict(sd0)
+    tg = TrainStep(m2.to(cuda).train(), dtype=BF)
+    xs, tsb = x.clone(), t.clone()
+    tg.capture(xs, tsb)
+    assert float(tg.replay().item()) == l16
+    torch.cuda.synchronize()
+    assert torch.equal(tg.gflat, gflat) and torch.equal(tg.flat, ts.flat)
+    del tg, m2
+    g = gflat.cpu().double().numpy()
+    g16 = {k: g[o:o + n].reshape(shape) for k, (o, n, shape) in m.engine.offsets.items()}
+    sd = {k: v.double().requires_grad_(True) for k, v in sd0.items()}
+    st = B16.Storage(stored)
+    pb = B16.unet_forward(sd, xh.double(), st=st)
+    lb = U.focal_tversky(pb, th.double())
+    lb.backward()
+    assert set(st.pairs) == set(stored), set(stored) ^ set(st.pairs)
+    worst = 0.0
+    for k, (r, e) in st.pairs.items():
+        ulp = (r.to(BF).view(torch.int16).long() - e.to(BF).view(torch.int16).long()).abs()
+        near = (r - e).abs() <= 1e-6 * r.abs().max()
+        assert bool(((ulp <= 1) | near).all()), (k, int(ulp.max()))
+        frac = float((r != e).double().mean())
+        worst = max(worst, frac)
+        assert frac <= 1e-3, (k, frac)
+    oerr = float(np.abs(o16 - pb.detach().numpy()).max())
+    gb = {k: v.grad.numpy() for k, v in sd.items()}
+    num = sum(np.sum((g16[k] - gb[k]) ** 2) for k in gb)
+    den = sum(np.sum(gb[k] ** 2) for k in gb)
+    gerr = (num / den) ** 0.5
+    print(f"bf16 TrainStep bs 4 x 48^3 vs bf16-storage oracle (forced): {len(st.pairs)} storage "
+          f"points, worst mismatch fraction {worst:.1e}; out {oerr:.1e}, loss {l16:.7f} vs "
+          f"{lb.item():.7f}, grad rel L2 {gerr:.1e}")
     assert oerr <= 1e-5, oerr
     assert abs(l16 - lb.item()) <= 1e-6 * abs(lb.item())
     assert gerr <= 1e-3, gerr

@@ -77,7 +77,7 @@ def test_bf16_twins_mirror_fp32_entry_points():
 
 def test_host_queries_without_gpu():
     from light_unet import _native
-    assert _native.query("l3u_abi_version") == _native.ABI_VERSION == 4
+    assert _native.query("l3u_abi_version") == _native.ABI_VERSION == 5
     assert _native.query("l3u_dw3_nchunk", 4, 32, 48, 48, 48) == 30   # 3 z-slabs x 10 y-strips
     assert _native.query("l3u_dw3_nchunk", 4, 16, 48, 48, 48) == 40   # 12-plane slabs: 4 x 10
     assert _native.query("l3u_pw_bwd_supported", 16, 32, 48 ** 3) == 1
@@ -107,6 +107,29 @@ def test_host_queries_without_gpu():
     assert _native.query("l3u_dw3_nchunk", 4, 32, 24, 24, 24) == 18   # 6 z-slabs x 3 y-strips
     assert _native.query("l3u_dw3_nchunk", 4, 128, 6, 6, 6) == 1
     assert _native.query("l3u_pw_stat_nsb", 16, 16, 48 ** 3) == 432   # 256-voxel tiles
+
+
+def test_pw_bwd_chunk_invariant():
+    """The pointwise-backward voxel chunk and the partial counts agree, for every volume the
+    engine can see (csrc/pwconv.hip pw_chunk_ok): each chunk is ONE workgroup sweep -- a multiple
+    of 256 voxels (the K = 1 kernel's SCH / 4 threads are whole waves) and at most 512 (its
+    128-thread bound) -- and the partial count is N * ceil(S / chunk) for both the fused and the
+    weight-only forms.  Round 5's 192-voxel chunks broke the first condition (48-thread
+    workgroups) and gave NaN weight gradients; this fails before any GPU run would."""
+    from light_unet import _native
+    sizes = sorted({d * h * w for d in (3, 4, 5, 6, 8, 11, 12, 16, 24, 32, 40, 48, 64, 80, 128)
+                    for h, w in ((d, d), (44, 36), (80, 80), (6, 8))} | {4, 1020, 1024, 4092, 4096,
+                                                                        65532, 65536, 256 ** 3})
+    for S in sizes:
+        ch = _native.query("l3u_pw_bwd_chunk", S)
+        assert ch % 256 == 0 and 256 <= ch <= 512, (S, ch)
+        for N in (1, 4):
+            nsc = -(-S // ch)
+            assert _native.query("l3u_pw_bwd_weight_nparts", N, S) == N * nsc, (S, N)
+            if S % 4 == 0:
+                for J, K in ((16, 1), (16, 16), (32, 16), (16, 32), (32, 64)):
+                    assert _native.query("l3u_pw_bwd_nparts", N, J, K, S) == N * nsc, (S, J, K)
+    assert _native.query("l3u_pw_bwd_chunk", 0) == 0
 
 
 def test_no_cpu_fallback_in_product_package():

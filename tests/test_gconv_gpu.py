@@ -59,7 +59,11 @@ def pre_act(y, rec):
 # the first block / use_grouped=False, ragged volumes and partial voxel blocks
 SHAPES = [(2, 16, 16, 8, 7, 6, 9), (1, 1, 16, 1, 12, 10, 8), (2, 32, 16, 8, 24, 24, 24),
           (4, 128, 128, 8, 6, 6, 6), (1, 16, 16, 1, 8, 8, 8), (2, 8, 16, 4, 5, 5, 5),
-          (1, 16, 40, 1, 6, 6, 6), (1, 64, 64, 8, 12, 12, 12)]
+          (1, 16, 40, 1, 6, 6, 6), (1, 64, 64, 8, 12, 12, 12),
+          # W % 4 == 0 with more than 16 input channels per group: gconv3q_kernel's multi-stage
+          # weight path (a barrier + stage_w inside the k loop, the next channel's rows fetched
+          # across the stage boundary), LDS-staged (8^3) and global-row (24^3) forms
+          (1, 32, 32, 1, 8, 8, 8), (2, 64, 32, 2, 24, 24, 24)]
 
 
 @pytest.mark.parametrize("shape", SHAPES)

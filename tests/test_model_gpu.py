@@ -248,7 +248,15 @@ def test_full_size_batch_independence(cuda):
     assert (p4 - p1).abs().max().item() <= 1e-6
 
 
-def test_trainstep_data_parallel_two_ranks(cuda, tmp_path):
+# (encoder channels, activation storage, volume edge): the fp32 16 -> 128 network, BASELINE config
+# 3 (the same network with bf16 activation storage) and config 5's 32 -> 256 network (at 32^3 here:
+# the protocol, not the volume, is under test; the full 64^3 step is test_fullsize_gpu's)
+DP_CASES = [((16, 32, 64, 128), "f32", 32), ((16, 32, 64, 128), "bf16", 32),
+            ((32, 64, 128, 256), "f32", 32)]
+
+
+@pytest.mark.parametrize("enc,adt,size", DP_CASES)
+def test_trainstep_data_parallel_two_ranks(cuda, tmp_path, enc, adt, size):
     """The product data-parallel step (TrainStep: 3-segment graph with eager collectives, in-kernel
     FTL gradient from all-reduced sums) on 2 ranks x bs 2 (gloo here, both ranks on this GPU;
     RCCL on a node) against the single-process bs-4 step:
@@ -270,11 +278,13 @@ def test_trainstep_data_parallel_two_ranks(cuda, tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(root, "tests", "_trainstep_dist_worker.py"), str(tmp_path)]
+           os.path.join(root, "tests", "_trainstep_dist_worker.py"), str(tmp_path),
+           ",".join(map(str, enc)), adt, str(size)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     rk = [np.load(tmp_path / f"rank{i}.npz") for i in range(2)]
-    bt = W.batches(2)
+    bt = W.batches(2, size)
+    dtype = torch.bfloat16 if adt == "bf16" else torch.float32
     dx = [torch.from_numpy(x).to(cuda) for x, _ in bt]
     dt = [torch.from_numpy(t).to(cuda) for _, t in bt]
 
@@ -282,8 +292,8 @@ def test_trainstep_data_parallel_two_ranks(cuda, tmp_path):
         return float(np.linalg.norm(a.astype(np.float64) - b) / np.linalg.norm(b))
 
     # single process, bs 4: eager step, then a second eager step
-    m = W.fresh_model(cuda, 0.0)
-    ts = TrainStep(m)
+    m = W.fresh_model(cuda, 0.0, enc)
+    ts = TrainStep(m, dtype=dtype)
     p0 = ts.flat.cpu().numpy().astype(np.float64)
     l1 = ts(dx[0], dt[0]).item()
     g1 = ts.gflat.cpu().numpy().astype(np.float64)
@@ -305,15 +315,16 @@ def test_trainstep_data_parallel_two_ranks(cuda, tmp_path):
     # local mode: mean of the half-batch gradients
     gh = []
     for h in range(2):
-        mh = W.fresh_model(cuda, 0.0)
-        th = TrainStep(mh)
+        mh = W.fresh_model(cuda, 0.0, enc)
+        th = TrainStep(mh, dtype=dtype)
         th(dx[0][2 * h:2 * h + 2].contiguous(), dt[0][2 * h:2 * h + 2].contiguous())
         gh.append(th.gflat.cpu().numpy().astype(np.float64))
     gmean = 0.5 * (gh[0] + gh[1])
     for z in rk:
         assert rel(z["B_g1"], gmean) <= 1e-4, rel(z["B_g1"], gmean)
     # dropout masks: distinct per rank, rank 0 == single-process samples 0-1
-    ms = W.fresh_model(cuda, 0.1)
+    ms = W.fresh_model(cuda, 0.1, enc)
+    ms.engine.set_act_dtype(dtype)
     _, sv = ms.engine.forward(ms.flat_parameters(), dx[0], training=True, dropout_p=0.1,
                               counter=ms._rng_counter, save=True)
     differ = False
