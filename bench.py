@@ -317,6 +317,62 @@ def call_bytes(name, a):
         nw = (co if a[6] else 0) + (co if a[7] else 0)   # y1 / r not written when rank-1
         return ("dw", f"front (1ch dw{' + 2 rank-1 pw' if nw else ''}) [{N},1->{co},{d}x{h}x{w}]",
                 4 * N * S + e * N * S * (1 + nw + (1 if a[10] else 0)))
+    # ---- the InstanceNorm / block-tail family (norm.hip) and the out_conv + loss launches
+    if base == "l3u_norm_act_fwd":   # (y2, y2ns, rec2, src2, r, rns, rec_r, src_r, sc, out, ons, N, C, S)
+        N, C, S = a[11:14]
+        cr = 1 if a[5] < 0 else C     # rank-1 residual: one stored channel
+        return "norm", f"block tail fwd [{N},{C},{S}]", e * N * S * (2 * C + cr)
+    if base == "l3u_norm_act_pool_fwd":  # (..., out, ons, pooled, pns, idx, N, C, D, H, W)
+        N, C, D, H, W = a[14:19]
+        S = D * H * W
+        cr = 1 if a[5] < 0 else C
+        return ("norm", f"block tail fwd + maxpool [{N},{C},{D}x{H}x{W}]",
+                e * N * S * (2 * C + cr) + N * C * (S // 8) * (e + 1))
+    if base == "l3u_norm_act_bwd_reduce":  # (dout, dns, out, ons, y2, y2ns, rec2, r, rns, rec_r, part, N, C, S)
+        N, C, S = a[11:14]
+        cr = 1 if a[8] < 0 else C
+        return "norm", f"block tail bwd reduce [{N},{C},{S}]", N * S * (4 * C + e * (2 * C + cr))
+    if base == "l3u_norm_act_bwd_reduce_r1":  # (dz, dzns, dscale, out, ons, y2, y2ns, rec2, r, rns, rec_r, part, N, C, S)
+        N, C, S = a[12:15]
+        cr = 1 if a[9] < 0 else C
+        return "norm", f"block tail bwd reduce (rank-1 dout) [{N},{C},{S}]", N * S * (4 + e * (2 * C + cr))
+    if base == "l3u_norm_act_bwd_reduce_up":  # (dout, dns, dpool, dpns, idx, out, ons, y2, y2ns, rec2, r, rns, rec_r, part, N, C, D, H, W)
+        N, C, D, H, W = a[14:19]
+        S = D * H * W
+        cr = 1 if a[11] < 0 else C
+        return ("norm", f"block tail bwd reduce (+maxpool bwd) [{N},{C},{D}x{H}x{W}]",
+                N * S * (4 * C + e * (2 * C + cr)) + N * C * (S // 8) * 5)
+    if base in ("l3u_norm_act_bwd_apply", "l3u_norm_act_bwd"):  # (dout, dns, out, ons, y2, y2ns, rec2, r, rns, rec_r, part, dy2, dy2ns, dr, drns, N, C, S)
+        N, C, S = a[15:18]
+        return ("norm", f"block tail bwd{' (one launch)' if base == 'l3u_norm_act_bwd' else ' apply'} [{N},{C},{S}]",
+                N * S * C * (4 + 3 * e + 8))
+    if base == "l3u_norm_act_bwd_up":  # (dout, dns, dpool, dpns, idx, out, ons, y2, y2ns, rec2, r, rns, rec_r, part, dy2, dy2ns, dr, drns, N, C, D, H, W)
+        N, C, D, H, W = a[18:23]
+        S = D * H * W
+        return ("norm", f"block tail bwd (one launch, +maxpool bwd) [{N},{C},{D}x{H}x{W}]",
+                N * S * C * (4 + 3 * e + 8) + N * C * (S // 8) * 5)
+    if base == "l3u_in_bwd_apply":   # (dy, dyns, y, yns, rec, ip, np, dx, dxns, N, C, S)
+        N, C, S = a[9:12]
+        return "norm", f"IN bwd apply [{N},{C},{S}]", N * C * S * (8 + e)
+    if base == "l3u_maxpool2_fwd":   # (x, xns, y, yns, idx, N, C, D, H, W)
+        N, C, D, H, W = a[5:10]
+        S = D * H * W
+        return "norm", f"maxpool fwd [{N},{C},{D}x{H}x{W}]", N * C * (e * S + (S // 8) * (e + 1))
+    if base == "l3u_maxpool2_bwd":   # (dpool, dpns, idx, dskip, dskns, dlev, dlevns, N, C, D, H, W)
+        N, C, D, H, W = a[7:12]
+        S = D * H * W
+        return "norm", f"maxpool bwd [{N},{C},{D}x{H}x{W}]", N * C * (8 * S + (S // 8) * 5)
+    if base == "l3u_outconv_fwd":    # (h, hns, w, b, p, t, part, N, C, S)
+        N, C, S = a[7:10]
+        return "io", f"out_conv + sigmoid{' + FTL sums' if a[5] else ''} [{N},{C}->1,{S}]", \
+            N * S * (e * C + 4 + (4 if a[5] else 0))
+    if base in ("l3u_outconv_bwd", "l3u_outconv_bwd_dz", "l3u_outconv_bwd_ftl", "l3u_outconv_bwd_ftl_dz"):
+        N, C, S = a[16:19]          # (dp | p, p | t, t | fpart, ..., h(9), hns, w, dh, dhns, part, loss, N, C, S)
+        ftl = "ftl" in base or a[0] is None
+        dz = base.endswith("_dz")
+        rd = 4 * 2 if ftl else 4 * (2 if a[2] is None else 3)   # p, t (and dp)
+        return ("io", f"out_conv + sigmoid{' + FTL' if ftl else ''} bwd{' (rank-1 dz)' if dz else ''} [{N},{C}->1,{S}]",
+                N * S * (rd + e * C + (4 if dz else 4 * C)))
     return None
 
 
@@ -329,7 +385,7 @@ def family_rooflines(nat_call, calls):
         if r is not None and r[0] != "reduce":   # (re-running it would apply AdamW again)
             sel.append((name, args, r))
     ms = StepRecorder.time_calls(nat_call, [(n, a) for n, a, _ in sel])
-    fam = {"dw": [], "gemm": []}
+    fam = {"dw": [], "gemm": [], "norm": [], "io": []}
     for (name, _, (f, label, b)), t in zip(sel, ms):
         fam[f].append({"call": label, "us": round(1000 * t, 2), "bytes": int(b),
                        "achieved": round(b / (t * 1e-3) / 1e9, 1),
@@ -387,9 +443,11 @@ def instep_evidence(workload, launches):
            "tree_matches": same_tree,
            "step_kernel_us": rec["step_kernel_us"], "launches": rec["launches"],
            "under_10us": rec.get("under_10us")}
-    for fam in ("dw", "gemm", "reduce"):
+    for fam in ("dw", "gemm", "reduce", "norm", "io"):
         if fam in rec:
             out[fam] = {k: rec[fam][k] for k in ("launches", "bytes", "us", "achieved", "frac")}
+    if "coverage" in rec:
+        out["coverage"] = rec["coverage"]
     if "reduce" in rec and rec["reduce"]["calls"]:
         out["reduce"]["call"] = rec["reduce"]["calls"][0]["call"]
     out["dominant"] = max(rec["dw"]["calls"] + rec["gemm"]["calls"], key=lambda r: r["us"])
@@ -1066,6 +1124,9 @@ def main():
                 "depthwise": fams["dw"],
                 "gemm": dict(fams["gemm"], calls=sorted(fams["gemm"]["calls"], key=lambda r: -r["us"])[:5],
                              mfma=gemm_mfma_evidence()),
+                # the InstanceNorm / block-tail launches and the out_conv + loss launches
+                "norm": dict(fams["norm"], calls=sorted(fams["norm"]["calls"], key=lambda r: -r["us"])[:5]),
+                "io": fams["io"],
             },
         }
         if world == 1 and not args.no_cpu_baseline:

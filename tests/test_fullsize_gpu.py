@@ -42,7 +42,7 @@ def _oracle(sd, x, t, dtype):
     out = U.unet_forward(P, x.to(dtype))
     loss = U.focal_tversky(out, t.to(dtype))
     loss.backward()
-    return out.detach().double().numpy(), float(loss), {k: p.grad.double().numpy() for k, p in P.items()}
+    return out.detach().double().numpy(), float(loss.detach()), {k: p.grad.double().numpy() for k, p in P.items()}
 
 
 def _errs(g, ref):

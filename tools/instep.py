@@ -1,4 +1,5 @@
-"""In-step rooflines of the depthwise, GEMM and gradient-reduction families: the rocprofv3 kernel trace of the
+"""In-step rooflines of the depthwise, GEMM, gradient-reduction, InstanceNorm / block-tail ("norm") and
+out_conv + loss ("io") families: the rocprofv3 kernel trace of the
 graph-replayed training step (tools/profile.sh) aligned launch by launch with the C-ABI calls
 of the same step (bench.py --dump-calls: name, family, label, algorithmic bytes).
 
@@ -95,7 +96,7 @@ def main():
     for j, kname, us in align(ks, calls):
         k0, u0 = per_call.get(j, ("", 0.0))
         per_call[j] = (k0 + (" + " if k0 else "") + kname, u0 + us)
-    fam = {"dw": [], "gemm": [], "reduce": []}
+    fam = {"dw": [], "gemm": [], "reduce": [], "norm": [], "io": []}
     for j, c in enumerate(calls):
         if c["family"] is None:
             continue
@@ -117,6 +118,9 @@ def main():
         rec[f] = {"launches": len(rows), "bytes": tb, "us": round(tt * 1e6, 1),
                   "achieved": round(tb / tt / 1e9, 1), "frac": round(tb / tt / 1e9 / PEAK, 4),
                   "calls": rows}
+    # the share of the step's kernel time the families' byte models account for
+    cov = sum(rec[f]["us"] for f in fam if f in rec)
+    rec["coverage"] = {"family_us": round(cov, 1), "frac_of_step": round(cov / rec["step_kernel_us"], 4)}
     rec["under_10us"] = {"launches": sum(1 for _, u in ks if u < 10.0),
                          "us": round(sum(u for _, u in ks if u < 10.0), 1)}
     json.dump(rec, open(out_path, "w"), indent=1)
