@@ -176,11 +176,12 @@ L3U_DEV void seq_sum(const double* __restrict__ p, int n, double t[NV]) {
 #pragma unroll
   for (int v = 0; v < NV; ++v) t[v] = 0.0;
   for (int i0 = 0; i0 < n; i0 += 8) {
+    // clamped unconditional loads (a predicated load became a branch with a vmcnt(0) behind it)
     double a[8][NV];
 #pragma unroll
     for (int u = 0; u < 8; ++u)
 #pragma unroll
-      for (int v = 0; v < NV; ++v) a[u][v] = i0 + u < n ? p[(i0 + u) * NV + v] : 0.0;
+      for (int v = 0; v < NV; ++v) a[u][v] = p[min(i0 + u, n - 1) * NV + v];
 #pragma unroll
     for (int u = 0; u < 8; ++u)
       if (i0 + u < n) {
@@ -197,15 +198,31 @@ L3U_DEV unsigned long long splitmix64(unsigned long long z) {
   return z ^ (z >> 31);
 }
 
-// the record's per-channel inputs (affine parameters, Dropout3d step, rank-1 scale), loaded
-// BEFORE the partials so that both arrive in one memory round trip
+// A load from a workgroup-uniform address issued as a VECTOR load (global_load, counted by
+// vmcnt, in order).  A uniform load would otherwise be a scalar load (s_load), and scalar loads
+// complete out of order: every later use of ANY scalar load -- a kernel argument fetched lazily
+// inside a branch included -- then waits with lgkmcnt(0) for all of them.  In the small-level
+// IN consumers that chained the record's inputs (gamma / beta, then the Dropout3d step and rank-1
+// scale, then the kernel-argument base of the partials) into three extra memory round trips
+// before the partials were even requested (round 6 wave stamps, dwv_fwd at 6^3: partials in
+// registers 3.5 us after the wave began, the data 1.5 us).  The opaque zero (a VGPR the compiler
+// cannot prove uniform) makes the address per-lane.
+template <typename V>
+L3U_DEV V vld(const V* p) {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return p[z];
+}
+
+// the record's per-channel inputs (affine parameters, Dropout3d step, rank-1 scale), vector
+// loads issued with the partials so that all of them arrive in one memory round trip
 struct RecIn { float g, b, rk1; int st; };
 L3U_DEV RecIn record_inputs(const l3u_norm_src& s, int c) {
   RecIn q;
-  q.g = s.gamma ? s.gamma[c] : 1.f;
-  q.b = s.beta ? s.beta[c] : 0.f;
-  q.st = (s.drop_p > 0.f && s.step) ? *s.step : 0;
-  q.rk1 = s.rank1 ? s.rank1[c] : 0.f;
+  q.g = s.gamma ? vld(s.gamma + c) : 1.f;
+  q.b = s.beta ? vld(s.beta + c) : 0.f;
+  q.st = (s.drop_p > 0.f && s.step) ? vld(s.step) : 0;
+  q.rk1 = s.rank1 ? vld(s.rank1 + c) : 0.f;
   return q;
 }
 L3U_DEV void record_from(const l3u_norm_src& s, const RecIn& q, int n, int c, int C, float cn,
@@ -342,27 +359,38 @@ L3U_DEV void block_record(const l3u_norm_src& s, int n, int c, int C, bool store
 }
 
 // Two records at once (waves 0 and 1 merge in parallel), one barrier; sh8: 16 floats of LDS.
-L3U_DEV void block_record2(const l3u_norm_src& a, const l3u_norm_src& b, bool has_b, int n, int c,
-                           int C, bool store, float* sh8) {
+// field-wise selects: a reference picked at run time between the two by-value kernel arguments
+// made the compiler copy both to scratch in every thread (120 B of private memory per thread,
+// ~25 MB of HBM writes per 48^3 launch, profiles/r1i_pmc_step.json)
+L3U_DEV l3u_norm_src pick_src(const l3u_norm_src& a, const l3u_norm_src& b, bool q) {
+  l3u_norm_src s;
+  s.stat_part = q ? a.stat_part : b.stat_part;
+  s.nsb = q ? a.nsb : b.nsb;
+  s.layer = q ? a.layer : b.layer;
+  s.gamma = q ? a.gamma : b.gamma;
+  s.beta = q ? a.beta : b.beta;
+  s.drop_p = q ? a.drop_p : b.drop_p;
+  s.seed = q ? a.seed : b.seed;
+  s.step = q ? a.step : b.step;
+  s.rec_out = q ? a.rec_out : b.rec_out;
+  s.rank1 = q ? a.rank1 : b.rank1;
+  return s;
+}
+// split form: the merging waves request the records' loads (block_record2_pre) BEFORE the
+// caller's streamed loads -- vector loads complete in order, so records requested behind the
+// data could only be merged once the data had arrived -- and merge them after (block_record2_fin)
+L3U_DEV void block_record2_pre(const l3u_norm_src& a, const l3u_norm_src& b, bool has_b, int n,
+                               int c, int C, RecPre& rp) {
+  const int wv = threadIdx.x >> 6;
+  if (wv == 0 || (wv == 1 && has_b)) record_pre(pick_src(a, b, wv == 0), n, c, C, rp);
+}
+L3U_DEV void block_record2_fin(const l3u_norm_src& a, const l3u_norm_src& b, bool has_b, int n,
+                               int c, int C, bool store, float* sh8, RecPre& rp) {
   const int wv = threadIdx.x >> 6;
   if (wv == 0 || (wv == 1 && has_b)) {
-    // field-wise selects: a reference picked at run time between the two by-value kernel
-    // arguments made the compiler copy both to scratch in every thread (120 B of private
-    // memory per thread, ~25 MB of HBM writes per 48^3 launch, profiles/r1i_pmc_step.json)
-    const bool q = wv == 0;
-    l3u_norm_src s;
-    s.stat_part = q ? a.stat_part : b.stat_part;
-    s.nsb = q ? a.nsb : b.nsb;
-    s.layer = q ? a.layer : b.layer;
-    s.gamma = q ? a.gamma : b.gamma;
-    s.beta = q ? a.beta : b.beta;
-    s.drop_p = q ? a.drop_p : b.drop_p;
-    s.seed = q ? a.seed : b.seed;
-    s.step = q ? a.step : b.step;
-    s.rec_out = q ? a.rec_out : b.rec_out;
-    s.rank1 = q ? a.rank1 : b.rank1;
+    const l3u_norm_src s = pick_src(a, b, wv == 0);
     float r[kRec];
-    finalize_record(s, n, c, C, r);
+    record_finish(s, rp, n, c, C, r);
     if ((threadIdx.x & 63) == 0) {
 #pragma unroll
       for (int i = 0; i < kRec; ++i) sh8[wv * 8 + i] = r[i];
@@ -374,6 +402,12 @@ L3U_DEV void block_record2(const l3u_norm_src& a, const l3u_norm_src& b, bool ha
     }
   }
   __syncthreads();
+}
+L3U_DEV void block_record2(const l3u_norm_src& a, const l3u_norm_src& b, bool has_b, int n, int c,
+                           int C, bool store, float* sh8) {
+  RecPre rp;
+  block_record2_pre(a, b, has_b, n, c, C, rp);
+  block_record2_fin(a, b, has_b, n, c, C, store, sh8, rp);
 }
 
 // a / b for 0 <= a < 2^24, b > 0, with inv = 1.f / b: one float multiply and a correction step

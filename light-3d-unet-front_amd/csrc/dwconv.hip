@@ -1385,8 +1385,15 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int nc = blockIdx.x, c = nc % C, n = nc / C;
   const long long HW = (long long)H * W, S = D * HW, cofs = (long long)c * S;
+  // wave 0 requests the record's partials and inputs (vector loads, common.h vld) FIRST, then
+  // every thread its data, then the taps (scalar loads): one memory round trip for all of them,
+  // and the record merge needs only the loads ahead of the data (vector loads complete in order)
+  RecPre rp;
+  const bool mrg = (XF || EPI == 1) && has_src;
+  if (mrg && threadIdx.x < 64) record_pre(src, n, c, C, rp);
   float raw[kVR];
   v_fetch(raw, x + (long long)n * xns + cofs, D, H, W);
+  __builtin_amdgcn_sched_barrier(0);
   float wk[27];
 #pragma unroll
   for (int t = 0; t < 27; ++t) wk[t] = w[c * 27 + (FLIP ? 26 - t : t)];
@@ -1394,7 +1401,20 @@ __global__ __launch_bounds__(256) void dwv_fwd_kernel(
   if (XF || EPI == 1) {
     if (has_src) {   // (per-wave merges measured +0.2..0.4 us at 6^3: wave 0 merges, LDS broadcast)
       float* s8 = lds;
-      block_record(src, n, c, C, true, s8);
+      if (threadIdx.x < 64) {
+        float r[kRec];
+        record_finish(src, rp, n, c, C, r);
+        if (threadIdx.x == 0) {
+#pragma unroll
+          for (int i = 0; i < kRec; ++i) s8[i] = r[i];
+          if (src.rec_out) {
+            float* o = src.rec_out + (long long)nc * kRec;
+#pragma unroll
+            for (int i = 0; i < kRec; ++i) o[i] = r[i];
+          }
+        }
+      }
+      __syncthreads();
       mu = s8[0]; rstd = s8[1]; sc = s8[2]; sh = s8[3]; kk = s8[4];
       __syncthreads();
     } else {

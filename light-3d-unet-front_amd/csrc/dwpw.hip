@@ -141,6 +141,13 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
   const WMap wm = w_map(y0, rows, H, W, WQ, l);
   const int zlo = max(0, z0 - 1), zhi = min(D - 1, z1);
   auto zc = [&](int zz) { return (long long)min(max(zz, zlo), zhi) * HW; };
+  // the records' partial sums are requested before the planes (vector loads complete in order:
+  // the merge then waits for nothing behind them)
+  RecPre rpre[CPW];
+  if (XF && has_src) {
+#pragma unroll
+    for (int i = 0; i < CPW; ++i) record_pre(src, n, wv * CPW + i, K, rpre[i]);
+  }
   Stage<T> st[CPW][PD];
 #pragma unroll
   for (int i = 0; i < CPW; ++i) {
@@ -156,7 +163,7 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
       const int c = wv * CPW + i;
       if (has_src) {
         float rr[kRec];
-        finalize_record(src, n, c, K, rr);
+        record_finish(src, rpre[i], n, c, K, rr);
         mu[i] = rr[0]; sc[i] = rr[2]; sh[i] = rr[3]; rks[i] = rr[7];
         if (zb == 0 && yb == 0 && l == 0 && src.rec_out) {
           float* o = src.rec_out + ((long long)n * K + c) * kRec;

@@ -85,8 +85,12 @@ __global__ __launch_bounds__(256) void outconv_fwd_kernel(
   const int n = blockIdx.y;
   const T* hp = h + (long long)n * hns;
   float* pp = p + (long long)n * S;
-  const float bv = b[0];
   const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  // the targets are requested with the channels (one round trip for every operand; they were
+  // loaded after the probabilities' store)
+  f4 tv4 = {0.f, 0.f, 0.f, 0.f};
+  if (VEC && t != nullptr && i0 < S) tv4 = ldv4(t + (long long)n * S + i0);
+  const float bv = b[0];
   f4 z = {bv, bv, bv, bv};
   if (VEC) {
     // every channel's float4 requested before the first use (C <= 32; the runtime-C loop issued
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(256) void outconv_fwd_kernel(
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     if (i0 + q < S) {
-      const float tv = t[(long long)n * S + i0 + q];
+      const float tv = VEC ? tv4[q] : t[(long long)n * S + i0 + q];
       spt = fmaf(pv[q], tv, spt);
       sp += pv[q];
       st += tv;
@@ -162,19 +166,27 @@ L3U_DEV void ftl_lane_sums(const float* __restrict__ part, int nb, double& a, do
   a = b = c = 0.0;
   // 8 strided partials in flight per lane (one L2 round trip instead of eight), added in the same
   // i order; out-of-range slots add +0.0, which leaves a (never -0.0) unchanged: same bits
+  // (clamped unconditional loads, the out-of-range slots dropped by a select at the add: the
+  // predicated form `ok ? part[..] : 0` was compiled as a branch around each load with a
+  // vmcnt(0) behind it -- eight dependent round trips, behind the streamed operands of the
+  // out_conv backward)
   constexpr int B = 8;
   for (int i = l; i < nb; i += B * 64) {
     float va[B], vb[B], vc[B];
 #pragma unroll
     for (int u = 0; u < B; ++u) {
-      const int j = i + u * 64;
-      const bool ok = j < nb;
-      va[u] = ok ? part[j * 3] : 0.f;
-      vb[u] = ok ? part[j * 3 + 1] : 0.f;
-      vc[u] = ok ? part[j * 3 + 2] : 0.f;
+      const int j = min(i + u * 64, nb - 1);
+      va[u] = part[j * 3];
+      vb[u] = part[j * 3 + 1];
+      vc[u] = part[j * 3 + 2];
     }
 #pragma unroll
-    for (int u = 0; u < B; ++u) { a += va[u]; b += vb[u]; c += vc[u]; }
+    for (int u = 0; u < B; ++u) {
+      const bool ok = i + u * 64 < nb;
+      a += ok ? va[u] : 0.f;
+      b += ok ? vb[u] : 0.f;
+      c += ok ? vc[u] : 0.f;
+    }
   }
   a = wave_sum_d(a);
   b = wave_sum_d(b);
@@ -701,24 +713,39 @@ __global__ __launch_bounds__(256) void front_fwd_kernel(
   const bool act = i0 < S;
   const float* xp = x + (long long)n * xns;
   f4 xv = {0.f, 0.f, 0.f, 0.f}, zv = {0.f, 0.f, 0.f, 0.f};
+  // every operand requested in one round trip: the 9 neighbourhood rows (float4 + the two edge
+  // values) at clamped addresses without branches (a branch around each row's loads had the
+  // compiler wait for the previous row first: nine dependent round trips), rows outside the
+  // volume zeroed after the load; the taps (scalar loads) beside them.  Same fma order and
+  // values as before: a zeroed row adds +0 to the accumulator that started at +0.
+  const int ic = act ? i0 : 0;
+  const int xx = ic % W, t1 = ic / W, yy = t1 % H, zz = t1 / H;   // quad: xx .. xx+3, one row
+  f4 m9[9];
+  float l9[9], r9[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int zr = min(max(zz + k / 3 - 1, 0), D - 1), yr = min(max(yy + k % 3 - 1, 0), H - 1);
+    const float* row = xp + ((long long)zr * H + yr) * W;
+    m9[k] = *reinterpret_cast<const f4*>(row + xx);
+    l9[k] = row[max(xx - 1, 0)];
+    r9[k] = row[min(xx + 4, W - 1)];
+  }
+  xv = m9[4];
+  float wk[27];
+#pragma unroll
+  for (int t = 0; t < 27; ++t) wk[t] = wdw[t];
   if (act) {
-    xv = *reinterpret_cast<const f4*>(xp + i0);
-    const int xx = i0 % W, t1 = i0 / W, yy = t1 % H, zz = t1 / H;   // quad: xx .. xx+3, one row
 #pragma unroll
-    for (int dz = -1; dz <= 1; ++dz) {
-      if (zz + dz < 0 || zz + dz >= D) continue;
+    for (int k = 0; k < 9; ++k) {
+      const int dz = k / 3 - 1, dy = k % 3 - 1;
+      const bool in = zz + dz >= 0 && zz + dz < D && yy + dy >= 0 && yy + dy < H;
+      const f4 m = in ? m9[k] : f4{0.f, 0.f, 0.f, 0.f};
+      const float lft = in && xx > 0 ? l9[k] : 0.f, rgt = in && xx + 4 < W ? r9[k] : 0.f;
+      const float v[6] = {lft, m[0], m[1], m[2], m[3], rgt};
+      const float* w3 = wk + k * 3;
 #pragma unroll
-      for (int dy = -1; dy <= 1; ++dy) {
-        if (yy + dy < 0 || yy + dy >= H) continue;
-        const float* row = xp + ((long long)(zz + dz) * H + (yy + dy)) * W;
-        const f4 m = *reinterpret_cast<const f4*>(row + xx);
-        const float lft = xx > 0 ? row[xx - 1] : 0.f, rgt = xx + 4 < W ? row[xx + 4] : 0.f;
-        const float v[6] = {lft, m[0], m[1], m[2], m[3], rgt};
-        const float* wk = wdw + ((dz + 1) * 3 + (dy + 1)) * 3;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          zv[q] = fmaf(wk[0], v[q], fmaf(wk[1], v[q + 1], fmaf(wk[2], v[q + 2], zv[q])));
-      }
+      for (int q = 0; q < 4; ++q)
+        zv[q] = fmaf(w3[0], v[q], fmaf(w3[1], v[q + 1], fmaf(w3[2], v[q + 2], zv[q])));
     }
     stv4(z1 + (long long)n * S + i0, zv);
     if (xc) stv4(xc + (long long)n * S + i0, xv);

@@ -43,14 +43,16 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
   const T* yp = y2 + (long long)n * y2ns + (long long)c * S;
   const T* rp = r + (long long)n * (rk ? -rns : rns) + (rk ? 0ll : (long long)c * S);
   T* op = out + (long long)n * ons + (long long)c * S;
-  // the first tile is requested before the records are finalized (their partial-sum loads
-  // overlap it); every later tile one iteration ahead
+  // the records' partial sums are requested first, then the first tile (one round trip for both;
+  // the merge waits only for the loads ahead of the tile); every later tile one iteration ahead
   const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4, istep = gridDim.x * 1024;
+  RecPre rpre;   // the records' loads before the tile's (common.h block_record2_pre)
+  if (HAS_SRC) block_record2_pre(src2, srcr, shortcut != 0, n, c, C, rpre);
   f4 yv = {0.f, 0.f, 0.f, 0.f}, rv = yv;
   if (VEC && i0 < S) { yv = ldv4(yp + i0); rv = ldv4(rp + i0); }
   float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f, rks = 1.f;
   if (HAS_SRC) {
-    block_record2(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh);
+    block_record2_fin(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh, rpre);
     m2 = sh[0]; a2 = sh[2]; b2 = sh[3];
     if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; rks = sh[15]; }
   } else {
@@ -110,8 +112,8 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
     const int q = (int)(o % W4), t = (int)(o / W4), oy = t % Ho, oz = t / Ho;
     return ((long long)(2 * oz) * H + 2 * oy) * W + 4 * q;
   };
-  // the thread's first 2x2x4 block is requested before the records are finalized (the partial-
-  // sum loads overlap it); every later block one iteration ahead
+  // the records' partial sums are requested first, then the thread's first 2x2x4 block (one round
+  // trip for both); every later block one iteration ahead
   const long long o0 = blockIdx.x * 256ll + threadIdx.x, ostep = (long long)gridDim.x * 256;
   f4 yv[4], rv[4];
   auto fetch = [&](long long o) {
@@ -123,10 +125,12 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
       rv[j] = ldv4(rp + off);
     }
   };
+  RecPre rpre;   // the records' loads before the tile's (common.h block_record2_pre)
+  if (HAS_SRC) block_record2_pre(src2, srcr, shortcut != 0, n, c, C, rpre);
   if (o0 < Sp) fetch(o0);
   float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f, rks = 1.f;
   if (HAS_SRC) {
-    block_record2(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh);
+    block_record2_fin(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh, rpre);
     m2 = sh[0]; a2 = sh[2]; b2 = sh[3];
     if (shortcut) { mr = sh[8]; ar = sh[10]; br = sh[11]; rks = sh[15]; }
   } else {

@@ -688,7 +688,7 @@ struct TailSecond {
 };
 
 #ifndef L3U_PWBF_WAVES1
-#define L3U_PWBF_WAVES1 5
+#define L3U_PWBF_WAVES1 4
 #endif
 // minimum waves per SIMD asked of the 16-row forms with up to 32 columns (0: the compiler's
 // choice, 4 for the block-tail forms at 106-108 VGPRs)
@@ -704,18 +704,24 @@ constexpr int kPwbfPB = L3U_PWBF_PB;
 // VGPRs, no spill; the prologue forms spill 11-38 VGPRs at 4 waves)
 constexpr int kPwbfWaves2 = L3U_PWBF_WAVES2;
 #ifndef L3U_PWBF_WAVES1K1
-#define L3U_PWBF_WAVES1K1 6
+#define L3U_PWBF_WAVES1K1 5
 #endif
 // ... and of the 16-row, 16-column forms (80 VGPRs at 6 waves without a spill; the 32-column ones
 // spill 11-20 there)
 constexpr int kPwbfWaves1k1 = L3U_PWBF_WAVES1K1;
+#ifndef L3U_PWBF_WAVES3
+#define L3U_PWBF_WAVES3 3
+#endif
+// ... and of the 32-row forms with a prologue (0: the compiler's choice)
+constexpr int kPwbfWaves3 = L3U_PWBF_WAVES3;
 template <int NJ, int NK, int PRO>
 constexpr int pwbf_waves() {
   return NJ == 1 ? (NK == 1 && kPwbfWaves1k1 > 0 ? kPwbfWaves1k1
                                                  : (NK <= 2 && kPwbfWaves1 > 0 ? kPwbfWaves1 : 1))
-                 : (PRO == 0 && NK <= 2 && kPwbfWaves2 > 0 ? kPwbfWaves2 : 1);
+                 : (PRO == 0 && NK <= 2 && kPwbfWaves2 > 0 ? kPwbfWaves2
+                                                           : (PRO && kPwbfWaves3 > 0 ? kPwbfWaves3 : 1));
 }
-template <typename T, int NJ, int NK, int PRO, bool R1 = false, bool R1B = false>
+template <typename T, int NJ, int NK, int PRO, bool R1 = false, bool R1B = false, bool PL = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(pwbf_waves<NJ, NK, PRO>()))) void pw_bwd_fused_kernel(
     const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
@@ -758,32 +764,79 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(pwbf_waves<
   const T* xn = x + (long long)n * xns;
   float* dxn = dx + (long long)n * dxns;
 
-  // 1. every streamed load of the tile is issued first ...
+  // 0. the small per-workgroup operands are requested FIRST, into registers: the weight slice,
+  // (PRO) the first batch of the InstanceNorm-backward partials and the records.  Vector loads
+  // complete in order, so operands requested behind the streamed tile could only be consumed once
+  // the whole tile had arrived: the weight staging loop and the partial batch were two more
+  // dependent round trips, and the records a third behind the first barrier (round 6 ISA
+  // review).  Requested first, the partial sums, the barrier and the coefficients overlap the
+  // tile's flight.  Clamped unconditional loads (nthr >= 256: pw_chunk_ok), selected at use.
+  constexpr int PB = NJ == 1 && NK == 1 && kPwbfWaves1k1 >= 6 ? 2 : kPwbfPB;   // partials per batch
+  // (the 16-column forms at 6 waves per SIMD have no room for the early batch: 80 VGPRs, 8-10
+  // spilled; they request it behind the tile as before)
+  constexpr bool EP = PRO && !(NJ == 1 && NK == 1 && kPwbfWaves1k1 >= 6) && !PL;   // (PL: its pool loads)
+  constexpr int WPT = (TJ * WS + 255) / 256;
+  float wreg[WPT];
+#pragma unroll
+  for (int u = 0; u < WPT; ++u) {
+    const int i = min(tid + u * nthr, TJ * WS - 1), j = i / WS, kc = i - j * WS;
+    wreg[u] = w[(long long)min(j, J - 1) * K + min(k0 + kc, K - 1)];
+  }
+  const int pj = min(tid / PS, J - 1), psub = tid % PS;
+  const int pst = PRO == 2 ? 3 : 2, po1 = PRO == 2 ? sel : 1;
+  const double* pp = in_part + ((long long)pj * N + n) * npart * pst;
+  double pa0[EP ? PB : 1], pa1[EP ? PB : 1];
+  float q0 = 0.f, q1 = 0.f, q5 = 0.f, q7 = 0.f;
+  if constexpr (EP) {
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+      const int i = min(psub + u * PS, npart - 1);
+      pa0[u] = pp[i * pst];
+      pa1[u] = pp[i * pst + po1];
+    }
+  }
+  if constexpr (PRO) {
+    const float* q = rec + ((long long)n * J + min(tid, J - 1)) * kRec;
+    q0 = q[0]; q1 = q[1]; q5 = q[5]; q7 = q[7];
+  }
+
+  // rank-1 dout[j] = dscale[j] * dz (l3u_outconv_bwd_dz): the scales are small operands too
+  float dsv[PRO == 2 && !PL ? JR : 1];   // (never with the pool fold: encoder blocks)
+  if constexpr (PRO == 2 && !PL) {
+#pragma unroll
+    for (int jr = 0; jr < JR; ++jr) dsv[jr] = dscale != nullptr ? dscale[min(4 * jr + lk, J - 1)] : 1.f;
+  }
+
+  // 1. then every streamed load of the tile, unconditional at clamped addresses and zeroed after
+  // the load where it lies outside the tile: a branch around a load leaves the wait-count pass
+  // unsure how many loads follow the small operands, and it then waits for the whole tile before
+  // the coefficients
+  const bool sok = sd < s_hi;
+  const int sdc = sok ? sd : s_hi - 4;
+  const long long gst = (PRO == 2 && dscale != nullptr) ? 0ll : (long long)S;   // rank-1 dz: one row
   f4 g[JR], yv[PRO ? JR : 1], ov[PRO == 2 ? JR : 1];
+  // PL (PRO 2): + the next level's MaxPool3d backward (folded; a template flag so that the other
+  // forms carry no pool code), the pooled gradient and argmax loads unconditional as well
+  int pz = 0, py = 0, px = 0;
+  if constexpr (PL) {
+    const int HW = Hf * Wf;
+    pz = fdiv(sdc, HW, 1.f / HW);
+    const int rm = sdc - pz * HW;
+    py = fdiv(rm, Wf, 1.f / Wf);
+    px = rm - py * Wf;
+  }
 #pragma unroll
   for (int jr = 0; jr < JR; ++jr) {
-    const int j = 4 * jr + lk;
-    g[jr] = f4{0.f, 0.f, 0.f, 0.f};
-    if (j < J && sd < s_hi) {
-      if (PRO == 2 && dscale != nullptr)   // rank-1 dout[j] = dscale[j] * dz (l3u_outconv_bwd_dz)
-        g[jr] = dscale[j] * ldv4(dyn + sd);
-      else
-        g[jr] = ldv4(dyn + (long long)j * S + sd);
-      if (PRO == 2 && dpool != nullptr) {   // + the next level's MaxPool3d backward (folded)
-        const int HW = Hf * Wf, z = fdiv(sd, HW, 1.f / HW), rm = sd - z * HW, y = fdiv(rm, Wf, 1.f / Wf);
-        g[jr] = unpool_add(g[jr], dpool + (long long)n * dpns + (long long)j * (S / 8),
-                           pidx + ((long long)n * J + j) * (S / 8), z, y, rm - y * Wf, Hf, Wf);
-      }
-    }
+    const int jc = min(4 * jr + lk, J - 1);
+    g[jr] = ldv4(dyn + (long long)jc * gst + sdc);
+    if constexpr (PL)
+      g[jr] = unpool_add(g[jr], dpool + (long long)n * dpns + (long long)jc * (S / 8),
+                         pidx + ((long long)n * J + jc) * (S / 8), pz, py, px, Hf, Wf);
   }
   if (PRO == 2) {   // the block output (LeakyReLU mask of the tail)
     const T* on = oin + (long long)n * oins;
 #pragma unroll
-    for (int jr = 0; jr < JR; ++jr) {
-      const int j = 4 * jr + lk;
-      ov[jr] = f4{0.f, 0.f, 0.f, 0.f};
-      if (j < J && sd < s_hi) ov[jr] = ldv4(on + (long long)j * S + sd);
-    }
+    for (int jr = 0; jr < JR; ++jr) ov[jr] = ldv4(on + (long long)min(4 * jr + lk, J - 1) * S + sdc);
   }
   // R1 (yns < 0): a rank-1 normalised operand, channel j = rec[j][7] * one stored channel
   // (include/l3u.h); a template flag so that the other variants keep their registers.  R1B: only
@@ -792,11 +845,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(pwbf_waves<
   if (PRO) {
     const T* yn = yin + (long long)n * (yk ? -yns : yns);
 #pragma unroll
-    for (int jr = 0; jr < JR; ++jr) {
-      const int j = 4 * jr + lk;
-      yv[jr] = f4{0.f, 0.f, 0.f, 0.f};
-      if (j < J && sd < s_hi) yv[jr] = ldv4(yn + (yk ? 0ll : (long long)j * S) + sd);
-    }
+    for (int jr = 0; jr < JR; ++jr)
+      yv[jr] = ldv4(yn + (yk ? 0ll : (long long)min(4 * jr + lk, J - 1) * S) + sdc);
+  }
+#pragma unroll
+  for (int jr = 0; jr < JR; ++jr) {
+    const bool ok = 4 * jr + lk < J && sok;
+    if constexpr (PRO == 2 && !PL) g[jr] = dsv[jr] * g[jr];   // (dsv = 1 without dscale: exact)
+    const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+    g[jr] = ok ? g[jr] : z4;
+    if (PRO == 2) ov[jr] = ok ? ov[jr] : z4;
+    if (PRO) yv[jr] = ok ? yv[jr] : z4;
   }
   // X (the weight gradient's B operand): with a prologue (PRO 1 / 2) it is requested after dY is
   // formed, so that the dY / out / y registers are dead by then (TJ = 32, TK = 64: 226 -> 166
@@ -813,32 +872,36 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(pwbf_waves<
   };
   if constexpr (XL) load_xv();
 
-  // 2. ... then the small per-workgroup operands: the weight slice and (PRO) the per-channel
-  // InstanceNorm-backward coefficients, whose fp64 partial sums are spread over PS lanes per
-  // channel and combined in a fixed order
-  for (int i = tid; i < TJ * WS; i += nthr) {
-    const int j = i / WS, kc = i - j * WS, k = k0 + kc;
-    w_l[i] = (j < J && kc < TK && k < K) ? w[(long long)j * K + k] : 0.f;
+  // 2. the weight slice into LDS and (PRO) the per-channel InstanceNorm-backward coefficients,
+  // whose fp64 partial sums are spread over PS lanes per channel and combined in a fixed order
+#pragma unroll
+  for (int u = 0; u < WPT; ++u) {
+    const int i = tid + u * nthr, j = i / WS, kc = i - j * WS, k = k0 + kc;
+    if (i < TJ * WS) w_l[i] = (j < J && kc < TK && k < K) ? wreg[u] : 0.f;
   }
   if (PRO && tid < TJ * PS) {
-    const int j = tid / PS, sub = tid % PS;
+    const int j = tid / PS, sub = psub;
     double t0 = 0.0, t1 = 0.0;
     if (j < J) {
       // block-tail partials [J][N][npart][3]: {sum g, sum g*xhat2, sum g*xhat_r} (PRO 2), or the
       // depthwise backward's IN partials [J][N][npart][2] (PRO 1); a lane's share (i = sub,
-      // sub + PS, ..., up to 40 partials at 48^3) in batches of 8 clamped unconditional loads: one
-      // memory round trip per batch instead of one per partial (same order of the adds)
-      const int st = PRO == 2 ? 3 : 2, o1 = PRO == 2 ? sel : 1;
-      const double* pp = in_part + ((long long)j * N + n) * npart * st;
-      // (batches of 2 for the 16-column forms at 6 waves per SIMD: their 80-VGPR budget)
-      constexpr int PB = NJ == 1 && NK == 1 && kPwbfWaves1k1 >= 6 ? 2 : kPwbfPB;
-      for (int i0 = sub; i0 < npart; i0 += PB * PS) {
+      // sub + PS, ..., up to 40 partials at 48^3) in batches of PB clamped unconditional loads
+      // (the first batch requested above): one memory round trip per batch (same order of the adds)
+      if constexpr (EP) {
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {
+          const bool ok = sub + u * PS < npart;
+          t0 += ok ? pa0[u] : 0.0;
+          t1 += ok ? pa1[u] : 0.0;
+        }
+      }
+      for (int i0 = sub + (EP ? PB * PS : 0); i0 < npart; i0 += PB * PS) {
         double a0[PB], a1[PB];
 #pragma unroll
         for (int u = 0; u < PB; ++u) {
           const int i = min(i0 + u * PS, npart - 1);
-          a0[u] = pp[i * st];
-          a1[u] = pp[i * st + o1];
+          a0[u] = pp[i * pst];
+          a1[u] = pp[i * pst + po1];
         }
 #pragma unroll
         for (int u = 0; u < PB; ++u) {
@@ -857,13 +920,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(pwbf_waves<
     if (tid < J) {
       double t0 = 0.0, t1 = 0.0;
       for (int i = 0; i < PS; ++i) { t0 += psum[(tid * PS + i) * 2]; t1 += psum[(tid * PS + i) * 2 + 1]; }
-      const float* q = rec + ((long long)n * J + tid) * kRec;
-      o[0] = q[1] * q[5];          // f = rstd * gamma
+      o[0] = q1 * q5;              // f = rstd * gamma
       o[1] = (float)(t0 / S);      // M1
-      o[2] = q[0];                 // mu
-      o[3] = q[1];                 // rstd
+      o[2] = q0;                   // mu
+      o[3] = q1;                   // rstd
       o[4] = (float)(t1 / S);      // M2
-      o[5] = q[7];                 // rank-1 scale of the operand (yns < 0)
+      o[5] = q7;                   // rank-1 scale of the operand (yns < 0)
     } else {
       o[0] = o[1] = o[2] = o[3] = o[4] = o[5] = 0.f;
     }
@@ -1221,6 +1283,25 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
     const int j = jb + 4 * jr + lk, k = k0 + lr;
     wa[jr] = k < K ? (G ? w[(long long)k * J + j] : w[(long long)j * K + k]) : 0.f;
   }
+  // PRO: the InstanceNorm-backward partials (the first NPB of them) and the records are small
+  // operands as well, requested before the streamed tile: loads complete in order, so requested
+  // behind it they were a second dependent round trip (plus one per seq_sum batch, whose
+  // predicated loads each waited for everything in flight)
+  constexpr int NPB = 4;
+  const int pc = min(tid, J - 1);
+  const double* pp = PRO ? in_part + ((long long)pc * N + n) * npart * 2 : nullptr;
+  double pa[PRO ? NPB : 1][2];
+  float q0 = 0.f, q1 = 0.f, q5 = 0.f;
+  if constexpr (PRO != 0) {
+#pragma unroll
+    for (int u = 0; u < NPB; ++u) {
+      const int i = min(u, npart - 1);
+      pa[u][0] = pp[i * 2];
+      pa[u][1] = pp[i * 2 + 1];
+    }
+    const float* q = rec + ((long long)n * J + pc) * kRec;
+    q0 = q[0]; q1 = q[1]; q5 = q[5];
+  }
 
   for (int tile = t0; tile < t1; ++tile) {
     const int v0 = tile * 64;
@@ -1251,17 +1332,19 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
       xb[g] = load_x4<GV, false>(xn, k0 + lr, K, v0 + 16 * g + 4 * lk, S, S, 0, 0);
 
     if (PRO && tile == t0) {
-      // per-row InstanceNorm-backward coefficients (rows < J <= 128), requested after the first
-      // tile's streamed loads so that both arrive in one memory round trip
+      // per-row InstanceNorm-backward coefficients (rows < J <= 128); the partials summed in
+      // index order (seq_sum's order: same bits), the ones past NPB (none at 12^3 / 6^3) loaded here
       if (tid < J) {
-        double t[2];
-        seq_sum<2>(in_part + ((long long)tid * N + n) * npart * 2, npart, t);
-        const float* q = rec + ((long long)n * J + tid) * kRec;
+        double t[2] = {0.0, 0.0};
+#pragma unroll
+        for (int u = 0; u < NPB; ++u)
+          if (u < npart) { t[0] += pa[u][0]; t[1] += pa[u][1]; }
+        for (int i = NPB; i < npart; ++i) { t[0] += pp[i * 2]; t[1] += pp[i * 2 + 1]; }
         float* o = coef + tid * 8;
-        o[0] = q[1] * q[5];
+        o[0] = q1 * q5;
         o[1] = (float)(t[0] / S);
-        o[2] = q[0];
-        o[3] = q[1];
+        o[2] = q0;
+        o[3] = q1;
         o[4] = (float)(t[1] / S);
       }
       __syncthreads();
@@ -1844,9 +1927,10 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK)), block(64 * nwv);
   const size_t dlds = (size_t)max(nwv, 4) * 16 * kDyTileDS * sizeof(float);   // 16-row dY tiles
-#define PWBT0(A_, B_, R_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2, R_>), grid, block, dlds, stream, \
-      dout, dout_nstride, yr, yr_nstride, rec, tail_part, npart, x, x_nstride, w, dx, dx_nstride, \
+#define PWBT1(A_, B_, R_, P_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2, R_, false, P_>), grid, block, \
+      dlds, stream, dout, dout_nstride, yr, yr_nstride, rec, tail_part, npart, x, x_nstride, w, dx, dx_nstride, \
       accumulate, part, N, J, K, S, SCH, nsc, out, out_nstride, sel, dscale, dpool, dpns, pidx, Hf, Wf)
+#define PWBT0(A_, B_, R_) do { if (dpool) PWBT1(A_, B_, R_, true); else PWBT1(A_, B_, R_, false); } while (0)
 #define PWBT(A_, B_) PWBT0(A_, B_, false)
   // a rank-1 yr (the first block's shortcut, K = 1): its own variant
   L3U_REQUIRE(yr_nstride >= 0 || (NJ == 1 && NK == 1));
@@ -1859,6 +1943,7 @@ int pw_bwd_tail_impl(const float* dout, long long dout_nstride, const T* out, lo
   else PWBT(2, 4);
 #undef PWBT
 #undef PWBT0
+#undef PWBT1
   L3U_CHECK_LAUNCH();
 }
 
@@ -1890,10 +1975,11 @@ int pw_bwd_tail_pair_impl(const float* dout, long long dout_nstride, const float
   L3U_REQUIRE(nwv >= 1 && nwv <= 8 && SCH == 64 * nwv);
   dim3 grid(N * nsc, (K + 16 * NK - 1) / (16 * NK), 2), block(64 * nwv);
   const size_t dlds = (size_t)max(nwv, 4) * 16 * kDyTileDS * sizeof(float);   // 16-row dY tiles
-#define PWTP0(A_, B_, R_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2, false, R_>), grid, block, dlds, stream, \
-      dout, dout_nstride, a.yr, a.yrns, a.rec, tail_part, npart, a.x, a.xns, a.w, a.dx, a.dxns, \
+#define PWTP1(A_, B_, R_, P_) hipLaunchKernelGGL((pw_bwd_fused_kernel<T, A_, B_, 2, false, R_, P_>), grid, block, \
+      dlds, stream, dout, dout_nstride, a.yr, a.yrns, a.rec, tail_part, npart, a.x, a.xns, a.w, a.dx, a.dxns, \
       a.accumulate, a.part, N, J, a.K, S, SCH, nsc, out, out_nstride, a.sel, dscale, dpool, dpns, pidx, \
       Hf, Wf, b)
+#define PWTP0(A_, B_, R_) do { if (dpool) PWTP1(A_, B_, R_, true); else PWTP1(A_, B_, R_, false); } while (0)
 #define PWTP(A_, B_) PWTP0(A_, B_, false)
   // a rank-1 second operand (the first block's shortcut, K = 1, beside conv2's K = J <= 16)
   L3U_REQUIRE(b.yrns >= 0 || (NJ == 1 && NK == 1));
@@ -1906,6 +1992,7 @@ int pw_bwd_tail_pair_impl(const float* dout, long long dout_nstride, const float
   else PWTP(2, 4);
 #undef PWTP
 #undef PWTP0
+#undef PWTP1
   L3U_CHECK_LAUNCH();
 }
 
