@@ -1102,7 +1102,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(pwbf_waves<
 // through LDS for one output column.  A thread owns 4 voxels, a workgroup the pw_bwd_fused
 // chunk of SCH voxels (same partial layout part[chunk][J][1]); rows 16 at a time (J <= 32).  A
 // rank-1 y (yns < 0) is one stored channel, row j = rec[j][7] * it (the materialised values).
-template <typename T>
+template <typename T, bool YK>
 __global__ __launch_bounds__(128) void pw_bwd_k1_kernel(
     const float* __restrict__ dy, long long dyns, const T* __restrict__ yin, long long yns,
     const float* __restrict__ rec, const double* __restrict__ in_part, int npart,
@@ -1116,56 +1116,79 @@ __global__ __launch_bounds__(128) void pw_bwd_k1_kernel(
   const int sc = blockIdx.x % nsc, n = blockIdx.x / nsc;
   const int s = sc * SCH + 4 * tid;
   const bool ok = s < S && 4 * tid < SCH;
-  const bool yk = yns < 0;
+  const int sdc = ok ? s : S - 4;   // clamped address of the lanes past the chunk / volume
+  constexpr bool yk = YK;   // rank-1 y (yns < 0): a template flag, the other form keeps 16 y rows
   const float* dyn = dy + (long long)n * dyns;
   const T* yn = yin + (long long)n * (yk ? -yns : yns);
-  // the first 16 rows' streamed loads, then the coefficients (one memory round trip)
-  f4 g[16], yv[16];
+  // (0) the small operands first (vector loads complete in order: requested behind the tile they
+  // were two more dependent round trips, the partials with a wait behind every predicated load):
+  // 4 lanes per row take the row's IN-backward partials (PB per lane, clamped unconditional
+  // loads, added in index order; rows past 16 and partials past 4 * PB are loaded later), the
+  // lanes j < J the row's record and weight
+  constexpr int PB = 12;
+  const int sub = tid & 3, pr0 = min(tid >> 2, J - 1);
+  const double* pp0 = in_part + ((long long)pr0 * N + n) * npart * 2;
+  double2 pv[PB];
+#pragma unroll
+  for (int u = 0; u < PB; ++u) pv[u] = *reinterpret_cast<const double2*>(pp0 + min(sub + 4 * u, npart - 1) * 2);
+  const int jq = min(tid, J - 1);
+  const float* qr = rec + ((long long)n * J + jq) * kRec;
+  const float q0 = qr[0], q1 = qr[1], q5 = qr[5], q7 = qr[7], qw = w[jq];
+  // (1) the first 16 rows' streamed loads, unconditional at clamped addresses
+  f4 g[16], yv[yk ? 1 : 16];
   const f4 z4 = {0.f, 0.f, 0.f, 0.f};
   auto load_rows = [&](int j0) {
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) {
-      const int j = j0 + jj;
-      g[jj] = (j < J && ok) ? ldv4(dyn + (long long)j * S + s) : z4;
-      if (!yk) yv[jj] = (j < J && ok) ? ldv4(yn + (long long)j * S + s) : z4;
+      const int jc = min(j0 + jj, J - 1);
+      g[jj] = ldv4(dyn + (long long)jc * S + sdc);
+      if constexpr (!yk) yv[jj] = ldv4(yn + (long long)jc * S + sdc);
     }
-    if (yk) yv[0] = ok ? ldv4(yn + s) : z4;
+    if constexpr (yk) yv[0] = ldv4(yn + sdc);
   };
   load_rows(0);
-  const f4 xv = ok ? ldv4(x + (long long)n * xns + s) : z4;
-  // 4 lanes per row sum the IN-backward partials (16 loads per lane in flight at once, then added
-  // in index order), combined in lane order
+  const f4 xv = ldv4(x + (long long)n * xns + sdc);
+  // (2) the partial sums: 4 lanes per row, combined in lane order
   for (int jr = tid >> 2; jr < J; jr += blockDim.x >> 2) {
-    const int sub = tid & 3;
     double t0 = 0.0, t1 = 0.0;
     const double* pp = in_part + ((long long)jr * N + n) * npart * 2;
-    constexpr int PB = 16;
-    for (int i0 = sub; i0 < npart; i0 += 4 * PB) {
-      double2 v[PB];
+    int i0 = sub;
+    if (jr == tid >> 2) {   // the first pass: the batch requested in (0)
 #pragma unroll
       for (int u = 0; u < PB; ++u) {
-        const int i = i0 + 4 * u;
-        v[u] = i < npart ? *reinterpret_cast<const double2*>(pp + i * 2) : double2{0.0, 0.0};
+        const bool in = sub + 4 * u < npart;
+        t0 += in ? pv[u].x : 0.0;
+        t1 += in ? pv[u].y : 0.0;
       }
+      i0 = sub + 4 * PB;
+    }
+    for (; i0 < npart; i0 += 4 * PB) {
+      double2 v[PB];
 #pragma unroll
-      for (int u = 0; u < PB; ++u) { t0 += v[u].x; t1 += v[u].y; }
+      for (int u = 0; u < PB; ++u) v[u] = *reinterpret_cast<const double2*>(pp + min(i0 + 4 * u, npart - 1) * 2);
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const bool in = i0 + 4 * u < npart;
+        t0 += in ? v[u].x : 0.0;
+        t1 += in ? v[u].y : 0.0;
+      }
     }
     psum[(jr * 4 + sub) * 2] = t0;
     psum[(jr * 4 + sub) * 2 + 1] = t1;
   }
   __syncthreads();
-  for (int j = tid; j < J; j += blockDim.x) {
+  L3U_STAMP_MARK(0);
+  if (tid < J) {   // J <= 32 < blockDim.x
     double t0 = 0.0, t1 = 0.0;
-    for (int i = 0; i < 4; ++i) { t0 += psum[(j * 4 + i) * 2]; t1 += psum[(j * 4 + i) * 2 + 1]; }
-    const float* q = rec + ((long long)n * J + j) * kRec;
-    float* o = coef + j * 8;
-    o[0] = q[1] * q[5];          // f = rstd * gamma
+    for (int i = 0; i < 4; ++i) { t0 += psum[(tid * 4 + i) * 2]; t1 += psum[(tid * 4 + i) * 2 + 1]; }
+    float* o = coef + tid * 8;
+    o[0] = q1 * q5;              // f = rstd * gamma
     o[1] = (float)(t0 / S);      // M1
-    o[2] = q[0];                 // mu
-    o[3] = q[1];                 // rstd
+    o[2] = q0;                   // mu
+    o[3] = q1;                   // rstd
     o[4] = (float)(t1 / S);      // M2
-    o[5] = q[7];                 // rank-1 scale
-    o[6] = w[j];                 // W[j][0]
+    o[5] = q7;                   // rank-1 scale
+    o[6] = qw;                   // W[j][0]
   }
   __syncthreads();
   f4 dxa = z4;
@@ -1173,27 +1196,30 @@ __global__ __launch_bounds__(128) void pw_bwd_k1_kernel(
 #pragma unroll
   for (int j = 0; j < 32; ++j) pw[j] = 0.f;
   const f4 y1 = yv[0];
-  auto rows = [&](auto H) {   // rows 16 H .. 16 H + 15 (compile-time indices: registers)
+  // rows 16 H .. 16 H + 15 (compile-time indices: registers); rows j >= J contribute zeros (a
+  // select, no branch: the rows' arithmetic and the reductions below interleave)
+  auto rows = [&](auto H) {
     constexpr int h = decltype(H)::value;
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) {
       const int j = 16 * h + jj;
-      if (j < J) {   // uniform
-        const float* c = coef + j * 8;
-        const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
-        const f4 yj = yk ? mul_rn(y1, c[5]) : yv[jj];
-        f4 d;
+      const bool rok = ok && j < J;
+      const float* c = coef + min(j, J - 1) * 8;
+      const float f = c[0], M1 = c[1], mu = c[2], rs = c[3], M2 = c[4];
+      f4 yj;
+      if constexpr (yk) yj = mul_rn(y1, c[5]); else yj = yv[jj];
+      f4 d;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) d[q] = ok ? f * (g[jj][q] - M1 - (yj[q] - mu) * rs * M2) : 0.f;
-        const float wj = c[6];
+      for (int q = 0; q < 4; ++q) d[q] = rok ? f * (g[jj][q] - M1 - (yj[q] - mu) * rs * M2) : 0.f;
+      const float wj = c[6];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          dxa[q] = fmaf(wj, d[q], dxa[q]);
-          pw[j] = fmaf(d[q], xv[q], pw[j]);
-        }
+      for (int q = 0; q < 4; ++q) {
+        dxa[q] = fmaf(wj, d[q], dxa[q]);
+        pw[j] = fmaf(d[q], xv[q], pw[j]);
       }
     }
   };
+  L3U_STAMP_MARK(1);
   rows(std::integral_constant<int, 0>{});
   if (J > 16) {   // uniform
     load_rows(16);
@@ -1204,16 +1230,25 @@ __global__ __launch_bounds__(128) void pw_bwd_k1_kernel(
     if (accumulate) dxa += ldv4(dst);
     *reinterpret_cast<f4*>(dst) = dxa;
   }
-  // weight-gradient partial of the chunk: xor tree over the wave, then the waves in order
+  // weight-gradient partial of the chunk: xor tree over the wave, then the waves in order (the 16
+  // rows of a half reduced together: their shuffle chains interleave)
+  auto reduce_half = [&](auto H) {
+    constexpr int h = decltype(H)::value;
+    float v[16];
 #pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    if (j < J) {   // uniform
-      float v = pw[j];
+    for (int jj = 0; jj < 16; ++jj) v[jj] = pw[16 * h + jj];
 #pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (l == 0) wred[wave][j] = v;
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) v[jj] += __shfl_xor(v[jj], o, 64);
+    if (l == 0) {
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj)
+        if (16 * h + jj < J) wred[wave][16 * h + jj] = v[jj];
     }
-  }
+  };
+  reduce_half(std::integral_constant<int, 0>{});
+  if (J > 16) reduce_half(std::integral_constant<int, 1>{});
   __syncthreads();
   for (int j = tid; j < J; j += blockDim.x) {
     float v = wred[0][j];
@@ -2035,9 +2070,11 @@ int pw_bwd_impl(const float* dy, long long dy_nstride, const T* y, long long y_n
   // rank-1): the VALU kernel, same chunks and partial layout
   if (K == 1 && y != nullptr && SCH <= 512 && J <= 32) {
     L3U_REQUIRE(pw_chunk_ok(SCH));   // SCH / 4 threads: whole waves, <= the 128-thread bound
-    hipLaunchKernelGGL((pw_bwd_k1_kernel<T>), dim3(N * nsc), dim3(SCH / 4), 0, stream, dy, dy_nstride,
-                       y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride,
-                       accumulate, part, N, J, S, SCH, nsc);
+#define PK1(Y_) hipLaunchKernelGGL((pw_bwd_k1_kernel<T, Y_>), dim3(N * nsc), dim3(SCH / 4), 0, stream, dy, \
+      dy_nstride, y, y_nstride, rec, in_part, npart, x, x_nstride, w, dx, dx_nstride, accumulate, part, N, J, \
+      S, SCH, nsc)
+    if (y_nstride < 0) PK1(true); else PK1(false);
+#undef PK1
     L3U_CHECK_LAUNCH();
   }
   L3U_REQUIRE(y_nstride >= 0);   // a rank-1 y is K = 1 (above)
