@@ -424,17 +424,25 @@ L3U_DEV int fdiv(int a, int b, float inv) {
 // is v (the skip-connection gradient quad) plus dpool of the window's argmax (idx = 4dz + 2dy + dx
 // per pooled voxel, l3u_maxpool2_fwd's encoding) -- l3u_maxpool2_bwd's expression, bit for bit.
 // dpp / ipp: the (n, c) planes of dpool [Ho*Wo*Do] and idx; H, W: the fine level's plane.
+// Split form for kernels that request every operand before the first use: unpool_tap loads the
+// pooled gradient pair and its argmax code, unpool_apply adds them (same expression).
+struct UnpoolTap { f2_t g; int id; };
+L3U_DEV UnpoolTap unpool_tap(const float* __restrict__ dpp, const unsigned char* __restrict__ ipp,
+                             int z, int y, int x, int H, int W) {
+  const long long o2 = ((long long)(z >> 1) * (H >> 1) + (y >> 1)) * (W >> 1) + (x >> 1);
+  return {*reinterpret_cast<const f2_t*>(dpp + o2), reinterpret_cast<const unsigned short*>(ipp)[o2 >> 1]};
+}
+L3U_DEV f4_t unpool_apply(f4_t v, UnpoolTap t, int z, int y) {
+  const int i0 = t.id & 0xff, i1 = t.id >> 8, j = 2 * (z & 1) + (y & 1);
+  v[0] += i0 == 2 * j ? t.g.x : 0.f;
+  v[1] += i0 == 2 * j + 1 ? t.g.x : 0.f;
+  v[2] += i1 == 2 * j ? t.g.y : 0.f;
+  v[3] += i1 == 2 * j + 1 ? t.g.y : 0.f;
+  return v;
+}
 L3U_DEV f4_t unpool_add(f4_t v, const float* __restrict__ dpp, const unsigned char* __restrict__ ipp,
                         int z, int y, int x, int H, int W) {
-  const long long o2 = ((long long)(z >> 1) * (H >> 1) + (y >> 1)) * (W >> 1) + (x >> 1);
-  const f2_t g = *reinterpret_cast<const f2_t*>(dpp + o2);
-  const int id = reinterpret_cast<const unsigned short*>(ipp)[o2 >> 1], i0 = id & 0xff, i1 = id >> 8;
-  const int j = 2 * (z & 1) + (y & 1);
-  v[0] += i0 == 2 * j ? g.x : 0.f;
-  v[1] += i0 == 2 * j + 1 ? g.x : 0.f;
-  v[2] += i1 == 2 * j ? g.y : 0.f;
-  v[3] += i1 == 2 * j + 1 ? g.y : 0.f;
-  return v;
+  return unpool_apply(v, unpool_tap(dpp, ipp, z, y, x, H, W), z, y);
 }
 
 // XCD-aware block remap (guide §5.5 T1, bijective form): blocks that share halo planes / weight

@@ -357,7 +357,10 @@ size_t dp_lds(int K, int NB, int RB, int W) {
          (size_t)16 * 16 * 2 * sizeof(double) + (size_t)K * 27 * sizeof(float);
 }
 
-constexpr int kDwpwTz = 8;
+#ifndef L3U_DWPW_TZ
+#define L3U_DWPW_TZ 8
+#endif
+constexpr int kDwpwTz = L3U_DWPW_TZ;   // output planes per workgroup slab
 
 DPGeom dp_geom(int K, int Nout, int D, int H, int W, int sc) {
   DPGeom g{};

@@ -48,8 +48,10 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
   const int i0 = (blockIdx.x * 256 + threadIdx.x) * 4, istep = gridDim.x * 1024;
   RecPre rpre;   // the records' loads before the tile's (common.h block_record2_pre)
   if (HAS_SRC) block_record2_pre(src2, srcr, shortcut != 0, n, c, C, rpre);
+  // (requests clamped to the last tile instead of branched: a load behind a branch makes every
+  // later wait assume the worst about what is in flight)
   f4 yv = {0.f, 0.f, 0.f, 0.f}, rv = yv;
-  if (VEC && i0 < S) { yv = ldv4(yp + i0); rv = ldv4(rp + i0); }
+  if (VEC) { const int ic = min(i0, S - 4); yv = ldv4(yp + ic); rv = ldv4(rp + ic); }
   float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f, rks = 1.f;
   if (HAS_SRC) {
     block_record2_fin(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh, rpre);
@@ -68,8 +70,8 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
   }
   if (VEC) {
     for (int i = i0; i < S; i += istep) {
-      f4 yn = {0.f, 0.f, 0.f, 0.f}, rn = yn;
-      if (i + istep < S) { yn = ldv4(yp + i + istep); rn = ldv4(rp + i + istep); }
+      const int in_ = min(i + istep, S - 4);
+      const f4 yn = ldv4(yp + in_), rn = ldv4(rp + in_);
       if (rk) rv = mul_rn(rv, rks);
       f4 o;
 #pragma unroll
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
   const long long o0 = blockIdx.x * 256ll + threadIdx.x, ostep = (long long)gridDim.x * 256;
   f4 yv[4], rv[4];
   auto fetch = [&](long long o) {
-    const long long base = base_of(o < Sp ? o : 0);
+    const long long base = base_of(o < Sp ? o : Sp - 1);   // past the end: the last block (cached)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const long long off = base + ((long long)(j >> 1) * H + (j & 1)) * W;
@@ -127,7 +129,7 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
   };
   RecPre rpre;   // the records' loads before the tile's (common.h block_record2_pre)
   if (HAS_SRC) block_record2_pre(src2, srcr, shortcut != 0, n, c, C, rpre);
-  if (o0 < Sp) fetch(o0);
+  fetch(o0);   // clamped in fetch: no branch ahead of the loads
   float m2, a2, b2, ar = 1.f, br = 0.f, mr = 0.f, rks = 1.f;
   if (HAS_SRC) {
     block_record2_fin(src2, srcr, shortcut != 0, n, c, C, blockIdx.x == 0, sh, rpre);
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[j][e] = lrelu(fmaf(a2, yv[j][e] - m2, b2) + fmaf(ar, rv[j][e] - mr, br));
-    if (o + ostep < Sp) fetch(o + ostep);
+    fetch(o + ostep);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const long long off = base + ((long long)(j >> 1) * H + (j & 1)) * W;
@@ -181,8 +183,11 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
 }
 
 // partials per (c, n, block): [sum g, sum g*xhat2, sum g*xhat_r],  g = dout * lrelu'(out)
-constexpr int kNabrU = 2;
-template <typename T, bool VEC, bool RK = false>
+#ifndef L3U_NABR_U
+#define L3U_NABR_U 2
+#endif
+constexpr int kNabrU = L3U_NABR_U;   // grid-stride tiles in flight per thread
+template <typename T, bool VEC, bool RK = false, bool PL = false>
 __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     const float* __restrict__ dout, long long dns, const T* __restrict__ out, long long ons,
     const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
@@ -211,36 +216,52 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
   if (VEC) {
     // U grid-stride tiles per round: all their loads in flight before the first use, the sums
     // still taken tile by tile in index order (same bits as one tile per round)
+    // Branch-free requests: tail tiles clamped to the last in-range tile (loaded, not summed), the
+    // residual read from `out` when there is none, the pooled taps (PL) issued after the tiles; so
+    // no load waits on a branch join (guide §6: one vmcnt wait per round, not one per operand).
     constexpr int U = kNabrU;
     const int step = nb * 1024;
+    const T* rq = recr ? rp : op;
     for (int i0 = (blockIdx.x * 256 + threadIdx.x) * 4; i0 < S; i0 += U * step) {
       f4 ov[U], dv[U], yv[U], rv[U];
+      UnpoolTap pt[U];
+      int zz[U], yy[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * step;
-        ov[u] = dv[u] = yv[u] = rv[u] = f4{0.f, 0.f, 0.f, 0.f};
-        if (i < S) {
-          ov[u] = ldv4(op + i);
-          dv[u] = dscale ? dsc * ldv4(dp + i) : ldv4(dp + i);
-          if (dpool) {   // + the MaxPool3d backward of the next level (l3u_maxpool2_bwd folded in)
-            const int HW = H * W, z = fdiv(i, HW, 1.f / HW), rm = i - z * HW, y = fdiv(rm, W, 1.f / W);
-            dv[u] = unpool_add(dv[u], dpool + (long long)n * dpns + (long long)c * (S / 8),
-                               pidx + (long long)nc * (S / 8), z, y, rm - y * W, H, W);
-          }
-          yv[u] = ldv4(yp + i);
-          if (recr) rv[u] = rk ? mul_rn(ldv4(rp + i), rks) : ldv4(rp + i);
+        const int i = min(i0 + u * step, S - 4);
+        ov[u] = ldv4(op + i);
+        dv[u] = ldv4(dp + i);
+        yv[u] = ldv4(yp + i);
+        rv[u] = ldv4(rq + i);
+      }
+      if constexpr (PL) {   // + the MaxPool3d backward of the next level (l3u_maxpool2_bwd folded in)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = min(i0 + u * step, S - 4);
+          const int HW = H * W, z = fdiv(i, HW, 1.f / HW), rm = i - z * HW, y = fdiv(rm, W, 1.f / W);
+          zz[u] = z; yy[u] = y;
+          pt[u] = unpool_tap(dpool + (long long)n * dpns + (long long)c * (S / 8),
+                             pidx + (long long)nc * (S / 8), z, y, rm - y * W, H, W);
         }
+      }
+      __builtin_amdgcn_sched_barrier(0);   // every request above issued before the first use
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        dv[u] = dsc * dv[u];   // dsc = 1 without dscale: exact
+        if constexpr (PL) dv[u] = unpool_apply(dv[u], pt[u], zz[u], yy[u]);
+        if (rk) rv[u] = mul_rn(rv[u], rks);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (i0 + u * step < S) {
+        const bool in = u == 0 || i0 + u * step < S;   // a clamped tail tile: selected away, not branched
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float g = dv[u][q] * lrelu_d(ov[u][q]);
-            s0 += g;
-            s1 += (double)g * ((yv[u][q] - m2) * rs2);
-            if (recr) s2 += (double)g * ((rv[u][q] - mr) * rsr);
-          }
+        for (int q = 0; q < 4; ++q) {
+          const float g = dv[u][q] * lrelu_d(ov[u][q]);
+          const double t1 = (double)g * ((yv[u][q] - m2) * rs2);
+          const double t2 = (double)g * ((rv[u][q] - mr) * rsr);
+          s0 = in ? s0 + g : s0;
+          s1 = in ? s1 + t1 : s1;
+          if (recr) s2 = in ? s2 + t2 : s2;
         }
       }
     }
@@ -316,7 +337,7 @@ __global__ __launch_bounds__(256) void norm_act_bwd_apply_kernel(
 // the 12^3 / 6^3 levels, where a launch costs more than the work): the three plane sums are
 // workgroup sums held by every thread, stored as the single partial, then applied.  Same values,
 // bit for bit, as the reduce + apply pair (the apply's fixed-order merge of one partial is exact).
-template <typename T, bool VEC>
+template <typename T, bool VEC, bool PL = false>
 __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
     const float* __restrict__ dout, long long dns, const T* __restrict__ out, long long ons,
     const T* __restrict__ y2, long long y2ns, const float* __restrict__ rec2,
@@ -343,25 +364,36 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
   if (VEC && S <= NI * 1024) {
     // every tile requested at once, one load phase; the apply reuses the registers (same
     // per-thread order and expressions as the looped form below: same bits)
+    // (clamped, branch-free requests as in norm_act_bwd_reduce_kernel; the pooled taps last)
     f4 dv[NI], ov[NI], yv[NI], rv[NI];
+    UnpoolTap pt[NI];
+    int zz[NI], yy[NI];
+    const T* rq = recr ? rp : op;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
-      const int i = threadIdx.x * 4 + k * 1024;
-      dv[k] = ov[k] = yv[k] = rv[k] = f4{0.f, 0.f, 0.f, 0.f};
-      if (i < S) {
-        dv[k] = ldv4(dp + i);
-        if (dpool) {   // + the next level's MaxPool3d backward (l3u_maxpool2_bwd folded in)
-          const int HW = H * W, z = fdiv(i, HW, 1.f / HW), rm = i - z * HW, y = fdiv(rm, W, 1.f / W);
-          dv[k] = unpool_add(dv[k], dpool + (long long)n * dpns + (long long)c * (S / 8),
-                             pidx + (long long)nc * (S / 8), z, y, rm - y * W, H, W);
-        }
-        ov[k] = ldv4(op + i);
-        yv[k] = ldv4(yp + i);
-        if (recr) rv[k] = ldv4(rp + i);
+      const int i = min(threadIdx.x * 4 + k * 1024, S - 4);
+      dv[k] = ldv4(dp + i);
+      ov[k] = ldv4(op + i);
+      yv[k] = ldv4(yp + i);
+      rv[k] = ldv4(rq + i);
+    }
+    if (PL) {   // + the next level's MaxPool3d backward (l3u_maxpool2_bwd folded in)
+#pragma unroll
+      for (int k = 0; k < NI; ++k) {
+        const int i = min(threadIdx.x * 4 + k * 1024, S - 4);
+        const int HW = H * W, z = fdiv(i, HW, 1.f / HW), rm = i - z * HW, y = fdiv(rm, W, 1.f / W);
+        zz[k] = z; yy[k] = y;
+        pt[k] = unpool_tap(dpool + (long long)n * dpns + (long long)c * (S / 8),
+                           pidx + (long long)nc * (S / 8), z, y, rm - y * W, H, W);
       }
+#pragma unroll
+      for (int k = 0; k < NI; ++k) dv[k] = unpool_apply(dv[k], pt[k], zz[k], yy[k]);
     }
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
+      // (a branch, not a select as in the reduce: g recomputed in the apply below then contracts
+      // exactly as in norm_act_bwd_apply_kernel -- the two stay bit-identical; the loads above
+      // are used after the branch too, so they cannot sink into it)
       if (threadIdx.x * 4 + k * 1024 < S) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -494,12 +526,27 @@ __global__ __launch_bounds__(256) void in_bwd_apply_kernel(
 }
 
 constexpr int kElemPerBlock = 4096;
-constexpr int kElemMaxBlocks = 16;
+#ifndef L3U_ELEM_MAXB
+#define L3U_ELEM_MAXB 16
+#endif
+constexpr int kElemMaxBlocks = L3U_ELEM_MAXB;
 // workgroups per (n, c) plane of the elementwise IN kernels: few enough that the per-workgroup
 // record merge (in-kernel finalize) stays small next to the streaming work
 int elem_blocks(int S) {
   int b = (S + kElemPerBlock - 1) / kElemPerBlock;
   return b > kElemMaxBlocks ? kElemMaxBlocks : (b < 1 ? 1 : b);
+}
+
+// the forward block tails (no partials, so free to differ from elem_blocks): workgroups per plane
+#ifndef L3U_NAF_ELEMS
+#define L3U_NAF_ELEMS 4096
+#endif
+#ifndef L3U_NAF_MAXB
+#define L3U_NAF_MAXB 16
+#endif
+int fwd_blocks(int S) {
+  int b = (S + L3U_NAF_ELEMS - 1) / L3U_NAF_ELEMS;
+  return b > L3U_NAF_MAXB ? L3U_NAF_MAXB : (b < 1 ? 1 : b);
 }
 
 }  // namespace
@@ -531,7 +578,7 @@ int norm_act_fwd_impl(const T* y2, long long y2_nstride, const float* rec2,
   L3U_REQUIRE(src2 ? (!shortcut || src_r) : (rec2 && (!shortcut || rec_r)));
   const bool vec = S % 4 == 0 && y2_nstride % 4 == 0 && r_nstride % 4 == 0 && out_nstride % 4 == 0;
   L3U_REQUIRE(r_nstride >= 0 || (sizeof(T) == 4 && shortcut && vec));   // rank-1 r: fp32 Conv1x1 shortcut
-  dim3 grid(elem_blocks(S), N * C);
+  dim3 grid(fwd_blocks(S), N * C);
   const l3u_norm_src z{};
   const l3u_norm_src s2 = src2 ? *src2 : z, sr = src_r ? *src_r : z;
 #define NAF0(V_, S_, R_) hipLaunchKernelGGL((norm_act_fwd_kernel<T, V_, S_, R_>), grid, dim3(256), 0, stream, y2, \
@@ -561,7 +608,7 @@ int norm_act_pool_fwd_impl(const T* y2, long long y2_nstride, const float* rec2,
               ((uintptr_t)r & (4 * E - 1)) == 0 && ((uintptr_t)out & (4 * E - 1)) == 0 &&
               ((uintptr_t)pooled & (2 * E - 1)) == 0 && ((uintptr_t)idx & 1) == 0);
   const long long S = (long long)D * H * W;
-  dim3 grid(elem_blocks((int)S), N * C);
+  dim3 grid(fwd_blocks((int)S), N * C);
   const l3u_norm_src z{};
   const l3u_norm_src s2 = src2 ? *src2 : z, sr = src_r ? *src_r : z;
 #define NAP(S_, R_) hipLaunchKernelGGL((norm_act_pool_fwd_kernel<T, S_, R_>), grid, dim3(256), 0, stream, y2, \
@@ -590,10 +637,13 @@ int norm_act_bwd_reduce_impl(const float* dout, long long dout_nstride, const T*
                                    dpns % 2 == 0 && ((uintptr_t)dpool & 7) == 0));
   dim3 grid(elem_blocks(S), N * C);
   L3U_REQUIRE(r_nstride >= 0 || vec);
+#define NABR(RK_, PL_) hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true, RK_, PL_>), grid, dim3(256), 0, \
+      stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, \
+      dscale, dpool, dpns, pidx, H, W)
   if (r_nstride < 0) {
-    if constexpr (sizeof(T) == 4)
-      hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale, dpool, dpns, pidx, H, W);
-  } else if (vec) hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale, dpool, dpns, pidx, H, W);
+    if constexpr (sizeof(T) == 4) { if (dpool) NABR(true, true); else NABR(true, false); }
+  } else if (vec) { if (dpool) NABR(false, true); else NABR(false, false); }
+#undef NABR
   else hipLaunchKernelGGL((norm_act_bwd_reduce_kernel<T, false>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, N, C, S, dscale);
   L3U_CHECK_LAUNCH();
 }
@@ -635,7 +685,8 @@ int norm_act_bwd_impl(const float* dout, long long dout_nstride, const T* out,
                                    H % 2 == 0 && W % 4 == 0 && dpns % 2 == 0 &&
                                    ((uintptr_t)dpool & 7) == 0));
   dim3 grid(1, N * C);
-  if (vec) hipLaunchKernelGGL((norm_act_bwd_one_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S, dpool, dpns, pidx, H, W);
+  if (vec && dpool) hipLaunchKernelGGL((norm_act_bwd_one_kernel<T, true, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S, dpool, dpns, pidx, H, W);
+  else if (vec) hipLaunchKernelGGL((norm_act_bwd_one_kernel<T, true>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
   else hipLaunchKernelGGL((norm_act_bwd_one_kernel<T, false>), grid, dim3(256), 0, stream, dout, dout_nstride, out, out_nstride, y2, y2_nstride, rec2, r, r_nstride, rec_r, part, dy2, dy2_nstride, dr, dr_nstride, N, C, S);
   L3U_CHECK_LAUNCH();
 }

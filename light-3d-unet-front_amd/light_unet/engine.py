@@ -242,6 +242,7 @@ class UNetEngine:
         self.applied_update = False
         self._dry = False
         self._items_rec = None
+        self.seg_bytes = {}    # partial bytes per parameter of the last planned backward
         self.debug = None      # dict -> backward stashes each block's output-gradient view
         self.fwd_arena = _Arena()
         self.bwd_arena = _Arena()
@@ -321,6 +322,9 @@ class UNetEngine:
                                           "partials from its base (32-bit offsets in segment_sum)")
             self._items_rec.append((src_off + t0 * tstride, count, istride, tstride, ln,
                                     base + t0, accumulate, f64))
+            sb = getattr(self, "seg_bytes", None)   # partial bytes per parameter (tools/seg_bytes.py)
+            if sb is not None and getattr(self, "_dry", False):
+                sb[dst_name] = sb.get(dst_name, 0) + count * ln * (8 if f64 else 4)
             t0 += ln
 
     @staticmethod
@@ -707,6 +711,7 @@ class UNetEngine:
                 self._dry = True
                 self.bwd_arena.reset(None)
                 self._items_rec = []
+                self.seg_bytes = {}
                 try:
                     self._backward_impl(flat, gflat, sv, dp, need_dx, ftl)
                 finally:
