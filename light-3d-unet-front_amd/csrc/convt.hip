@@ -38,7 +38,7 @@ namespace {
 
 L3U_DEV f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
-template <typename T, int CO, int PB, int CIB, int NCS>
+template <typename T, int CO, int PB, int CIB, int NCS, bool PF = true>
 __global__ __launch_bounds__(256) void convt_bwd_tile_kernel(
     const float* __restrict__ dy, long long dyns, const T* __restrict__ x, long long xns,
     const float* __restrict__ w, float* __restrict__ dx, long long dxns, float* __restrict__ wpart,
@@ -173,11 +173,16 @@ __global__ __launch_bounds__(256) void convt_bwd_tile_kernel(
     for (int st = 0; st < NST; ++st) {
       store_stage(st);
       lds_barrier();
+#ifdef L3U_STAMP_CT
+      if (st == 0 && t == t_lo) L3U_STAMP_MARK(0);   // stamp variant: the first stage staged
+#endif
       if constexpr (NST > 1) __builtin_amdgcn_sched_barrier(0);   // keep the stages apart
       // the next stage's loads (and taps) are in flight during this stage's MFMAs
       if (st + 1 < NST) {
         load_stage(t, st + 1);
-      } else if (t + 1 < t_hi) {
+      } else if (PF && t + 1 < t_hi) {
+        // (PF = false: one tile per workgroup, no next tile; its staging registers are then free
+        // during the MFMAs, which lets the LDS operand reads run ahead instead of one at a time)
         load_stage(t + 1, 0);
       }
       if constexpr (NST > 1) load_w(wn, ((st + 1) % NST) * NCS);
@@ -196,6 +201,10 @@ __global__ __launch_bounds__(256) void convt_bwd_tile_kernel(
 #pragma unroll
           for (int ab = 0; ab < 4; ++ab) vn[ab] = sdy[((4 * (cq + 1) + lk) * 4 + ab) * RP + 16 * pbx + lr];
         }
+        // the reads above stay ahead of this quad's MFMAs (left to itself the scheduler issued each
+        // read right before its four MFMAs and waited for it: one LDS latency per read, at one
+        // wave per SIMD nothing hides it)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ab = 0; ab < 4; ++ab) {
           const float* wq = wr[NST > 1 ? cc : st * NCS + cc][q];
@@ -248,6 +257,9 @@ __global__ __launch_bounds__(256) void convt_bwd_tile_kernel(
       lds_barrier();   // sdy / sx are rewritten by the next stage
     }
   }
+#ifdef L3U_STAMP_CT
+  L3U_STAMP_MARK(1);   // stamp variant: every tile's MFMAs issued
+#endif
   // ---- weight-gradient partial of this workgroup: part[bx][ci][co*8 + 4a + 2b + c]
   float* o = wpart + (long long)bx * Ci * K;
 #pragma unroll
@@ -338,8 +350,9 @@ int convt_tile_launch(const float* dy, long long dy_nstride, const T* x, long lo
               ((uintptr_t)x & (4 * sizeof(T) - 1)) == 0 && dy_nstride % 4 == 0 && x_nstride % 4 == 0 &&
               dx_nstride % 2 == 0);
   dim3 grid(N * t.ntg, Ci / (16 * t.cib)), block(256);
-#define CTT(CO_, PB_, CIB_) hipLaunchKernelGGL((convt_bwd_tile_kernel<T, CO_, PB_, CIB_, (CO_ == 64 ? 1 : CO_ / 16)>), grid, block, 0, \
-    stream, dy, dy_nstride, x, x_nstride, w, dx, dx_nstride, wpart, bpart, Ci, D, H, W, t.ntile, t.ntg, t.tpb)
+#define CTT0(CO_, PB_, CIB_, PF_) hipLaunchKernelGGL((convt_bwd_tile_kernel<T, CO_, PB_, CIB_, (CO_ == 64 ? 1 : CO_ / 16), PF_>), \
+    grid, block, 0, stream, dy, dy_nstride, x, x_nstride, w, dx, dx_nstride, wpart, bpart, Ci, D, H, W, t.ntile, t.ntg, t.tpb)
+#define CTT(CO_, PB_, CIB_) do { if (t.tpb > 1) CTT0(CO_, PB_, CIB_, true); else CTT0(CO_, PB_, CIB_, false); } while (0)
   if (Co == 64) {
     CTT(64, 4, 1);
   } else if (Co == 16) {
@@ -348,6 +361,7 @@ int convt_tile_launch(const float* dy, long long dy_nstride, const T* x, long lo
     if (t.cib == 4) CTT(32, 1, 4); else if (t.cib == 2) CTT(32, 2, 2); else CTT(32, 4, 1);
   }
 #undef CTT
+#undef CTT0
   L3U_CHECK_LAUNCH();
 }
 

@@ -113,7 +113,10 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
   constexpr int K = 16 * CPW, NB = 2 + 2 * SC, NT = 4 * NC * (1 + SC);
   // register budget (1024 threads: <= 128 VGPRs): two channels per wave stage one plane ahead
   // and read their taps from LDS; one channel per wave stages two planes ahead, taps in SGPRs
-  constexpr int PD = CPW == 1 ? 2 : 1;
+#ifndef L3U_DWPW_PD
+#define L3U_DWPW_PD 2
+#endif
+  constexpr int PD = CPW == 1 ? L3U_DWPW_PD : 1;
   constexpr bool LTAP = CPW > 1;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int WQ = W >> 2, PP = (RB + 2) * W, HW = H * W, VP = 256;
@@ -207,6 +210,9 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
   f4 a0[CPW], a1[CPW], a2[CPW];
 #pragma unroll
   for (int i = 0; i < CPW; ++i) a0[i] = a1[i] = a2[i] = f4{0.f, 0.f, 0.f, 0.f};
+#ifdef L3U_STAMP_DWPW
+  L3U_STAMP_MARK(0);   // stamp variant: setup (taps, records, first planes requested) done
+#endif
 
   // (c) the channel GEMM on the MFMA of plane step tt's Z tile: Y (or R) tile of 16 channels x
   // 64 voxels.  It runs one plane step late, between the next step's barrier and its stencil, so
@@ -301,12 +307,12 @@ __global__ __launch_bounds__(1024) void dwpw_fwd_kernel(
     }
   };
 #pragma unroll
-  for (int t = 0; t < TZC + 2; t += PD) {
-#pragma unroll
-    for (int k = 0; k < PD; ++k) step(t + k, k);
-  }
+  for (int t = 0; t < TZC + 2; ++t) step(t, t % PD);   // fully unrolled: the ring slot is static
   __syncthreads();   // the last step's Z tile
   if (fin_at(TZC + 1)) gemm(TZC + 1);
+#ifdef L3U_STAMP_DWPW
+  L3U_STAMP_MARK(1);   // stamp variant: the plane march done
+#endif
 
   // ---- statistics partials: lanes of a row -> waves of the same (m, which) in g order
   if (mm) {

@@ -1519,30 +1519,48 @@ L3U_DEV void convt_dx_pair_body(int bx, int by, int bz,
 #pragma unroll
   for (int m = 0; m < NC; ++m) ae[m] = ao[m] = f4{0.f, 0.f, 0.f, 0.f};
   const int nq = (Co + 3) >> 2;
-  for (int cq = wave; cq < nq; cq += KW) {
-    const int co = 4 * cq + lk;
-    const bool cok = co < Co;
-    f4 v[4];
+  // UB co quads of the wave per batch with every load of the batch in flight before the first
+  // MFMA (one memory round trip per batch, not per co quad): clamped unconditional addresses, the
+  // out-of-range operands zeroed after the load (a predicated load makes hipcc branch around it and
+  // wait for everything in flight); the MFMAs in the same order as one quad at a time
+  constexpr int UB = 4;
+  for (int cq0 = wave; cq0 < nq; cq0 += UB * KW) {
+    f4 v[UB][4];
+    float wv[UB][NC][8];
 #pragma unroll
-    for (int ab = 0; ab < 4; ++ab)
-      v[ab] = (ok && cok) ? *reinterpret_cast<const f4*>(dyn + (long long)co * S8 + ro[ab])
-                          : f4{0.f, 0.f, 0.f, 0.f};
-    float wv[NC][8];
+    for (int u = 0; u < UB; ++u) {
+      const int co = min(4 * (cq0 + u * KW) + lk, Co - 1);
 #pragma unroll
-    for (int m = 0; m < NC; ++m) {
-      const int ci = ci0 + 16 * m + lr;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) wv[m][e] = (cok && ci < Ci) ? w[(long long)ci * Co * 8 + co * 8 + e] : 0.f;
-    }
-#pragma unroll
-    for (int ab = 0; ab < 4; ++ab)
+      for (int ab = 0; ab < 4; ++ab) v[u][ab] = *reinterpret_cast<const f4*>(dyn + (long long)co * S8 + ro[ab]);
 #pragma unroll
       for (int m = 0; m < NC; ++m) {
-        ae[m] = mfma4(wv[m][2 * ab], v[ab][0], ae[m]);
-        ae[m] = mfma4(wv[m][2 * ab + 1], v[ab][1], ae[m]);
-        ao[m] = mfma4(wv[m][2 * ab], v[ab][2], ao[m]);
-        ao[m] = mfma4(wv[m][2 * ab + 1], v[ab][3], ao[m]);
+        const int ci = min(ci0 + 16 * m + lr, Ci - 1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wv[u][m][e] = w[(long long)ci * Co * 8 + co * 8 + e];
       }
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int co = 4 * (cq0 + u * KW) + lk;
+      const bool cok = co < Co;
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab) v[u][ab] = (ok && cok) ? v[u][ab] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < NC; ++m) {
+        const bool wok = cok && ci0 + 16 * m + lr < Ci;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) wv[u][m][e] = wok ? wv[u][m][e] : 0.f;
+      }
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab)
+#pragma unroll
+        for (int m = 0; m < NC; ++m) {
+          ae[m] = mfma4(wv[u][m][2 * ab], v[u][ab][0], ae[m]);
+          ae[m] = mfma4(wv[u][m][2 * ab + 1], v[u][ab][1], ae[m]);
+          ao[m] = mfma4(wv[u][m][2 * ab], v[u][ab][2], ao[m]);
+          ao[m] = mfma4(wv[u][m][2 * ab + 1], v[u][ab][3], ao[m]);
+        }
+    }
   }
   if (KW > 1) {
 #pragma unroll
@@ -1621,35 +1639,43 @@ L3U_DEV void convt_dw_pair_body(int bx, int by,
   float bacc[NG];
 #pragma unroll
   for (int g = 0; g < NG; ++g) bacc[g] = 0.f;
-  for (int pb = p_lo + 4 * wave; pb < p_hi; pb += 16) {
-    const int p = pb + lk;
-    const bool ok = p < p_hi;
-    const int pc = ok ? p : p_lo;
-    const int xp = pc % WP, t = pc / WP, y = t % H, z = t / H;
-    const long long ro = ((long long)(2 * z + a_) * (2 * H) + (2 * y + b_)) * (2 * W) + 4 * xp;
-    const long long xo = ((long long)z * H + y) * W + 2 * xp;
-    f4 v[NG];
+  // UB voxel-pair steps per batch, every load of the batch in flight before the first MFMA (as in
+  // convt_dx_pair_body); steps past the chunk load clamped addresses and add zeros
+  constexpr int UB = NJ * NG <= 2 ? 8 : 4;
+  for (int pb0 = p_lo + 4 * wave; pb0 < p_hi; pb0 += UB * 16) {
+    f4 v[UB][NG];
+    f2_t xv[UB][NJ];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const int co = 4 * (g0 + g) + (lr >> 2);
-      v[g] = (ok && co < Co) ? *reinterpret_cast<const f4*>(dyn + (long long)co * S8 + ro)
-                             : f4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < UB; ++u) {
+      const int p = pb0 + 16 * u + lk;
+      const int pc = p < p_hi ? p : p_lo;
+      const int xp = pc % WP, t = pc / WP, y = t % H, z = t / H;
+      const long long ro = ((long long)(2 * z + a_) * (2 * H) + (2 * y + b_)) * (2 * W) + 4 * xp;
+      const long long xo = ((long long)z * H + y) * W + 2 * xp;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const int co = min(4 * (g0 + g) + (lr >> 2), Co - 1);
+        v[u][g] = *reinterpret_cast<const f4*>(dyn + (long long)co * S8 + ro);
+      }
+#pragma unroll
+      for (int m = 0; m < NJ; ++m) xv[u][m] = ldv2(xn + (long long)min(ci0 + 16 * m + lr, Ci - 1) * S + xo);
     }
-    f2_t xv[NJ];
 #pragma unroll
-    for (int m = 0; m < NJ; ++m) {
-      const int ci = ci0 + 16 * m + lr;
-      xv[m] = (ok && ci < Ci) ? ldv2(xn + (long long)ci * S + xo) : f2_t{0.f, 0.f};
-    }
+    for (int u = 0; u < UB; ++u) {
+      const bool ok = pb0 + 16 * u + lk < p_hi;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      bacc[g] += (v[g][0] + v[g][1]) + (v[g][2] + v[g][3]);
+      for (int g = 0; g < NG; ++g) {
+        const bool vok = ok && 4 * (g0 + g) + (lr >> 2) < Co;
+        const f4 vg = vok ? v[u][g] : f4{0.f, 0.f, 0.f, 0.f};
+        bacc[g] += (vg[0] + vg[1]) + (vg[2] + vg[3]);
 #pragma unroll
-      for (int m = 0; m < NJ; ++m) {
-        acc[m][g][0] = mfma4(xv[m][0], v[g][0], acc[m][g][0]);
-        acc[m][g][1] = mfma4(xv[m][0], v[g][1], acc[m][g][1]);
-        acc[m][g][0] = mfma4(xv[m][1], v[g][2], acc[m][g][0]);
-        acc[m][g][1] = mfma4(xv[m][1], v[g][3], acc[m][g][1]);
+        for (int m = 0; m < NJ; ++m) {
+          const f2_t xm = (ok && ci0 + 16 * m + lr < Ci) ? xv[u][m] : f2_t{0.f, 0.f};
+          acc[m][g][0] = mfma4(xm[0], vg[0], acc[m][g][0]);
+          acc[m][g][1] = mfma4(xm[0], vg[1], acc[m][g][1]);
+          acc[m][g][0] = mfma4(xm[1], vg[2], acc[m][g][0]);
+          acc[m][g][1] = mfma4(xm[1], vg[3], acc[m][g][1]);
+        }
       }
     }
   }
