@@ -1322,7 +1322,7 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
   // operands as well, requested before the streamed tile: loads complete in order, so requested
   // behind it they were a second dependent round trip (plus one per seq_sum batch, whose
   // predicated loads each waited for everything in flight)
-  constexpr int NPB = 4;
+  constexpr int NPB = JT == 1 ? 8 : 4;   // the 12^3 IN-fused depthwise backward leaves 6 per (n, c)
   const int pc = min(tid, J - 1);
   const double* pp = PRO ? in_part + ((long long)pc * N + n) * npart * 2 : nullptr;
   double pa[PRO ? NPB : 1][2];
@@ -1368,7 +1368,8 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
 
     if (PRO && tile == t0) {
       // per-row InstanceNorm-backward coefficients (rows < J <= 128); the partials summed in
-      // index order (seq_sum's order: same bits), the ones past NPB (none at 12^3 / 6^3) loaded here
+      // index order (seq_sum's order: same bits), the ones past NPB (none at 12^3 / 6^3: a loop
+      // of dependent loads otherwise) loaded here
       if (tid < J) {
         double t[2] = {0.0, 0.0};
 #pragma unroll
