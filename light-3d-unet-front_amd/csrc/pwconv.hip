@@ -1345,6 +1345,11 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
     // X in the B layout (rows k0 + lr)
     f4 gd[JT * 4], ga[JT][4], yd[PRO ? JT * 4 : 1], ya[PRO ? JT : 1][4], xb[4];
     const int vd = v0 + 4 * lr;
+    // accumulate: the dX values this lane adds to in the epilogue (waves 0..3: k0 + 4lk + wave),
+    // requested first (requested in the epilogue they were one more dependent round trip)
+    f4 dprev = {0.f, 0.f, 0.f, 0.f};
+    if (GV && accumulate)
+      dprev = ldv4(dx + (long long)n * dxns + (long long)min(k0 + 4 * lk + (wave & 3), K - 1) * S + min(vd, S - 4));
 #pragma unroll
     for (int jr = 0; jr < JT * 4; ++jr) gd[jr] = load_x4<GV, G>(dyn, jb + 4 * jr + lk, J, vd, S, S, Hq, Wq);
 #pragma unroll
@@ -1462,7 +1467,7 @@ __global__ __launch_bounds__(64 * NWV) void pw_bwd_wide_kernel(
         float* dst = dx + (long long)n * dxns + (long long)k * S + vd;
         if (GV) {
           if (vd < S) {
-            if (accumulate) v += ldv4(dst);
+            if (accumulate) v += dprev;
             stv4(dst, v);
           }
         } else {
