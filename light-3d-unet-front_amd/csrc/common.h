@@ -214,6 +214,21 @@ L3U_DEV V vld(const V* p) {
   return p[z];
 }
 
+// Kernel arguments all requested at the kernel's entry, in one batch of scalar loads with one
+// wait.  Left alone, hipcc loads each argument where it is first used: behind a uniform branch (a
+// paired launch's second problem, an optional operand) that is a scalar-load round trip, then a
+// wait, then the next batch -- up to four dependent round trips before the first vector load of
+// the pointwise GEMMs (ISA: s_load ... s_waitcnt lgkmcnt(0) pairs ahead of the first
+// global_load).  An empty asm that takes every argument in SGPRs makes them all live at entry.
+// Measured per kernel family (A/B): kept for the pointwise forwards (-3 us/step) and
+// the block tails (-2.5 us); the pointwise backwards, out_conv / front / reduction launches and
+// the ConvTranspose3d backward got slower or stayed equal (higher register counts), and the
+// stencil kernels spilled.
+template <typename A>
+L3U_DEV void karg_pin(const A& a) { asm volatile("" ::"s"(a)); }
+template <typename... A>
+L3U_DEV void kargs_now(const A&... a) { (karg_pin(a), ...); }
+
 // the record's per-channel inputs (affine parameters, Dropout3d step, rank-1 scale), vector
 // loads issued with the partials so that all of them arrive in one memory round trip
 struct RecIn { float g, b, rk1; int st; };

@@ -36,6 +36,7 @@ __global__ __launch_bounds__(256) void norm_act_fwd_kernel(
     const T* __restrict__ r, long long rns, const float* __restrict__ recr, l3u_norm_src srcr,
     int shortcut, T* __restrict__ out, long long ons, int C, int S) {
   L3U_STAMP_SCOPE(302);
+  kargs_now(y2, y2ns, rec2, r, rns, recr, shortcut, out, ons, C, S);
   __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   // RK (rns < 0): rank-1 residual, record_r[7] * one stored channel (include/l3u.h)
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(256) void norm_act_pool_fwd_kernel(
     int shortcut, T* __restrict__ out, long long ons, T* __restrict__ pooled,
     long long pns, unsigned char* __restrict__ idx, int C, int D, int H, int W) {
   L3U_STAMP_SCOPE(303);
+  kargs_now(y2, y2ns, rec2, r, rns, recr, shortcut, out, ons, pooled, pns, idx, C, D, H, W);
   __shared__ float sh[16];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   const long long S = (long long)D * H * W;
@@ -196,6 +198,8 @@ __global__ __launch_bounds__(256) void norm_act_bwd_reduce_kernel(
     const float* __restrict__ dpool = nullptr, long long dpns = 0,
     const unsigned char* __restrict__ pidx = nullptr, int H = 0, int W = 0) {
   L3U_STAMP_SCOPE(304);
+  kargs_now(dout, dns, out, ons, y2, y2ns, rec2, r, rns, recr, part, N, C, S, dscale, dpool, dpns,
+            pidx, H, W);
   __shared__ double red[4];
   const int nc = blockIdx.y, c = nc % C, n = nc / C, nb = gridDim.x;
   const float m2 = rec2[(long long)nc * kRec + 0], rs2 = rec2[(long long)nc * kRec + 1];
@@ -346,6 +350,8 @@ __global__ __launch_bounds__(256) void norm_act_bwd_one_kernel(
     long long drns, int N, int C, int S, const float* __restrict__ dpool = nullptr,
     long long dpns = 0, const unsigned char* __restrict__ pidx = nullptr, int H = 0, int W = 0) {
   L3U_STAMP_SCOPE(306);
+  kargs_now(dout, dns, out, ons, y2, y2ns, rec2, r, rns, recr, part, dy2, dy2ns, dr, drns, N, C, S,
+            dpool, dpns, pidx, H, W);
   __shared__ double red[4];
   const int nc = blockIdx.y, c = nc % C, n = nc / C;
   const float* q2 = rec2 + (long long)nc * kRec;

@@ -111,6 +111,8 @@ __global__ __launch_bounds__(256) void pw_fwd_kernel(
     T* __restrict__ y2 = nullptr, long long yns2 = 0, float* __restrict__ stat2 = nullptr,
     int N1 = 0) {
   L3U_STAMP_SCOPE(101);
+  kargs_now(x, xns, w, wl, bias, y, yns, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq, x2, xns2,
+            w2, y2, yns2, stat2, N1);
   constexpr int CO_BLK = 16 * NC;
   constexpr int TSB = 256 * NSW;
   constexpr int WS = (CO_BLK % 32 == 16) ? CO_BLK : CO_BLK + 16;
@@ -319,6 +321,8 @@ __global__ __launch_bounds__(256) void pw_fwd_ks_kernel(
     T* __restrict__ y2 = nullptr, long long yns2 = 0, float* __restrict__ stat2 = nullptr,
     int N1 = 0) {
   L3U_STAMP_SCOPE(102);
+  kargs_now(x, xns, w, wl, bias, y, yns, accumulate, stat_part, K, Nout, S, nsb, Dq, Hq, Wq, x2, xns2,
+            w2, y2, yns2, stat2, N1);
   constexpr int CO_BLK = 16 * NC;
   constexpr int NT = NC * 16;   // accumulator floats per lane
   extern __shared__ __attribute__((aligned(16))) float lds[];   // [4 waves][NT][64 lanes]
@@ -467,6 +471,8 @@ __global__ __launch_bounds__(64) void pw_fwd_w1_kernel(
     const T* __restrict__ x2, long long xns2, const float* __restrict__ w2, T* __restrict__ y2,
     long long yns2, float* __restrict__ stat2, int N1) {
   L3U_STAMP_SCOPE(110);
+  kargs_now(x, xns, w, wl, bias, y, yns, accumulate, stat_part, K, Nout, S, nsb, x2, xns2, w2, y2,
+            yns2, stat2, N1);
   const int l = threadIdx.x, lr = l & 15, lk = l >> 4;
   const int sb = blockIdx.x, co0 = blockIdx.y * 16 * NC;
   int n = blockIdx.z;
